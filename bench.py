@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""bench.py — batched cartpole++ env-steps/sec on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[2] / SURVEY.md §8d C3, per GPU): 65,536 envs, discrete
+5-action random policy (int8 actions pre-generated in HBM), action_repeats R = 3,
+steps_per_repeat 1, initial_force 55, max_episode_len 200 with in-kernel autoreset,
+fp32.  A "step" is one env-step of every env: one cp_step call = one fused R-substep
+kernel launch + one compacted reset launch.  Envs shard across ranks (seed 1234+rank,
+global env ids offset rank*B); the only collective is an RCCL all-gather of the
+episode returns once per 200-step window (C4).  value = N*B*K / max-over-ranks wall.
+
+roofline: the step kernel's algorithmic HBM bytes per launch over
+its average duration from HIP events recorded on its launch stream in the timed region.
+cpu_baseline: the CPU oracle (a port: same algorithm, gcc -O2, OpenMP) on a bounded
+sample of the same workload, rank 0 at N = 1 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from cartpoleplusplus_amd.batched import BatchedCartpole  # noqa: E402
+
+METRIC = "env-steps/sec at batch=65,536, 1→8 MI355X; max |pose−pybullet| over 200 steps"
+HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s spec, 6.29 measured)
+WINDOW = 200            # episode-return reporting window (steps)
+
+
+def step_kernel_bytes(R, action_bytes):
+    """Algorithmic HBM bytes one env moves in one step-kernel launch."""
+    state_read = 52 + 6 + 2            # 4 bodies x 13, 2 pending forces x 3, steps, done
+    state_write = 52 + 6 + 1           # bodies, pending forces, steps
+    warm_cache = 2 * (10 + 40)         # warm-start ids + impulses, read + write once per step
+    return 4 * (state_read + state_write + warm_cache) + action_bytes + 4 * 14 * R + 4 + 1 + 8
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(R, budget_s):
+    """Oracle (port) on the host: same workload on a bounded env sample."""
+    import numpy as np
+
+    from cartpoleplusplus_amd import abi
+    from oracle import oracle as O
+    O.build()
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+
+    def run(B, steps):
+        cfg = O.default_config(num_envs=B, action_repeats=R, initial_force=55.0, seed=1234, autoreset=1)
+        e = O.Envs(cfg)
+        e.reset()
+        rng = np.random.default_rng(1234)
+        acts = rng.integers(0, 5, (steps, B, 2)).astype(np.int8)
+        obs = np.zeros((B, R, 2, 7), np.float32)
+        rew = np.zeros(B, np.float32)
+        done = np.zeros(B, np.uint8)
+        t0 = time.perf_counter()
+        used = 1
+        for t in range(steps):
+            used = e.step_omp(acts[t], abi.CP_ACTION_DISCRETE, obs, rew, done, threads)
+        return time.perf_counter() - t0, used
+
+    probe_b = 256
+    dt, _ = run(probe_b, 20)
+    rate = probe_b * 20 / dt
+    steps = WINDOW + 1                  # one full episode incl. an in-step autoreset
+    B = int(min(65536, max(256, rate * budget_s / steps)))
+    B -= B % 64
+    dt, used = run(B, steps)
+    return {"value": round(B * steps / dt, 1), "unit": "env-steps/s", "cores": used, "kind": "port",
+            "sample": f"oracle/cp_oracle.c fp32 (same algorithm, gcc -O2 -march=x86-64-v3, OpenMP) on {B} envs x "
+                      f"{steps} steps of the same workload (R={R}, discrete random actions, autoreset incl.); "
+                      f"{dt:.1f} s wall on {used} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--repeats", type=int, default=3)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    B, R, K, W = args.batch, args.repeats, args.steps, args.warmup
+    env = BatchedCartpole(B, local, action_repeats=R, steps_per_repeat=1, max_episode_len=200,
+                          initial_force=55.0, autoreset=True, seed=1234 + rank, env_id_offset=rank * B)
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    actions = torch.randint(0, 5, (W + K, B, 2), dtype=torch.int8, device=dev, generator=gen)
+    gathered = torch.empty(world * B, device=dev, dtype=torch.float32)
+    env.reset()
+    for t in range(W):
+        env.step(actions[t])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    log(f"rank {rank}: B={B} R={R} warmup {W} done; timing {K} steps")
+
+    env.timing_begin(K)
+    hist = None
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for t in range(K):
+        env.step(actions[W + t])
+        if (t + 1) % WINDOW == 0:
+            r, _ = env.episode_returns()
+            if world > 1:
+                dist.all_gather_into_tensor(gathered, r)
+                g = gathered
+            else:
+                g = r
+            hist = torch.bincount(g.to(torch.int64).clamp_(0, 200), minlength=201)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    tm = env.timing_end()
+    el = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+
+    value = world * B * K / elapsed
+    per_launch_s = tm["step_ms"] / max(1, tm["step_launches"]) / 1e3
+    bytes_launch = B * step_kernel_bytes(R, 2)
+    achieved = bytes_launch / per_launch_s / 1e9
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": round(elapsed / K * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (random discrete actions, Philox bump pushes; no pybullet, see DESIGN.md)",
+        "config": {"workload": "C3: batch=65,536 envs/GPU, discrete 5-action, R=3, S=1, autoreset at 200, "
+                               "initial_force=55, fp32 (BASELINE.json configs[2]; N>1 = C4 with RCCL all-gather "
+                               "of episode returns per 200-step window)",
+                   "global_batch": world * B, "envs_per_gpu": B, "action_repeats": R, "steps_per_repeat": 1,
+                   "parallelism": f"dp{world} (independent env shards, no per-step collective)"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                     "kernel": "cp_step_kernel<discrete>",
+                     "bytes_per_launch": bytes_launch,
+                     "avg_launch_ms": round(per_launch_s * 1e3, 4),
+                     "launches": tm["step_launches"],
+                     "reset_kernel_avg_ms": round(tm["reset_ms"] / max(1, tm["reset_launches"]), 4)},
+        "episode_return_hist_nonzero": None if hist is None else int((hist > 0).sum().item()),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("cpu baseline ...")
+        out["cpu_baseline"] = cpu_baseline(R, args.cpu_seconds)
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

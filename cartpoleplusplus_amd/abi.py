@@ -1,0 +1,107 @@
+"""ctypes mirror of include/cartpole_amd.h (structs, constants, layouts).
+
+Pure data definitions: no library is loaded here.  `native.py` binds the HIP
+library's entry points with these types.
+"""
+import ctypes as C
+
+CP_ABI_VERSION = 1
+
+CP_BODY_GROUND, CP_BODY_CART, CP_BODY_POLE, CP_BODY_CART2, CP_BODY_POLE2 = range(5)
+CP_NUM_BODIES = 5
+CP_NUM_DYN = 4
+CP_NUM_PAIRS = 10
+CP_BODY_FIELDS = 13
+CP_MAX_POINTS = 20
+CP_MAX_FRICTION = 10
+CP_NUM_DISCRETE = 5
+
+
+def CP_SF_BODY(dyn, c):
+    return dyn * CP_BODY_FIELDS + c
+
+
+def CP_SF_PENDING(cart, c):
+    return CP_NUM_DYN * CP_BODY_FIELDS + cart * 3 + c
+
+
+CP_SF_STEPS = CP_NUM_DYN * CP_BODY_FIELDS + 6
+CP_SF_EPISODE = CP_SF_STEPS + 1
+CP_SF_DONE = CP_SF_STEPS + 2
+
+
+def CP_SF_WS_ID(pair):
+    return CP_SF_STEPS + 3 + pair
+
+
+def CP_SF_WS_LAM(pair, k):
+    return CP_SF_STEPS + 3 + CP_NUM_PAIRS + pair * 4 + k
+
+
+CP_STATE_FIELDS = CP_SF_STEPS + 3 + CP_NUM_PAIRS * 5
+
+CP_BUMP_PHILOX = 0
+CP_BUMP_HOST = 1
+CP_ACTION_CONTINUOUS = 0
+CP_ACTION_DISCRETE = 1
+
+# Discrete action table: order "no push, left, right, up, down"
+# (bullet_cartpole.py:84,89); entry = unit (fx, fy) scaled by action_force.
+DISCRETE_TABLE = ((0.0, 0.0), (-1.0, 0.0), (1.0, 0.0), (0.0, 1.0), (0.0, -1.0))
+
+_F3 = C.c_float * 3
+
+
+class cp_physics(C.Structure):
+    _fields_ = [
+        ("dt", C.c_float),
+        ("inv_dt", C.c_float),
+        ("gravity", _F3),
+        ("lin_damping", C.c_float),
+        ("ang_damping", C.c_float),
+        ("erp", C.c_float),
+        ("contact_margin", C.c_float),
+        ("residual_threshold", C.c_float),
+        ("solver_iterations", C.c_int32),
+        ("edge_bias", C.c_float),
+        ("max_angular_step", C.c_float),
+        ("warmstart", C.c_float),
+        ("half_extents", _F3 * CP_NUM_BODIES),
+        ("inv_mass", C.c_float * CP_NUM_BODIES),
+        ("inertia", _F3 * CP_NUM_BODIES),
+        ("inv_inertia", _F3 * CP_NUM_BODIES),
+        ("friction", C.c_float * CP_NUM_BODIES),
+        ("spawn_pos", _F3 * CP_NUM_BODIES),
+    ]
+
+
+class cp_config(C.Structure):
+    _fields_ = [
+        ("num_envs", C.c_int32),
+        ("action_repeats", C.c_int32),
+        ("steps_per_repeat", C.c_int32),
+        ("max_episode_len", C.c_int32),
+        ("action_force", C.c_float),
+        ("initial_force", C.c_float),
+        ("random_theta", C.c_int32),
+        ("initial_force_steps", C.c_int32),
+        ("settle_steps", C.c_int32),
+        ("done_on_bounds", C.c_int32),
+        ("pos_threshold", C.c_float),
+        ("angle_threshold", C.c_float),
+        ("tan_angle_threshold", C.c_float),
+        ("sin_angle_threshold", C.c_float),
+        ("autoreset", C.c_int32),
+        ("bump_mode", C.c_int32),
+        ("seed", C.c_uint64),
+        ("env_id_offset", C.c_int64),
+        ("phys", cp_physics),
+    ]
+
+
+def obs_shape(B, R):
+    return (B, R, 2, 7)
+
+
+def readback_shape(B, R, S):
+    return (B, 2, R, S, 4, 3)

@@ -1,0 +1,148 @@
+"""Batched cartpole++ env on one MI355X: B independent copies of the reference
+scene (bullet_cartpole.py:154-160) stepped by the HIP library, with inputs and
+outputs as PyTorch-ROCm tensors resident in HBM.
+
+    env = BatchedCartpole(65536, device=0, action_repeats=3, autoreset=True)
+    obs = env.reset()                                  # (B, R, 2, 7) float32
+    obs, reward, done = env.step(actions)              # actions (B,2,2) f32 or (B,2) int8
+
+One call of `step` is one env-step for every env: R x S physics substeps fused in
+one kernel launch (plus one compacted reset launch when autoreset is on).
+"""
+import ctypes as C
+
+import torch
+
+from . import abi, native
+
+
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+class BatchedCartpole:
+    def __init__(self, num_envs, device=0, *, action_repeats=2, steps_per_repeat=1, max_episode_len=200,
+                 action_force=50.0, initial_force=200.0, random_theta=True, done_on_bounds=False,
+                 autoreset=False, seed=0, env_id_offset=0, bump_mode="philox", discrete_actions=False,
+                 config=None, **phys):
+        self.lib = native.load()
+        if config is None:
+            config = native.default_config(
+                num_envs=int(num_envs), action_repeats=int(action_repeats),
+                steps_per_repeat=int(steps_per_repeat), max_episode_len=int(max_episode_len),
+                action_force=float(action_force), initial_force=float(initial_force),
+                random_theta=int(bool(random_theta)), done_on_bounds=int(bool(done_on_bounds)),
+                autoreset=int(bool(autoreset)), seed=int(seed), env_id_offset=int(env_id_offset),
+                bump_mode=abi.CP_BUMP_HOST if bump_mode == "host" else abi.CP_BUMP_PHILOX)
+            for k, v in phys.items():
+                setattr(config.phys, k, v)
+        self.cfg = config
+        self.B, self.R, self.S = config.num_envs, config.action_repeats, config.steps_per_repeat
+        self.discrete_actions = bool(discrete_actions)
+        self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        if self.device.type != "cuda":
+            raise native.CartpoleError("BatchedCartpole runs on a GPU device (no CPU fallback)")
+        self.h = C.c_void_p()
+        native.check(None, self.lib.cp_create(C.byref(config), self.device.index or 0, C.byref(self.h)),
+                     "cp_create")
+        f32 = dict(device=self.device, dtype=torch.float32)
+        self.obs = torch.zeros((self.B, self.R, 2, 7), **f32)
+        self.reward = torch.zeros(self.B, **f32)
+        self.done = torch.zeros(self.B, device=self.device, dtype=torch.uint8)
+        self.terminal_obs = torch.zeros_like(self.obs) if config.autoreset else None
+        self.readback = None
+
+    # -------------------------------------------------------------- plumbing
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.cp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+    # ------------------------------------------------------------------- API
+    def reset(self, mask=None):
+        """Reset envs (all, or where mask != 0); returns the obs tensor (B,R,2,7)."""
+        m = None
+        if mask is not None:
+            m = torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
+            assert m.numel() == self.B
+        native.check(self.h, self.lib.cp_reset(self.h, _ptr(m), _ptr(self.obs), self._stream()), "cp_reset")
+        return self.obs
+
+    def step(self, actions):
+        """One env-step for all envs.  actions: (B,2,2) float32 in [-1,1] (continuous,
+        bullet_cartpole.py:201-207) or (B,2) int8 indices into abi.DISCRETE_TABLE."""
+        if actions.dtype == torch.int8:
+            kind = abi.CP_ACTION_DISCRETE
+            assert actions.shape == (self.B, 2), actions.shape
+        else:
+            kind = abi.CP_ACTION_CONTINUOUS
+            if actions.dtype != torch.float32:
+                actions = actions.float()
+            assert actions.shape == (self.B, 2, 2), actions.shape
+        if actions.device != self.device:
+            actions = actions.to(self.device)
+        actions = actions.contiguous()
+        native.check(self.h, self.lib.cp_step(self.h, _ptr(actions), kind, _ptr(self.obs), _ptr(self.reward),
+                                              _ptr(self.done), _ptr(self.terminal_obs), self._stream()),
+                     "cp_step")
+        return self.obs, self.reward, self.done
+
+    def enable_readback(self, on=True, reference_bug=True):
+        """Per-substep 12-state pole readback (bullet_cartpole.py:212-234) into
+        self.readback (B, 2, R, S, 4, 3) = (xyz, rpy, linvel, angvel)."""
+        if on:
+            self.readback = torch.zeros(abi.readback_shape(self.B, self.R, self.S), device=self.device,
+                                        dtype=torch.float32)
+        else:
+            self.readback = None
+        native.check(self.h, self.lib.cp_set_readback(self.h, _ptr(self.readback), int(bool(reference_bug))),
+                     "cp_set_readback")
+
+    def set_bump_forces(self, forces):
+        """Parity mode (bump_mode='host'): LINK-frame bump forces (B, 30, 2, 2)."""
+        f = torch.as_tensor(forces, dtype=torch.float32, device=self.device).contiguous()
+        assert f.shape == (self.B, self.cfg.initial_force_steps, 2, 2), f.shape
+        native.check(self.h, self.lib.cp_set_bump_forces(self.h, _ptr(f), self._stream()), "cp_set_bump_forces")
+
+    def get_state(self):
+        s = torch.empty((abi.CP_STATE_FIELDS, self.B), device=self.device, dtype=torch.float32)
+        native.check(self.h, self.lib.cp_get_state(self.h, _ptr(s), self._stream()), "cp_get_state")
+        return s
+
+    def set_state(self, s):
+        s = torch.as_tensor(s, dtype=torch.float32, device=self.device).contiguous()
+        assert s.shape == (abi.CP_STATE_FIELDS, self.B)
+        native.check(self.h, self.lib.cp_set_state(self.h, _ptr(s), self._stream()), "cp_set_state")
+
+    def episode_returns(self):
+        r = torch.empty(self.B, device=self.device, dtype=torch.float32)
+        n = torch.empty(self.B, device=self.device, dtype=torch.int32)
+        native.check(self.h, self.lib.cp_episode_returns(self.h, _ptr(r), _ptr(n), self._stream()),
+                     "cp_episode_returns")
+        return r, n
+
+    def timing_begin(self, max_launches):
+        """Record HIP events around every step / reset kernel launch (see cp_timing_begin)."""
+        native.check(self.h, self.lib.cp_timing_begin(self.h, int(max_launches)), "cp_timing_begin")
+
+    def timing_end(self):
+        """-> dict(step_ms, step_launches, reset_ms, reset_launches); synchronises."""
+        sm, rm = C.c_double(), C.c_double()
+        sn, rn = C.c_int32(), C.c_int32()
+        native.check(self.h, self.lib.cp_timing_end(self.h, C.byref(sm), C.byref(sn), C.byref(rm), C.byref(rn)),
+                     "cp_timing_end")
+        return dict(step_ms=sm.value, step_launches=sn.value, reset_ms=rm.value, reset_launches=rn.value)
+
+    def overflow_counts(self):
+        o = torch.empty(self.B, device=self.device, dtype=torch.int32)
+        native.check(self.h, self.lib.cp_overflow_counts(self.h, _ptr(o), self._stream()), "cp_overflow_counts")
+        return o

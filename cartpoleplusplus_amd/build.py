@@ -1,0 +1,46 @@
+"""Build the HIP library in-tree: cartpoleplusplus_amd/libcartpole_hip.so (gfx950).
+
+    python -m cartpoleplusplus_amd.build          # or __graft_entry__.build()
+
+hipcc cross-compiles for gfx950 without a GPU.  -ffp-contract=off: only the
+explicit __builtin_fmaf calls fuse, which is what makes the kernel agree bit for
+bit with the CPU oracle.
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "csrc", "cp_kernels.hip")
+DEPS = [os.path.join(HERE, "csrc", f) for f in ("cp_kernels.hip", "cp_physics.h", "cp_math.h")] + [
+    os.path.join(HERE, "..", "include", "cartpole_amd.h")]
+LIB = os.path.join(HERE, "libcartpole_hip.so")
+ARCH = os.environ.get("CP_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
+         "-Wno-unused-result"]
+
+
+def up_to_date():
+    if not os.path.exists(LIB):
+        return False
+    t = os.path.getmtime(LIB)
+    return all(os.path.getmtime(d) <= t for d in DEPS)
+
+
+def build(force=False, verbose=False):
+    if not force and up_to_date():
+        return LIB
+    cmd = [HIPCC] + FLAGS + ["-o", LIB + ".tmp", SRC]
+    if verbose:
+        print(" ".join(cmd))
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError("hipcc failed:\n" + res.stdout + res.stderr)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,645 @@
+// cp_kernels.hip — batched cartpole++ env on MI355X (gfx950): kernels + C-ABI.
+//
+// Replaces bullet_cartpole.py's hot path (BulletCartpole.step/reset and the
+// pybullet calls behind them) for B independent envs, one lane per env.
+//
+//   cp_step_kernel   R x S substeps fused in one launch; force applied after each
+//                    substep (bullet_cartpole.py:199-207); obs at each repeat end
+//                    (:237 -> :298-311); steps/done/reward (:239-260).  Finishing
+//                    envs are appended to a reset list by wave ballot compaction.
+//   cp_reset_kernel  spawn poses, 100 settle + 30 bump substeps (:313-346), over a
+//                    compacted list of env ids (dense waves, no idle lanes).
+//
+// Memory: per-env state is SoA float32 [CP_STATE_FIELDS][B] in HBM (coalesced
+// per field); inside a launch the env lives in VGPRs and its contact rows in a
+// 40 KiB-per-wave LDS pool (4 waves per CU = 160 KiB).  DESIGN.md §Kernels.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/cartpole_amd.h"
+#include "cp_physics.h"
+
+namespace cp {
+
+__constant__ float kDiscrete[CP_NUM_DISCRETE][2] = {{0.f, 0.f}, {-1.f, 0.f}, {1.f, 0.f}, {0.f, 1.f}, {0.f, -1.f}};
+
+struct Bufs {
+    float* state;      // [CP_STATE_FIELDS][B]
+    float* term_obs;   // [R*14][B]
+    float* bumps;      // [B][ifs][2][2]
+    float* ret_acc;    // [B]
+    float* last_ret;   // [B]
+    int32_t* last_len; // [B]
+    int32_t* overflow; // [B]
+    int32_t* list;     // [B] reset list
+    int32_t* count;    // [1] reset list length
+    float* scratch;    // [4*CP_NUM_PAIRS][B] manifold headers of the current substep
+};
+
+CP_DEV uint32_t boff(int i) { return (uint32_t)i * 4u; }
+
+CP_DEV void load_sim(Sim& S, const Soa& st, uint32_t o) {
+#pragma unroll
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        S.b[d].x = mk(st.ld(CP_SF_BODY(d, 0), o), st.ld(CP_SF_BODY(d, 1), o), st.ld(CP_SF_BODY(d, 2), o));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) S.b[d].q[k] = st.ld(CP_SF_BODY(d, 3 + k), o);
+        S.b[d].v = mk(st.ld(CP_SF_BODY(d, 7), o), st.ld(CP_SF_BODY(d, 8), o), st.ld(CP_SF_BODY(d, 9), o));
+        S.b[d].w = mk(st.ld(CP_SF_BODY(d, 10), o), st.ld(CP_SF_BODY(d, 11), o), st.ld(CP_SF_BODY(d, 12), o));
+    }
+    S.f0 = mk(st.ld(CP_SF_PENDING(0, 0), o), st.ld(CP_SF_PENDING(0, 1), o), st.ld(CP_SF_PENDING(0, 2), o));
+    S.f2 = mk(st.ld(CP_SF_PENDING(1, 0), o), st.ld(CP_SF_PENDING(1, 1), o), st.ld(CP_SF_PENDING(1, 2), o));
+}
+
+CP_DEV void store_sim(const Sim& S, const Soa& st, uint32_t o) {
+#pragma unroll
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        st.st(CP_SF_BODY(d, 0), o, S.b[d].x.x);
+        st.st(CP_SF_BODY(d, 1), o, S.b[d].x.y);
+        st.st(CP_SF_BODY(d, 2), o, S.b[d].x.z);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) st.st(CP_SF_BODY(d, 3 + k), o, S.b[d].q[k]);
+        st.st(CP_SF_BODY(d, 7), o, S.b[d].v.x);
+        st.st(CP_SF_BODY(d, 8), o, S.b[d].v.y);
+        st.st(CP_SF_BODY(d, 9), o, S.b[d].v.z);
+        st.st(CP_SF_BODY(d, 10), o, S.b[d].w.x);
+        st.st(CP_SF_BODY(d, 11), o, S.b[d].w.y);
+        st.st(CP_SF_BODY(d, 12), o, S.b[d].w.z);
+    }
+    st.st(CP_SF_PENDING(0, 0), o, S.f0.x);
+    st.st(CP_SF_PENDING(0, 1), o, S.f0.y);
+    st.st(CP_SF_PENDING(0, 2), o, S.f0.z);
+    st.st(CP_SF_PENDING(1, 0), o, S.f2.x);
+    st.st(CP_SF_PENDING(1, 1), o, S.f2.y);
+    st.st(CP_SF_PENDING(1, 2), o, S.f2.z);
+}
+
+CP_DEV int32_t ldi(const Soa& st, int f, uint32_t o) { return __float_as_int(st.ld(f, o)); }
+CP_DEV void sti(const Soa& st, int f, uint32_t o, int32_t v) { st.st(f, o, __int_as_float(v)); }
+
+CP_DEV void write_obs_row(const Sim& S, float* dst) {
+    dst[0] = S.b[0].x.x; dst[1] = S.b[0].x.y; dst[2] = S.b[0].x.z;
+    dst[3] = S.b[0].q[0]; dst[4] = S.b[0].q[1]; dst[5] = S.b[0].q[2]; dst[6] = S.b[0].q[3];
+    dst[7] = S.b[1].x.x; dst[8] = S.b[1].x.y; dst[9] = S.b[1].x.z;
+    dst[10] = S.b[1].q[0]; dst[11] = S.b[1].q[1]; dst[12] = S.b[1].q[2]; dst[13] = S.b[1].q[3];
+}
+
+// 12-state pole readback (bullet_cartpole.py:212-229)
+template <int POLE, int VEL>
+CP_DEV void readback_pole(const Sim& S, float* dst) {
+    const Body& p = S.b[POLE];
+    const Body& vb = S.b[VEL];
+    V3 rpy = quat_euler(p.q[0], p.q[1], p.q[2], p.q[3]);
+    dst[0] = p.x.x; dst[1] = p.x.y; dst[2] = p.x.z;
+    dst[3] = rpy.x; dst[4] = rpy.y; dst[5] = rpy.z;
+    dst[6] = vb.v.x; dst[7] = vb.v.y; dst[8] = vb.v.z;
+    dst[9] = vb.w.x; dst[10] = vb.w.y; dst[11] = vb.w.z;
+}
+
+// commented-out bounds check of the reference (:243-253), on the pole pose
+CP_DEV bool bounds_exceeded(const Sim& S, const cp_config& cfg) {
+    const Body& p = S.b[1];
+    if (fabsf(p.x.x) > cfg.pos_threshold || fabsf(p.x.y) > cfg.pos_threshold) return true;
+    float qx = p.q[0], qy = p.q[1], qz = p.q[2], qw = p.q[3];
+    float Y = 2.0f * fmaf_(qy, qz, qw * qx);
+    float X = ((qw * qw - qx * qx) - qy * qy) + qz * qz;
+    bool roll_out = (X > 0.0f) ? (fabsf(Y) > X * cfg.tan_angle_threshold) : !(X == 0.0f && Y == 0.0f);
+    float sarg = -2.0f * fmaf_(qx, qz, -(qw * qy));
+    bool pitch_out = fabsf(sarg) > cfg.sin_angle_threshold;
+    return roll_out || pitch_out;
+}
+
+// Bump force k on cart C (LINK frame), bullet_cartpole.py:354-359
+CP_DEV void bump_force(const cp_config& cfg, const float* bumps, int i, int episode, int k, int c, float& fx,
+                       float& fy) {
+    if (cfg.bump_mode == CP_BUMP_HOST) {
+        const float* f = bumps + (((size_t)i * cfg.initial_force_steps + k) * 2 + c) * 2;
+        fx = f[0];
+        fy = f[1];
+        return;
+    }
+    const float F = cfg.initial_force;
+    if (!cfg.random_theta) {
+        fx = F;
+        fy = F * 0.0f;
+        return;
+    }
+    uint32_t idx = (uint32_t)(2 * k + c);
+    uint64_t gid = (uint64_t)(cfg.env_id_offset + i);
+    uint32_t w = philox_word(idx >> 2, (uint32_t)episode, (uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)cfg.seed,
+                             (uint32_t)(cfg.seed >> 32), (int)(idx & 3u));
+    float u = (float)(w >> 8) * 5.9604644775390625e-08f;
+    float s, co;
+    sincos_turns(u, s, co);
+    fx = F * co;
+    fy = F * s;
+}
+
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) cp_init_kernel(cp_config cfg, Bufs b) {
+    const int B = cfg.num_envs;
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    const Soa st = Soa::make(b.state, B, CP_STATE_FIELDS);
+    const uint32_t o = boff(i);
+    for (int f = 0; f < CP_STATE_FIELDS; ++f) st.st(f, o, 0.0f);
+#pragma unroll
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) st.st(CP_SF_BODY(d, k), o, cfg.phys.spawn_pos[d + 1][k]);
+        st.st(CP_SF_BODY(d, 6), o, 1.0f);
+    }
+#pragma unroll
+    for (int p = 0; p < CP_NUM_PAIRS; ++p) sti(st, CP_SF_WS_ID(p), o, -1);
+    sti(st, CP_SF_DONE, o, 1);  // not reset yet: reference raises, batched API reports done
+    b.ret_acc[i] = 0.0f;
+    b.last_ret[i] = 0.0f;
+    b.last_len[i] = 0;
+    b.overflow[i] = 0;
+}
+
+// env_mask -> compacted list (wave ballot + one atomic per wave)
+__global__ void __launch_bounds__(256) cp_mask_to_list_kernel(int B, const uint8_t* mask, int32_t* list,
+                                                               int32_t* count) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool want = i < B && (mask == nullptr || mask[i] != 0);
+    uint64_t bal = __ballot(want);
+    int lane = threadIdx.x & (WAVE - 1);
+    int n = __popcll(bal);
+    int base = 0;
+    if (lane == 0 && n) base = atomicAdd(count, n);
+    base = __shfl(base, 0);
+    if (want) list[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
+}
+
+__global__ void __launch_bounds__(WAVE) cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
+    __shared__ float lds_pool[POOL_FLOATS * WAVE];
+    const int B = cfg.num_envs;
+    const int t = blockIdx.x * WAVE + threadIdx.x;
+    const int n = *b.count;
+    if (t >= n) return;  // lanes past the compacted list
+    const int i = b.list[t];
+    float* pool = lds_pool + threadIdx.x;
+    const Mem G{Soa::make(b.state, B, CP_STATE_FIELDS), Soa::make(b.scratch, B, 4 * CP_NUM_PAIRS), boff(i)};
+    Sim S;
+    load_sim(S, G.st, G.off);  // pending forces survive the reset (pybullet keeps them)
+    const int episode = ldi(G.st, CP_SF_EPISODE, G.off);
+#pragma unroll
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        S.b[d].x = mk(cfg.phys.spawn_pos[d + 1][0], cfg.phys.spawn_pos[d + 1][1], cfg.phys.spawn_pos[d + 1][2]);
+        S.b[d].q[0] = 0.0f; S.b[d].q[1] = 0.0f; S.b[d].q[2] = 0.0f; S.b[d].q[3] = 1.0f;
+        S.b[d].v = mk(0.0f, 0.0f, 0.0f);
+        S.b[d].w = mk(0.0f, 0.0f, 0.0f);
+    }
+#pragma unroll
+    for (int p = 0; p < CP_NUM_PAIRS; ++p) {
+        sti(G.st, CP_SF_WS_ID(p), G.off, -1);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) G.ss(CP_SF_WS_LAM(p, k), 0.0f);
+    }
+    int ov = 0;
+    const int nsub = cfg.settle_steps + cfg.initial_force_steps;
+    for (int s = 0; s < nsub; ++s) {
+        substep(S, cfg.phys, pool, ov, G);
+        const int k = s - cfg.settle_steps;
+        if (k >= 0) {
+            float fx, fy;
+            bump_force(cfg, b.bumps, i, episode, k, 0, fx, fy);
+            apply_force_link<0>(S, fx, fy);
+            bump_force(cfg, b.bumps, i, episode, k, 1, fx, fy);
+            apply_force_link<1>(S, fx, fy);
+        }
+    }
+    store_sim(S, G.st, G.off);
+    b.overflow[i] += ov;
+    float row[14];
+    write_obs_row(S, row);
+    const int R = cfg.action_repeats;
+    float* o = obs_out + (size_t)i * R * 14;
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int f = 0; f < 14; ++f) o[r * 14 + f] = row[f];
+    sti(G.st, CP_SF_STEPS, G.off, 0);
+    sti(G.st, CP_SF_DONE, G.off, 0);
+    sti(G.st, CP_SF_EPISODE, G.off, episode + 1);
+    b.ret_acc[i] = 0.0f;
+}
+
+template <int KIND>
+__global__ void __launch_bounds__(WAVE) cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out,
+                                                        float* reward_out, uint8_t* done_out, float* term_out,
+                                                        float* readback, int rb_bug) {
+    __shared__ float lds_pool[POOL_FLOATS * WAVE];
+    const int B = cfg.num_envs;
+    const int i = blockIdx.x * WAVE + threadIdx.x;
+    const bool inb = i < B;
+    const int R = cfg.action_repeats, SR = cfg.steps_per_repeat;
+    float* pool = lds_pool + threadIdx.x;
+    bool want_reset = false;
+    if (inb) {
+        const Mem G{Soa::make(b.state, B, CP_STATE_FIELDS), Soa::make(b.scratch, B, 4 * CP_NUM_PAIRS), boff(i)};
+        const Soa term = Soa::make(b.term_obs, B, R * 14);
+        float* obs = obs_out + (size_t)i * R * 14;
+        if (ldi(G.st, CP_SF_DONE, G.off)) {  // step after done (bullet_cartpole.py:179-181)
+            for (int f = 0; f < R * 14; ++f) obs[f] = term.ld(f, G.off);
+            reward_out[i] = 0.0f;
+            done_out[i] = 1;
+        } else {
+            float a00, a01, a10, a11;
+            if constexpr (KIND == CP_ACTION_CONTINUOUS) {
+                const float4 a = reinterpret_cast<const float4*>(actions)[i];
+                a00 = a.x; a01 = a.y; a10 = a.z; a11 = a.w;
+            } else {
+                const char2 a = reinterpret_cast<const char2*>(actions)[i];
+                int k0 = a.x, k1 = a.y;
+                k0 = (k0 < 0 || k0 >= CP_NUM_DISCRETE) ? 0 : k0;
+                k1 = (k1 < 0 || k1 >= CP_NUM_DISCRETE) ? 0 : k1;
+                a00 = kDiscrete[k0][0]; a01 = kDiscrete[k0][1];
+                a10 = kDiscrete[k1][0]; a11 = kDiscrete[k1][1];
+            }
+            const float F = cfg.action_force;
+            const float f00 = a00 * F, f01 = a01 * F, f10 = a10 * F, f11 = a11 * F;
+            Sim S;
+            load_sim(S, G.st, G.off);
+            int ov = 0;
+            for (int r = 0; r < R; ++r) {
+                for (int s = 0; s < SR; ++s) {
+                    substep(S, cfg.phys, pool, ov, G);
+                    apply_force_link<0>(S, f00, f01);
+                    apply_force_link<1>(S, f10, f11);
+                    if (readback) {
+                        float* rb = readback + (size_t)i * 2 * R * SR * 12;
+                        readback_pole<1, 1>(S, rb + ((size_t)(0 * R + r) * SR + s) * 12);
+                        if (rb_bug) readback_pole<3, 1>(S, rb + ((size_t)(1 * R + r) * SR + s) * 12);
+                        else readback_pole<3, 3>(S, rb + ((size_t)(1 * R + r) * SR + s) * 12);
+                    }
+                }
+                float row[14];
+                write_obs_row(S, row);
+#pragma unroll
+                for (int f = 0; f < 14; ++f) obs[r * 14 + f] = row[f];
+            }
+            if (ov) b.overflow[i] += ov;
+            const int steps = ldi(G.st, CP_SF_STEPS, G.off) + 1;
+            bool done = steps >= cfg.max_episode_len;
+            if (cfg.done_on_bounds && bounds_exceeded(S, cfg)) done = true;
+            store_sim(S, G.st, G.off);
+            sti(G.st, CP_SF_STEPS, G.off, steps);
+            reward_out[i] = 1.0f;  // bullet_cartpole.py:260
+            done_out[i] = done ? 1 : 0;
+            const float ret = b.ret_acc[i] + 1.0f;
+            if (done) {
+                b.last_ret[i] = ret;
+                b.last_len[i] = steps;
+                b.ret_acc[i] = 0.0f;
+                for (int f = 0; f < R * 14; ++f) term.st(f, G.off, obs[f]);
+                if (term_out)
+                    for (int f = 0; f < R * 14; ++f) term_out[(size_t)i * R * 14 + f] = obs[f];
+                sti(G.st, CP_SF_DONE, G.off, 1);
+                want_reset = cfg.autoreset != 0;
+            } else {
+                b.ret_acc[i] = ret;
+            }
+        }
+    }
+    if (cfg.autoreset) {
+        // wave ballot compaction of the finishing envs into the reset list
+        const uint64_t bal = __ballot(want_reset);
+        const int lane = threadIdx.x;
+        const int n = __popcll(bal);
+        int base = 0;
+        if (lane == 0 && n) base = atomicAdd(b.count, n);
+        base = __shfl(base, 0);
+        if (want_reset) b.list[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
+    }
+}
+
+__global__ void __launch_bounds__(256) cp_copy_kernel(const float* src, float* dst, size_t n) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[i];
+}
+
+}  // namespace cp
+
+// ============================================================================ C-ABI
+struct cp_timing {
+    int cap = 0;                 // event pairs per kind
+    int nstep = 0, nreset = 0;   // pairs recorded
+    std::vector<hipEvent_t> ev;  // [0, 2cap): step pairs, [2cap, 4cap): reset pairs
+};
+
+struct cp_handle {
+    cp_config cfg;
+    int device;
+    cp::Bufs b;
+    float* readback;
+    int readback_bug;
+    cp_timing timing;
+    std::string err;
+};
+
+static void timing_free(cp_timing& t) {
+    for (hipEvent_t e : t.ev) (void)hipEventDestroy(e);
+    t.ev.clear();
+    t.cap = t.nstep = t.nreset = 0;
+}
+// returns the event pair to record around a launch of `kind` (0 step, 1 reset), or nullptr
+static hipEvent_t* timing_slot(cp_handle* h, int kind) {
+    cp_timing& t = h->timing;
+    if (t.cap == 0) return nullptr;
+    int& n = kind == 0 ? t.nstep : t.nreset;
+    if (n >= t.cap) return nullptr;
+    hipEvent_t* p = &t.ev[(size_t)(kind * t.cap + n) * 2];
+    ++n;
+    return p;
+}
+
+static thread_local std::string g_err;
+
+static int fail(cp_handle* h, const std::string& msg) {
+    if (h) h->err = msg;
+    g_err = msg;
+    return -1;
+}
+static int check(cp_handle* h, hipError_t e, const char* what) {
+    if (e != hipSuccess) return fail(h, std::string(what) + ": " + hipGetErrorString(e));
+    return 0;
+}
+#define CP_TRY(h, call)                                   \
+    do {                                                  \
+        if (check((h), (call), #call)) return -1;         \
+    } while (0)
+
+static inline unsigned grid_for(int n, int block) { return (unsigned)((n + block - 1) / block); }
+
+extern "C" {
+
+int cp_abi_version(void) { return CP_ABI_VERSION; }
+
+void cp_default_config(cp_config* c) {
+    std::memset(c, 0, sizeof(*c));
+    c->num_envs = 1;
+    c->action_repeats = 2;       // bullet_cartpole.py:23
+    c->steps_per_repeat = 1;     // :25
+    c->max_episode_len = 200;    // :31
+    c->action_force = 50.0f;     // :18
+    c->initial_force = 200.0f;   // :20
+    c->random_theta = 1;         // :22
+    c->initial_force_steps = 30; // :76
+    c->settle_steps = 100;       // :326
+    c->done_on_bounds = 0;       // :243-253 are commented out in the fork
+    c->pos_threshold = 3.0f;     // :58
+    c->angle_threshold = 0.35f;  // :62
+    c->tan_angle_threshold = (float)std::tan((double)0.35f);
+    c->sin_angle_threshold = (float)std::sin((double)0.35f);
+    c->autoreset = 0;
+    c->bump_mode = CP_BUMP_PHILOX;
+    c->seed = 0;
+    c->env_id_offset = 0;
+    cp_physics* p = &c->phys;
+    p->dt = (float)(1.0 / 240.0);
+    p->inv_dt = 240.0f;
+    p->gravity[0] = 0.0f;
+    p->gravity[1] = 0.0f;
+    p->gravity[2] = -9.81f;  // :152
+    p->lin_damping = 0.04f;
+    p->ang_damping = 0.04f;
+    p->erp = 0.2f;
+    p->contact_margin = 0.02f;
+    p->residual_threshold = 1e-7f;
+    p->solver_iterations = 50;
+    p->edge_bias = 1e-4f;
+    p->max_angular_step = (float)(0.25 * 3.141592653589793);
+    p->warmstart = 0.85f;
+    // models/ground.urdf, cart.urdf, pole.urdf, cart2.urdf, pole2.urdf
+    static const double he[5][3] = {{1.5, 1.5, 0.05}, {0.1, 0.1, 0.025}, {0.005, 0.005, 0.25},
+                                    {0.1, 0.1, 0.025}, {0.005, 0.005, 0.25}};
+    static const double mass[5] = {0.0, 1.0, 5.0, 1.0, 5.0};
+    static const double inert[5][3] = {{0, 0, 0},
+                                       {0.0035416666666, 0.0035416666666, 0.0066666666666},
+                                       {0.104208333333333, 0.104208333333333, 0.00008333333333},
+                                       {0.0035416666666, 0.0035416666666, 0.0066666666666},
+                                       {0.104208333333333, 0.104208333333333, 0.00008333333333}};
+    static const double mu[5] = {0.5, 0.0, 1.0, 0.0, 1.0};
+    static const double spawn[5][3] = {{0, 0, 0}, {0, 0, 0.08}, {0, 0, 0.35}, {1, 0, 0.08}, {1, 0, 0.35}};
+    for (int b = 0; b < 5; ++b) {
+        for (int k = 0; k < 3; ++k) {
+            p->half_extents[b][k] = (float)he[b][k];
+            p->inertia[b][k] = (float)inert[b][k];
+            p->inv_inertia[b][k] = inert[b][k] > 0 ? (float)(1.0 / inert[b][k]) : 0.0f;
+            p->spawn_pos[b][k] = (float)spawn[b][k];
+        }
+        p->inv_mass[b] = mass[b] > 0 ? (float)(1.0 / mass[b]) : 0.0f;
+        p->friction[b] = (float)mu[b];
+    }
+}
+
+const char* cp_last_error(const cp_handle* h) { return h ? h->err.c_str() : g_err.c_str(); }
+
+int cp_create(const cp_config* cfg, int device, cp_handle** out) {
+    if (!cfg || !out) return fail(nullptr, "cp_create: null argument");
+    if (cfg->num_envs <= 0) return fail(nullptr, "cp_create: num_envs must be > 0");
+    if (cfg->action_repeats <= 0 || cfg->steps_per_repeat <= 0)
+        return fail(nullptr, "cp_create: action_repeats and steps_per_repeat must be > 0");
+    if (cfg->initial_force_steps < 0 || cfg->settle_steps < 0)
+        return fail(nullptr, "cp_create: negative step counts");
+    if (cfg->phys.solver_iterations < 0) return fail(nullptr, "cp_create: negative solver_iterations");
+    if ((unsigned long long)cfg->num_envs * CP_STATE_FIELDS * 4ull >= (1ull << 32) ||
+        (unsigned long long)cfg->num_envs * cfg->action_repeats * 14ull * 4ull >= (1ull << 32))
+        return fail(nullptr, "cp_create: num_envs too large for one handle (SoA arrays must stay below 4 GiB)");
+    cp_handle* h = new (std::nothrow) cp_handle();
+    if (!h) return fail(nullptr, "cp_create: out of memory");
+    h->cfg = *cfg;
+    h->device = device;
+    h->readback = nullptr;
+    h->readback_bug = 1;
+    std::memset(&h->b, 0, sizeof(h->b));
+    const size_t B = (size_t)cfg->num_envs;
+    const int R = cfg->action_repeats;
+    auto fail_free = [&](hipError_t e, const char* what) {
+        std::string msg = std::string(what) + ": " + hipGetErrorString(e);
+        cp_destroy(h);
+        return fail(nullptr, msg);
+    };
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) return fail_free(e, "hipSetDevice");
+#define CP_ALLOC(ptr, bytes)                                   \
+    e = hipMalloc((void**)&(ptr), (bytes));                    \
+    if (e != hipSuccess) return fail_free(e, "hipMalloc " #ptr);
+    CP_ALLOC(h->b.state, (size_t)CP_STATE_FIELDS * B * sizeof(float));
+    CP_ALLOC(h->b.term_obs, (size_t)R * 14 * B * sizeof(float));
+    CP_ALLOC(h->b.bumps, B * (size_t)(cfg->initial_force_steps > 0 ? cfg->initial_force_steps : 1) * 4 * sizeof(float));
+    CP_ALLOC(h->b.ret_acc, B * sizeof(float));
+    CP_ALLOC(h->b.last_ret, B * sizeof(float));
+    CP_ALLOC(h->b.last_len, B * sizeof(int32_t));
+    CP_ALLOC(h->b.overflow, B * sizeof(int32_t));
+    CP_ALLOC(h->b.list, B * sizeof(int32_t));
+    CP_ALLOC(h->b.count, sizeof(int32_t));
+    CP_ALLOC(h->b.scratch, (size_t)4 * CP_NUM_PAIRS * B * sizeof(float));
+#undef CP_ALLOC
+    e = hipMemset(h->b.term_obs, 0, (size_t)R * 14 * B * sizeof(float));
+    if (e != hipSuccess) return fail_free(e, "hipMemset");
+    e = hipMemset(h->b.bumps, 0, B * (size_t)(cfg->initial_force_steps > 0 ? cfg->initial_force_steps : 1) * 4 * sizeof(float));
+    if (e != hipSuccess) return fail_free(e, "hipMemset");
+    hipLaunchKernelGGL(cp::cp_init_kernel, dim3(grid_for((int)B, 256)), dim3(256), 0, 0, h->cfg, h->b);
+    e = hipGetLastError();
+    if (e != hipSuccess) return fail_free(e, "cp_init_kernel");
+    e = hipDeviceSynchronize();
+    if (e != hipSuccess) return fail_free(e, "hipDeviceSynchronize");
+    *out = h;
+    return 0;
+}
+
+void cp_destroy(cp_handle* h) {
+    if (!h) return;
+    hipSetDevice(h->device);
+    timing_free(h->timing);
+    hipFree(h->b.state);
+    hipFree(h->b.term_obs);
+    hipFree(h->b.bumps);
+    hipFree(h->b.ret_acc);
+    hipFree(h->b.last_ret);
+    hipFree(h->b.last_len);
+    hipFree(h->b.overflow);
+    hipFree(h->b.list);
+    hipFree(h->b.count);
+    hipFree(h->b.scratch);
+    delete h;
+}
+
+static int launch_reset_from_list(cp_handle* h, float* obs_out, hipStream_t st) {
+    const int B = h->cfg.num_envs;
+    hipEvent_t* ev = timing_slot(h, 1);
+    if (ev) CP_TRY(h, hipEventRecord(ev[0], st));
+    hipLaunchKernelGGL(cp::cp_reset_kernel, dim3(grid_for(B, cp::WAVE)), dim3(cp::WAVE), 0, st, h->cfg, h->b, obs_out);
+    if (check(h, hipGetLastError(), "cp_reset_kernel")) return -1;
+    if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
+    return 0;
+}
+
+int cp_reset(cp_handle* h, const uint8_t* env_mask, float* obs_out, void* stream) {
+    if (!h || !obs_out) return fail(h, "cp_reset: null argument");
+    hipStream_t st = (hipStream_t)stream;
+    const int B = h->cfg.num_envs;
+    CP_TRY(h, hipSetDevice(h->device));
+    CP_TRY(h, hipMemsetAsync(h->b.count, 0, sizeof(int32_t), st));
+    hipLaunchKernelGGL(cp::cp_mask_to_list_kernel, dim3(grid_for(B, 256)), dim3(256), 0, st, B, env_mask, h->b.list,
+                       h->b.count);
+    CP_TRY(h, hipGetLastError());
+    return launch_reset_from_list(h, obs_out, st);
+}
+
+int cp_step(cp_handle* h, const void* actions, int action_kind, float* obs_out, float* reward_out,
+            uint8_t* done_out, float* terminal_obs_out, void* stream) {
+    if (!h || !actions || !obs_out || !reward_out || !done_out) return fail(h, "cp_step: null argument");
+    if (action_kind != CP_ACTION_CONTINUOUS && action_kind != CP_ACTION_DISCRETE)
+        return fail(h, "cp_step: action_kind must be CP_ACTION_CONTINUOUS or CP_ACTION_DISCRETE");
+    hipStream_t st = (hipStream_t)stream;
+    const int B = h->cfg.num_envs;
+    CP_TRY(h, hipSetDevice(h->device));
+    if (h->cfg.autoreset) CP_TRY(h, hipMemsetAsync(h->b.count, 0, sizeof(int32_t), st));
+    dim3 grid(grid_for(B, cp::WAVE)), block(cp::WAVE);
+    hipEvent_t* ev = timing_slot(h, 0);
+    if (ev) CP_TRY(h, hipEventRecord(ev[0], st));
+    if (action_kind == CP_ACTION_CONTINUOUS)
+        hipLaunchKernelGGL(cp::cp_step_kernel<CP_ACTION_CONTINUOUS>, grid, block, 0, st, h->cfg, h->b, actions,
+                           obs_out, reward_out, done_out, terminal_obs_out, h->readback, h->readback_bug);
+    else
+        hipLaunchKernelGGL(cp::cp_step_kernel<CP_ACTION_DISCRETE>, grid, block, 0, st, h->cfg, h->b, actions,
+                           obs_out, reward_out, done_out, terminal_obs_out, h->readback, h->readback_bug);
+    CP_TRY(h, hipGetLastError());
+    if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
+    if (h->cfg.autoreset) return launch_reset_from_list(h, obs_out, st);
+    return 0;
+}
+
+int cp_set_readback(cp_handle* h, float* readback_out, int reference_bug) {
+    if (!h) return fail(h, "cp_set_readback: null handle");
+    h->readback = readback_out;
+    h->readback_bug = reference_bug ? 1 : 0;
+    return 0;
+}
+
+int cp_set_bump_forces(cp_handle* h, const float* forces, void* stream) {
+    if (!h || !forces) return fail(h, "cp_set_bump_forces: null argument");
+    CP_TRY(h, hipSetDevice(h->device));
+    size_t n = (size_t)h->cfg.num_envs * h->cfg.initial_force_steps * 4;
+    CP_TRY(h, hipMemcpyAsync(h->b.bumps, forces, n * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return 0;
+}
+
+int cp_get_state(cp_handle* h, float* state_out, void* stream) {
+    if (!h || !state_out) return fail(h, "cp_get_state: null argument");
+    CP_TRY(h, hipSetDevice(h->device));
+    size_t n = (size_t)CP_STATE_FIELDS * h->cfg.num_envs;
+    CP_TRY(h, hipMemcpyAsync(state_out, h->b.state, n * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return 0;
+}
+
+int cp_set_state(cp_handle* h, const float* state_in, void* stream) {
+    if (!h || !state_in) return fail(h, "cp_set_state: null argument");
+    CP_TRY(h, hipSetDevice(h->device));
+    size_t n = (size_t)CP_STATE_FIELDS * h->cfg.num_envs;
+    CP_TRY(h, hipMemcpyAsync(h->b.state, state_in, n * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return 0;
+}
+
+int cp_episode_returns(cp_handle* h, float* returns_out, int32_t* lengths_out, void* stream) {
+    if (!h) return fail(h, "cp_episode_returns: null handle");
+    CP_TRY(h, hipSetDevice(h->device));
+    size_t B = (size_t)h->cfg.num_envs;
+    hipStream_t st = (hipStream_t)stream;
+    if (returns_out) CP_TRY(h, hipMemcpyAsync(returns_out, h->b.last_ret, B * sizeof(float), hipMemcpyDeviceToDevice, st));
+    if (lengths_out)
+        CP_TRY(h, hipMemcpyAsync(lengths_out, h->b.last_len, B * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    return 0;
+}
+
+int cp_overflow_counts(cp_handle* h, int32_t* out, void* stream) {
+    if (!h || !out) return fail(h, "cp_overflow_counts: null argument");
+    CP_TRY(h, hipSetDevice(h->device));
+    CP_TRY(h, hipMemcpyAsync(out, h->b.overflow, (size_t)h->cfg.num_envs * sizeof(int32_t), hipMemcpyDeviceToDevice,
+                             (hipStream_t)stream));
+    return 0;
+}
+
+int cp_timing_begin(cp_handle* h, int max_launches) {
+    if (!h || max_launches <= 0) return fail(h, "cp_timing_begin: bad argument");
+    CP_TRY(h, hipSetDevice(h->device));
+    timing_free(h->timing);
+    h->timing.ev.resize((size_t)max_launches * 4);
+    for (auto& e : h->timing.ev) CP_TRY(h, hipEventCreate(&e));
+    h->timing.cap = max_launches;
+    return 0;
+}
+
+int cp_timing_end(cp_handle* h, double* step_ms, int32_t* step_launches, double* reset_ms,
+                  int32_t* reset_launches) {
+    if (!h) return fail(h, "cp_timing_end: null handle");
+    cp_timing& t = h->timing;
+    double sums[2] = {0.0, 0.0};
+    int counts[2] = {t.nstep, t.nreset};
+    for (int kind = 0; kind < 2; ++kind) {
+        for (int n = 0; n < counts[kind]; ++n) {
+            hipEvent_t a = t.ev[(size_t)(kind * t.cap + n) * 2], b = t.ev[(size_t)(kind * t.cap + n) * 2 + 1];
+            CP_TRY(h, hipEventSynchronize(b));
+            float ms = 0.0f;
+            CP_TRY(h, hipEventElapsedTime(&ms, a, b));
+            sums[kind] += ms;
+        }
+    }
+    if (step_ms) *step_ms = sums[0];
+    if (step_launches) *step_launches = counts[0];
+    if (reset_ms) *reset_ms = sums[1];
+    if (reset_launches) *reset_launches = counts[1];
+    timing_free(t);
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,85 @@
+"""ctypes binding of the HIP library (libcartpole_hip.so, C-ABI in include/cartpole_amd.h).
+
+The product path has no CPU fallback: if the library is missing or no GPU is
+visible, these calls raise.  (`tests/` compare against the CPU oracle, which is
+never imported from here.)
+"""
+import ctypes as C
+import os
+
+from . import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcartpole_hip.so")
+
+# every entry point declared in include/cartpole_amd.h
+EXPORTS = (
+    "cp_default_config", "cp_create", "cp_destroy", "cp_last_error", "cp_abi_version",
+    "cp_reset", "cp_step", "cp_set_readback", "cp_set_bump_forces", "cp_get_state",
+    "cp_set_state", "cp_episode_returns", "cp_overflow_counts", "cp_timing_begin", "cp_timing_end",
+)
+
+_lib = None
+
+
+class CartpoleError(RuntimeError):
+    pass
+
+
+def load():
+    """Load the in-tree HIP library (does not touch the GPU)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise CartpoleError(
+            f"{LIB_PATH} is missing: build it with `python -m cartpoleplusplus_amd.build` "
+            "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    lib = C.CDLL(LIB_PATH)
+    P, VP, I = C.POINTER, C.c_void_p, C.c_int
+    cfgp = P(abi.cp_config)
+    sig = {
+        "cp_default_config": (None, [cfgp]),
+        "cp_create": (I, [cfgp, I, P(VP)]),
+        "cp_destroy": (None, [VP]),
+        "cp_last_error": (C.c_char_p, [VP]),
+        "cp_abi_version": (I, []),
+        "cp_reset": (I, [VP, VP, VP, VP]),
+        "cp_step": (I, [VP, VP, I, VP, VP, VP, VP, VP]),
+        "cp_set_readback": (I, [VP, VP, I]),
+        "cp_set_bump_forces": (I, [VP, VP, VP]),
+        "cp_get_state": (I, [VP, VP, VP]),
+        "cp_set_state": (I, [VP, VP, VP]),
+        "cp_episode_returns": (I, [VP, VP, VP, VP]),
+        "cp_overflow_counts": (I, [VP, VP, VP]),
+        "cp_timing_begin": (I, [VP, I]),
+        "cp_timing_end": (I, [VP, P(C.c_double), P(C.c_int32), P(C.c_double), P(C.c_int32)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype, f.argtypes = res, args
+    if lib.cp_abi_version() != abi.CP_ABI_VERSION:
+        raise CartpoleError("libcartpole_hip.so ABI version mismatch; rebuild it")
+    _lib = lib
+    return lib
+
+
+def default_config(**overrides):
+    """cp_config with the reference defaults (bullet_cartpole.py:15-40), then overrides."""
+    import math
+    cfg = abi.cp_config()
+    load().cp_default_config(C.byref(cfg))
+    for k, v in overrides.items():
+        if k == "angle_threshold":
+            cfg.tan_angle_threshold = math.tan(v)
+            cfg.sin_angle_threshold = math.sin(v)
+        if not hasattr(cfg, k):
+            raise AttributeError(f"cp_config has no field {k!r}")
+        setattr(cfg, k, v)
+    return cfg
+
+
+def check(h, status, what):
+    if status != 0:
+        msg = load().cp_last_error(h)
+        raise CartpoleError(f"{what} failed: {msg.decode() if msg else 'unknown error'}")

@@ -1,0 +1,200 @@
+/*
+ * cartpole_amd.h — C-ABI of the MI355X-native batched cartpole++ environment.
+ *
+ * Drop-in boundary for the reference's hot path: the `BulletCartpole` gym env
+ * (bullet_cartpole.py:48-359) and the pybullet calls it makes per step / reset
+ * (stepSimulation, applyExternalForce, getBasePositionAndOrientation,
+ * resetBasePositionAndOrientation; call sites listed per entry point below).
+ *
+ * Conventions
+ *   - extern "C", plain pointers and sizes; no torch/HIP types in signatures
+ *     (streams are passed as `void*` = hipStream_t, NULL = default stream).
+ *   - Every status is an int: 0 = ok, <0 = error; cp_last_error() explains.
+ *   - All per-call buffers are CALLER-OWNED DEVICE pointers (e.g. torch-ROCm
+ *     data_ptr()).  cp_step/cp_reset allocate nothing and never synchronise the
+ *     host, so a caller may capture them into a hipGraph.
+ *   - One handle per stream; a handle is not thread-safe, distinct handles are
+ *     independent (one process per GPU: each rank creates its own handle).
+ *
+ * Layouts (B = num_envs, R = action_repeats)
+ *   obs           float32 [B][R][2][7]   (cart pose, pole pose; xyz + quat xyzw),
+ *                 bullet_cartpole.py:298-311 + :43-45, (R,2,7) per env
+ *   actions       kind 0: float32 [B][2][2]  (action[0] -> cart, action[1] -> cart2,
+ *                         bullet_cartpole.py:201-207), scaled by action_force
+ *                 kind 1: int8    [B][2]     discrete table (see CP_DISCRETE_TABLE)
+ *   reward        float32 [B]            (1.0 per step, bullet_cartpole.py:260)
+ *   done          uint8   [B]
+ *   state (get/set) float32 [CP_STATE_FIELDS][B]  (SoA; see CP_SF_* below)
+ */
+#ifndef CARTPOLE_AMD_H
+#define CARTPOLE_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CP_ABI_VERSION 1
+
+/* Bodies, in the reference's loadURDF order (bullet_cartpole.py:154-160). */
+#define CP_BODY_GROUND 0
+#define CP_BODY_CART   1
+#define CP_BODY_POLE   2
+#define CP_BODY_CART2  3
+#define CP_BODY_POLE2  4
+#define CP_NUM_BODIES  5
+#define CP_NUM_DYN     4          /* dynamic bodies: cart, pole, cart2, pole2 */
+#define CP_NUM_PAIRS   10         /* all body pairs (a<b) */
+
+/* Per-body dynamic state: pos(3) quat xyzw(4) linvel(3) angvel(3). */
+#define CP_BODY_FIELDS 13
+/* SoA state fields for get/set: 4 dynamic bodies x 13, then pending world
+ * forces on cart and cart2 (3 each), then integer counters stored as float
+ * bit patterns (steps, episode, done). */
+#define CP_SF_BODY(dyn, c)  ((dyn) * CP_BODY_FIELDS + (c))
+#define CP_SF_PENDING(cart, c) (CP_NUM_DYN * CP_BODY_FIELDS + (cart) * 3 + (c))
+#define CP_SF_STEPS   (CP_NUM_DYN * CP_BODY_FIELDS + 6)
+#define CP_SF_EPISODE (CP_SF_STEPS + 1)
+#define CP_SF_DONE    (CP_SF_STEPS + 2)
+/* warm-start cache (persistent contact impulses, DESIGN.md §Physics model):
+ * per pair one packed word of 4 feature ids (bytes, 0xFF = empty slot), and
+ * the 4 accumulated normal impulses of the last substep */
+#define CP_SF_WS_ID(pair)      (CP_SF_STEPS + 3 + (pair))
+#define CP_SF_WS_LAM(pair, k)  (CP_SF_STEPS + 3 + CP_NUM_PAIRS + (pair) * 4 + (k))
+#define CP_STATE_FIELDS (CP_SF_STEPS + 3 + CP_NUM_PAIRS * 5)
+
+/* Contact pools per env (LDS-resident in the kernel; same caps in the oracle). */
+#define CP_MAX_POINTS   20        /* normal-contact rows per substep */
+#define CP_MAX_FRICTION 10        /* contact points that carry 2 friction rows */
+
+/* Discrete action table (the fork dropped upstream's mapping; the comment at
+ * bullet_cartpole.py:84,89 names the order "no push, left, right, up, down").
+ * Entry k is the unit (fx, fy) pushed on a cart, scaled by action_force. */
+#define CP_NUM_DISCRETE 5
+
+/* Physics parameters.  Defaults (cp_default_config) restate the Bullet /
+ * pybullet defaults as documented in DESIGN.md §Physics model; every one of
+ * them is an [ext] hypothesis (pybullet is not available to pin them). */
+typedef struct cp_physics {
+    float dt;                 /* fixed step, 1/240 s                           */
+    float inv_dt;             /* 1/dt (host-computed so all paths agree)       */
+    float gravity[3];         /* (0,0,-9.81), bullet_cartpole.py:152           */
+    float lin_damping;        /* k1 = k2 = 0.04 (btMultiBody default)          */
+    float ang_damping;        /* k1 = k2 = 0.04                                */
+    float erp;                /* contact error reduction, 0.2                  */
+    float contact_margin;     /* speculative contact distance, 0.02 m          */
+    float residual_threshold; /* PGS early-exit threshold, 1e-7                */
+    int32_t solver_iterations;/* PGS iterations, 50                            */
+    float edge_bias;          /* SAT: edge axis must beat faces by this, 1e-4 m */
+    float max_angular_step;   /* quaternion-integration clamp, pi/4 rad/step   */
+    float warmstart;          /* warm-start factor on cached impulses, 0.85    */
+    /* per body (ground, cart, pole, cart2, pole2) from the models/ URDF files */
+    float half_extents[CP_NUM_BODIES][3];
+    float inv_mass[CP_NUM_BODIES];
+    float inertia[CP_NUM_BODIES][3];      /* local principal inertia            */
+    float inv_inertia[CP_NUM_BODIES][3];
+    float friction[CP_NUM_BODIES];        /* lateral friction; pair mu = product */
+    float spawn_pos[CP_NUM_BODIES][3];    /* bullet_cartpole.py:154-160,319-323  */
+} cp_physics;
+
+typedef struct cp_config {
+    int32_t num_envs;            /* B                                          */
+    int32_t action_repeats;      /* --action-repeats (ref default 2)           */
+    int32_t steps_per_repeat;    /* --steps-per-repeat (1)                     */
+    int32_t max_episode_len;     /* --max-episode-len (200)                    */
+    float   action_force;        /* --action-force (50)                        */
+    float   initial_force;       /* --initial-force (200)                      */
+    int32_t random_theta;        /* !--no-random-theta                         */
+    int32_t initial_force_steps; /* 30, bullet_cartpole.py:76                  */
+    int32_t settle_steps;        /* 100, bullet_cartpole.py:326                */
+    int32_t done_on_bounds;      /* restore the commented check :243-253 (0)   */
+    float   pos_threshold;       /* 3.0, :58                                   */
+    float   angle_threshold;     /* 0.35, :62                                  */
+    float   tan_angle_threshold; /* tan(angle_threshold), host-computed        */
+    float   sin_angle_threshold; /* sin(angle_threshold), host-computed        */
+    int32_t autoreset;           /* reset done envs inside cp_step (0)         */
+    int32_t bump_mode;           /* CP_BUMP_PHILOX or CP_BUMP_HOST             */
+    uint64_t seed;               /* Philox key                                 */
+    int64_t env_id_offset;       /* global id of env 0 (rank * B when sharded) */
+    cp_physics phys;
+} cp_config;
+
+#define CP_BUMP_PHILOX 0   /* theta = 2*pi*U, U from Philox4x32-10(seed; env, episode, k) */
+#define CP_BUMP_HOST   1   /* parity mode: host supplies the 60 bump forces per env      */
+
+#define CP_ACTION_CONTINUOUS 0
+#define CP_ACTION_DISCRETE   1
+
+typedef struct cp_handle cp_handle;
+
+/* Fill `cfg` with the reference defaults (bullet_cartpole.py:15-40 + URDFs). */
+void cp_default_config(cp_config* cfg);
+
+/* Replaces BulletCartpole.__init__ (bullet_cartpole.py:50-167): p.connect,
+ * p.setGravity, 5x p.loadURDF.  Allocates the per-env SoA state on `device`
+ * (HBM) and puts every env at its spawn pose with zero pending force. */
+int  cp_create(const cp_config* cfg, int device, cp_handle** out);
+void cp_destroy(cp_handle* h);
+const char* cp_last_error(const cp_handle* h);   /* h may be NULL */
+int  cp_abi_version(void);
+
+/* Replaces BulletCartpole.reset (bullet_cartpole.py:313-346): for every env with
+ * env_mask[i] != 0 (env_mask NULL = all): 4x resetBasePositionAndOrientation,
+ * 100 settle stepSimulation, 30x (stepSimulation + bump cart + bump cart2),
+ * then obs[r] = (pose cart, pose pole) for all r.  Pending forces survive the
+ * reset, as in pybullet.  obs_out [B][R][2][7] (rows of unmasked envs are left
+ * untouched).  env_mask is a device pointer. */
+int cp_reset(cp_handle* h, const uint8_t* env_mask, float* obs_out, void* stream);
+
+/* Replaces BulletCartpole.step (bullet_cartpole.py:178-275): R x S substeps,
+ * each followed by applyExternalForce on cart/cart2 (LINK_FRAME, at the COM),
+ * obs captured at the end of each repeat, steps += 1, done at max_episode_len
+ * (and bounds if enabled), reward 1.0.  An env that is already done returns
+ * its last obs, reward 0, done 1 and is not simulated (:179-181).  With
+ * autoreset, envs that finish are reset in the same call: obs_out then holds
+ * the fresh episode's first obs and terminal_obs_out (may be NULL) the
+ * finishing obs.  All pointers are device pointers; terminal_obs_out and
+ * pole_readback_out may be NULL. */
+int cp_step(cp_handle* h, const void* actions, int action_kind,
+            float* obs_out, float* reward_out, uint8_t* done_out,
+            float* terminal_obs_out, void* stream);
+
+/* Optional per-substep 12-state readback of both poles (bullet_cartpole.py:212-234,
+ * exposed there as monkey_positions / monkey_velocities):
+ * float32 [B][2 poles][R][S][4][3] = (xyz, rpy, linvel, angvel).  Enabled when
+ * `readback_out` is non-NULL on the next cp_step; pass NULL to disable.
+ * `reference_bug` != 0 reproduces :224 (pole2 rows read pole's velocity). */
+int cp_set_readback(cp_handle* h, float* readback_out, int reference_bug);
+
+/* Parity mode (bump_mode == CP_BUMP_HOST): the 2*initial_force_steps bump
+ * forces per env in LINK frame, float32 [B][initial_force_steps][2 carts][2],
+ * in the reference's draw order (cart then cart2 per bump step, :331-332).
+ * Device pointer; copied into the handle (used by every later reset). */
+int cp_set_bump_forces(cp_handle* h, const float* forces, void* stream);
+
+/* Full env state, SoA float32 [CP_STATE_FIELDS][B] (device pointers). */
+int cp_get_state(cp_handle* h, float* state_out, void* stream);
+int cp_set_state(cp_handle* h, const float* state_in, void* stream);
+
+/* Last completed episode per env: return (float32 [B]) and length (int32 [B]);
+ * either pointer may be NULL.  Feeds the RCCL return histogram. */
+int cp_episode_returns(cp_handle* h, float* returns_out, int32_t* lengths_out, void* stream);
+
+/* Diagnostics: per-env count of contact rows dropped by the CP_MAX_* caps since
+ * creation (int32 [B], device).  0 everywhere in normal operation. */
+int cp_overflow_counts(cp_handle* h, int32_t* out, void* stream);
+
+/* Kernel timing with HIP events recorded on the launch stream around every
+ * step-kernel and reset-kernel launch of the next `max_launches` cp_step /
+ * cp_reset calls (bench.py's roofline).  cp_timing_end synchronises on the last
+ * event and returns the summed durations (ms) and launch counts.  Not for use
+ * inside hipGraph capture. */
+int cp_timing_begin(cp_handle* h, int max_launches);
+int cp_timing_end(cp_handle* h, double* step_ms, int32_t* step_launches, double* reset_ms,
+                  int32_t* reset_launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CARTPOLE_AMD_H */

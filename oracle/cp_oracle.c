@@ -1,0 +1,1112 @@
+/*
+ * cp_oracle.c — CPU restatement of the batched cartpole++ hot path.
+ * TEST INFRASTRUCTURE ONLY (see cp_oracle.h): the parity oracle for the HIP
+ * kernel and the CPU baseline of bench.py.  Never linked by the product.
+ *
+ * Control flow follows the reference env:
+ *   reset  bullet_cartpole.py:313-346 (+ bump_cart :348-352, random_force_in_plane :354-359)
+ *   step   bullet_cartpole.py:178-275 (force applied AFTER each substep :199-207)
+ *   obs    bullet_cartpole.py:298-311 (+ state_fields_of_pose_of :43-45)
+ * Physics restates the Bullet step the scene exercises (SURVEY.md §8a rows a8-a10,
+ * all [ext]; parity vs pybullet is UNPINNED) — the exact model is DESIGN.md
+ * §Physics model.  Scene constants come from models/{ground,cart,pole,cart2,pole2}.urdf.
+ *
+ * Numerics: every multiply-add that the HIP kernel fuses is written here as an
+ * explicit fma, the file is compiled with -ffp-contract=off, and the few
+ * transcendentals are own polynomials, so the fp32 build reproduces the kernel
+ * bit for bit.  ORC_DOUBLE builds the same algorithm in fp64.
+ */
+#include "cp_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef ORC_DEBUG
+#include <stdio.h>
+#endif
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#ifdef ORC_DOUBLE
+typedef double real;
+#define FMA fma
+#define SQRT sqrt
+#define FABS fabs
+#else
+typedef float real;
+#define FMA fmaf
+#define SQRT sqrtf
+#define FABS fabsf
+#endif
+#define RC(x) ((real)(x))
+
+int orc_sizeof_real(void) { return (int)sizeof(real); }
+
+/* ------------------------------------------------------------------ vectors */
+typedef struct { real x, y, z; } v3;
+
+static inline v3 mk(real x, real y, real z) { v3 r = {x, y, z}; return r; }
+static inline v3 add(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline v3 sub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline v3 scl(v3 a, real s) { return mk(a.x * s, a.y * s, a.z * s); }
+static inline v3 neg(v3 a) { return mk(-a.x, -a.y, -a.z); }
+/* a + b*s */
+static inline v3 madd(v3 a, v3 b, real s) { return mk(FMA(b.x, s, a.x), FMA(b.y, s, a.y), FMA(b.z, s, a.z)); }
+static inline real dot(v3 a, v3 b) { return FMA(a.x, b.x, FMA(a.y, b.y, a.z * b.z)); }
+static inline v3 cross(v3 a, v3 b) {
+    return mk(FMA(a.y, b.z, -(a.z * b.y)), FMA(a.z, b.x, -(a.x * b.z)), FMA(a.x, b.y, -(a.y * b.x)));
+}
+static inline real comp(v3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+
+/* box axes from a unit quaternion (x,y,z,w): ax[i] = world direction of local axis i */
+static void quat_axes(const real q[4], v3 ax[3]) {
+    real x = q[0], y = q[1], z = q[2], w = q[3];
+    real x2 = x + x, y2 = y + y, z2 = z + z;
+    real xx = x * x2, yy = y * y2, zz = z * z2;
+    real xy = x * y2, xz = x * z2, yz = y * z2;
+    real wx = w * x2, wy = w * y2, wz = w * z2;
+    ax[0] = mk(RC(1) - (yy + zz), xy + wz, xz - wy);
+    ax[1] = mk(xy - wz, RC(1) - (xx + zz), yz + wx);
+    ax[2] = mk(xz + wy, yz - wx, RC(1) - (xx + yy));
+}
+/* local -> world: ax0*l.x + ax1*l.y + ax2*l.z */
+static inline v3 rot(const v3 ax[3], v3 l) {
+    return mk(FMA(ax[0].x, l.x, FMA(ax[1].x, l.y, ax[2].x * l.z)),
+              FMA(ax[0].y, l.x, FMA(ax[1].y, l.y, ax[2].y * l.z)),
+              FMA(ax[0].z, l.x, FMA(ax[1].z, l.y, ax[2].z * l.z)));
+}
+static inline v3 rot_t(const v3 ax[3], v3 w) { return mk(dot(ax[0], w), dot(ax[1], w), dot(ax[2], w)); }
+
+/* world inverse inertia M = sum_k iI[k] ax_k ax_k^T, stored xx xy xz yy yz zz */
+static void world_inv_inertia(const v3 ax[3], const float iI[3], real M[6]) {
+    v3 t0 = scl(ax[0], (real)iI[0]), t1 = scl(ax[1], (real)iI[1]), t2 = scl(ax[2], (real)iI[2]);
+    M[0] = FMA(t0.x, ax[0].x, FMA(t1.x, ax[1].x, t2.x * ax[2].x));
+    M[1] = FMA(t0.x, ax[0].y, FMA(t1.x, ax[1].y, t2.x * ax[2].y));
+    M[2] = FMA(t0.x, ax[0].z, FMA(t1.x, ax[1].z, t2.x * ax[2].z));
+    M[3] = FMA(t0.y, ax[0].y, FMA(t1.y, ax[1].y, t2.y * ax[2].y));
+    M[4] = FMA(t0.y, ax[0].z, FMA(t1.y, ax[1].z, t2.y * ax[2].z));
+    M[5] = FMA(t0.z, ax[0].z, FMA(t1.z, ax[1].z, t2.z * ax[2].z));
+}
+static inline v3 symv(const real M[6], v3 v) {
+    return mk(FMA(M[0], v.x, FMA(M[1], v.y, M[2] * v.z)),
+              FMA(M[1], v.x, FMA(M[3], v.y, M[4] * v.z)),
+              FMA(M[2], v.x, FMA(M[4], v.y, M[5] * v.z)));
+}
+
+/* --------------------------------------------------------- own transcendentals */
+static inline void sincos_small(real x, real* s, real* c) {
+    /* Taylor through x^9 / x^8; used for |x| <= pi/4 */
+    real x2 = x * x;
+    real p = FMA(x2, RC(2.7557319223985893e-6), RC(-1.9841269841269841e-4));
+    p = FMA(x2, p, RC(8.3333333333333333e-3));
+    p = FMA(x2, p, RC(-1.6666666666666667e-1));
+    *s = FMA(x * x2, p, x);
+    real q = FMA(x2, RC(2.4801587301587302e-5), RC(-1.3888888888888889e-3));
+    q = FMA(x2, q, RC(4.1666666666666667e-2));
+    q = FMA(x2, q, RC(-0.5));
+    *c = FMA(x2, q, RC(1.0));
+}
+
+/* sin/cos of 2*pi*u for u in [0,1) (bump direction, bullet_cartpole.py:355) */
+static void sincos_turns(real u, real* s_out, real* c_out) {
+    real y = u * RC(4.0);
+    int q = (int)y;
+    if (q > 3) q = 3;
+    real f = y - (real)q;
+    real x = (f - RC(0.5)) * RC(1.5707963267948966);
+    real s, c;
+    sincos_small(x, &s, &c);
+    real S = (s + c) * RC(0.7071067811865476);
+    real C = (c - s) * RC(0.7071067811865476);
+    switch (q) {
+        case 0: *s_out = S; *c_out = C; break;
+        case 1: *s_out = C; *c_out = -S; break;
+        case 2: *s_out = -S; *c_out = -C; break;
+        default: *s_out = -C; *c_out = S; break;
+    }
+}
+void orc_sincos_turns(float u, float* s, float* c) {
+    real rs, rc;
+    sincos_turns((real)u, &rs, &rc);
+    *s = (float)rs;
+    *c = (float)rc;
+}
+
+/* atan on [0, inf) (Cephes-style reduction + polynomial) */
+static real atan_pos(real z) {
+    real base = RC(0);
+    if (z > RC(2.414213562373095)) {
+        base = RC(1.5707963267948966);
+        z = RC(-1.0) / z;
+    } else if (z > RC(0.4142135623730950)) {
+        base = RC(0.7853981633974483);
+        z = (z - RC(1.0)) / (z + RC(1.0));
+    }
+    real z2 = z * z;
+    real p = FMA(z2, RC(8.05374449538e-2), RC(-1.38776856032e-1));
+    p = FMA(z2, p, RC(1.99777106478e-1));
+    p = FMA(z2, p, RC(-3.33329491539e-1));
+    return base + FMA(z * z2, p, z);
+}
+static real atan2_own(real y, real x) {
+    if (x == RC(0) && y == RC(0)) return RC(0);
+    real ax = FABS(x), ay = FABS(y);
+    real r = (ay <= ax) ? atan_pos(ay / ax) : RC(1.5707963267948966) - atan_pos(ax / ay);
+    if (x < RC(0)) r = RC(3.141592653589793) - r;
+    if (y < RC(0)) r = -r;
+    return r;
+}
+/* pybullet getEulerFromQuaternion (roll, pitch, yaw) [ext: recalled formula] */
+static void quat_euler(const real q[4], real rpy[3]) {
+    real x = q[0], y = q[1], z = q[2], w = q[3];
+    real sqw = w * w, sqx = x * x, sqy = y * y, sqz = z * z;
+    rpy[0] = atan2_own(RC(2) * FMA(y, z, w * x), ((sqw - sqx) - sqy) + sqz);
+    real sarg = RC(-2) * FMA(x, z, -(w * y));
+    if (sarg <= RC(-1)) rpy[1] = RC(-1.5707963267948966);
+    else if (sarg >= RC(1)) rpy[1] = RC(1.5707963267948966);
+    else rpy[1] = atan2_own(sarg, SQRT(FMA(-sarg, sarg, RC(1))));
+    rpy[2] = atan2_own(RC(2) * FMA(x, y, w * z), ((sqw + sqx) - sqy) - sqz);
+}
+
+/* ------------------------------------------------------------------ Philox */
+void orc_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
+    uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+    uint32_t k0 = key_in[0], k1 = key_in[1];
+    for (int r = 0; r < 10; ++r) {
+        if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* ------------------------------------------------------------ scene / config */
+void orc_default_config(cp_config* c) {
+    memset(c, 0, sizeof(*c));
+    c->num_envs = 1;
+    c->action_repeats = 2;           /* bullet_cartpole.py:23 */
+    c->steps_per_repeat = 1;         /* :25 */
+    c->max_episode_len = 200;        /* :31 */
+    c->action_force = 50.0f;         /* :18 */
+    c->initial_force = 200.0f;       /* :20 */
+    c->random_theta = 1;             /* :22 */
+    c->initial_force_steps = 30;     /* :76 */
+    c->settle_steps = 100;           /* :326 */
+    c->done_on_bounds = 0;
+    c->pos_threshold = 3.0f;         /* :58 */
+    c->angle_threshold = 0.35f;      /* :62 */
+    c->tan_angle_threshold = (float)tan(0.35f);
+    c->sin_angle_threshold = (float)sin(0.35f);
+    c->autoreset = 0;
+    c->bump_mode = CP_BUMP_PHILOX;
+    c->seed = 0;
+    c->env_id_offset = 0;
+    cp_physics* p = &c->phys;
+    p->dt = (float)(1.0 / 240.0);
+    p->inv_dt = (float)240.0;
+    p->gravity[0] = 0.0f; p->gravity[1] = 0.0f; p->gravity[2] = -9.81f;  /* :152 */
+    p->lin_damping = 0.04f;
+    p->ang_damping = 0.04f;
+    p->erp = 0.2f;
+    p->contact_margin = 0.02f;
+    p->residual_threshold = 1e-7f;
+    p->solver_iterations = 50;
+    p->edge_bias = 1e-4f;
+    p->max_angular_step = (float)(0.25 * 3.141592653589793);
+    p->warmstart = 0.85f;
+    /* models/ground.urdf: static box 3 x 3 x 0.1, no <contact> -> default friction 0.5 */
+    const double he[5][3] = {{1.5, 1.5, 0.05}, {0.1, 0.1, 0.025}, {0.005, 0.005, 0.25},
+                             {0.1, 0.1, 0.025}, {0.005, 0.005, 0.25}};
+    const double mass[5] = {0.0, 1.0, 5.0, 1.0, 5.0};
+    const double inert[5][3] = {{0, 0, 0},
+                                {0.0035416666666, 0.0035416666666, 0.0066666666666},
+                                {0.104208333333333, 0.104208333333333, 0.00008333333333},
+                                {0.0035416666666, 0.0035416666666, 0.0066666666666},
+                                {0.104208333333333, 0.104208333333333, 0.00008333333333}};
+    const double mu[5] = {0.5, 0.0, 1.0, 0.0, 1.0};
+    const double spawn[5][3] = {{0, 0, 0}, {0, 0, 0.08}, {0, 0, 0.35}, {1, 0, 0.08}, {1, 0, 0.35}};
+    for (int b = 0; b < 5; ++b) {
+        for (int k = 0; k < 3; ++k) {
+            p->half_extents[b][k] = (float)he[b][k];
+            p->inertia[b][k] = (float)inert[b][k];
+            p->inv_inertia[b][k] = inert[b][k] > 0 ? (float)(1.0 / inert[b][k]) : 0.0f;
+            p->spawn_pos[b][k] = (float)spawn[b][k];
+        }
+        p->inv_mass[b] = mass[b] > 0 ? (float)(1.0 / mass[b]) : 0.0f;
+        p->friction[b] = (float)mu[b];
+    }
+}
+
+static const int PAIR_A[CP_NUM_PAIRS] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3};
+static const int PAIR_B[CP_NUM_PAIRS] = {1, 2, 3, 4, 2, 3, 4, 3, 4, 4};
+
+/* --------------------------------------------------------------- simulation */
+typedef struct {
+    v3 x[CP_NUM_DYN];
+    real q[CP_NUM_DYN][4];
+    v3 v[CP_NUM_DYN], w[CP_NUM_DYN];
+    v3 f[CP_NUM_DYN];          /* pending world force */
+    v3 ax[CP_NUM_DYN][3];
+    real M[CP_NUM_DYN][6];
+    uint32_t ws_id[CP_NUM_PAIRS];    /* warm-start cache (4 packed feature ids per pair) */
+    real ws_lam[CP_NUM_PAIRS][4];
+} sim_t;
+
+typedef struct { v3 n; int cnt, base, fcnt, fbase; real mu; } manifold_t;
+typedef struct { v3 rb; real inv_eff, target, lam; int id; } point_t;
+typedef struct { real lam1, lam2, inv_eff1, inv_eff2; } fpoint_t;
+
+/* collision shape accessor: body g (0 = ground, static at the origin, identity axes) */
+typedef struct { v3 c; v3 ax[3]; real h[3]; } box_t;
+
+static void get_box(const sim_t* S, const cp_physics* P, int g, box_t* b) {
+    for (int k = 0; k < 3; ++k) b->h[k] = (real)P->half_extents[g][k];
+    if (g == 0) {
+        b->c = mk(RC(0), RC(0), RC(0));
+        b->ax[0] = mk(RC(1), RC(0), RC(0));
+        b->ax[1] = mk(RC(0), RC(1), RC(0));
+        b->ax[2] = mk(RC(0), RC(0), RC(1));
+    } else {
+        b->c = S->x[g - 1];
+        for (int k = 0; k < 3; ++k) b->ax[k] = S->ax[g - 1][k];
+    }
+}
+
+typedef struct { real u, v, n; int id; } cand_t;
+
+/* Face contact: reference face (axis ri, outward normal nr) of box R against the
+ * most anti-parallel face of box I.  Candidate points, in canonical order:
+ *   C1 incident face vertices inside the reference rectangle,
+ *   C2 reference rectangle corners strictly inside the incident face,
+ *   C3 incident-edge x rectangle-side crossings.
+ * Keep depth <= margin; reduce > 4 to 4 (deepest, farthest, max/min area). */
+static int face_contact(const box_t* R, int ri, v3 nr, const box_t* I, real margin,
+                        v3 pts[4], real dist[4], int fid[4]) {
+    int r1 = (ri + 1) % 3, r2 = (ri + 2) % 3;
+    v3 fc = madd(R->c, nr, R->h[ri]);
+    v3 u = R->ax[r1], v = R->ax[r2];
+    real hu = R->h[r1], hv = R->h[r2];
+    /* incident face */
+    real e0 = dot(nr, I->ax[0]), e1d = dot(nr, I->ax[1]), e2d = dot(nr, I->ax[2]);
+    int j = 0;
+    real best = FABS(e0);
+    if (FABS(e1d) > best) { j = 1; best = FABS(e1d); }
+    if (FABS(e2d) > best) { j = 2; }
+    real ej = (j == 0) ? e0 : (j == 1 ? e1d : e2d);
+    real isg = (ej > RC(0)) ? RC(-1) : RC(1);
+    v3 ic = madd(I->c, I->ax[j], isg * I->h[j]);
+    int j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+    v3 E1 = scl(I->ax[j1], I->h[j1]);
+    v3 E2 = scl(I->ax[j2], I->h[j2]);
+    v3 icr = sub(ic, fc);
+    real cu = dot(icr, u), cv = dot(icr, v), cn = dot(icr, nr);
+    real e1u = dot(E1, u), e1v = dot(E1, v), e1n = dot(E1, nr);
+    real e2u = dot(E2, u), e2v = dot(E2, v), e2n = dot(E2, nr);
+
+    cand_t P[4];
+    P[0].id = 0; P[1].id = 1; P[2].id = 2; P[3].id = 3;
+    P[0].u = (cu + e1u) + e2u; P[0].v = (cv + e1v) + e2v; P[0].n = (cn + e1n) + e2n;
+    P[1].u = (cu - e1u) + e2u; P[1].v = (cv - e1v) + e2v; P[1].n = (cn - e1n) + e2n;
+    P[2].u = (cu - e1u) - e2u; P[2].v = (cv - e1v) - e2v; P[2].n = (cn - e1n) - e2n;
+    P[3].u = (cu + e1u) - e2u; P[3].v = (cv + e1v) - e2v; P[3].n = (cn + e1n) - e2n;
+
+    cand_t cand[24];
+    int nc = 0;
+    /* C1 */
+    for (int k = 0; k < 4; ++k)
+        if (FABS(P[k].u) <= hu && FABS(P[k].v) <= hv && P[k].n <= margin) cand[nc++] = P[k];
+    /* C2 */
+    real det = FMA(e1u, e2v, -(e1v * e2u));
+    real idet = RC(1) / det;
+    for (int c = 0; c < 4; ++c) {
+        real X = (c == 0 || c == 3) ? hu : -hu;
+        real Y = (c < 2) ? hv : -hv;
+        real ru = X - cu, rv = Y - cv;
+        real al = FMA(ru, e2v, -(rv * e2u)) * idet;
+        real be = FMA(e1u, rv, -(e1v * ru)) * idet;
+        if (FABS(al) < RC(1) && FABS(be) < RC(1)) {
+            real dn = FMA(be, e2n, FMA(al, e1n, cn));
+            if (dn <= margin) { cand[nc].u = X; cand[nc].v = Y; cand[nc].n = dn; cand[nc].id = 4 + c; ++nc; }
+        }
+    }
+    /* C3 */
+    for (int k = 0; k < 4; ++k) {
+        cand_t p = P[k], q = P[(k + 1) & 3];
+        for (int s = 0; s < 4; ++s) {
+            real lim = (s & 1) ? ((s < 2) ? -hu : -hv) : ((s < 2) ? hu : hv);
+            real pc = (s < 2) ? p.u : p.v, qc = (s < 2) ? q.u : q.v;
+            real dp = pc - lim, dq = qc - lim;
+            if (!((dp < RC(0) && dq > RC(0)) || (dp > RC(0) && dq < RC(0)))) continue;
+            real t = dp / (dp - dq);
+            cand_t x;
+            if (s < 2) {
+                x.u = lim;
+                x.v = FMA(q.v - p.v, t, p.v);
+                if (!(FABS(x.v) <= hv)) continue;
+            } else {
+                x.v = lim;
+                x.u = FMA(q.u - p.u, t, p.u);
+                if (!(FABS(x.u) <= hu)) continue;
+            }
+            x.n = FMA(q.n - p.n, t, p.n);
+            x.id = 8 + 4 * k + s;
+            if (x.n <= margin) cand[nc++] = x;
+        }
+    }
+    int sel[24];
+    for (int k = 0; k < nc; ++k) sel[k] = 1;
+    if (nc > 4) {
+        for (int k = 0; k < nc; ++k) sel[k] = 0;
+        int i0 = 0;
+        for (int k = 1; k < nc; ++k) if (cand[k].n < cand[i0].n) i0 = k;
+        int i1 = -1; real bd = RC(0);
+        for (int k = 0; k < nc; ++k) {
+            if (k == i0) continue;
+            real du = cand[k].u - cand[i0].u, dv = cand[k].v - cand[i0].v;
+            real d2 = FMA(du, du, dv * dv);
+            if (i1 < 0 || d2 > bd) { i1 = k; bd = d2; }
+        }
+        real ex = cand[i1].u - cand[i0].u, ey = cand[i1].v - cand[i0].v;
+        int i2 = -1, i3 = -1; real ba = RC(0), bb = RC(0);
+        for (int k = 0; k < nc; ++k) {
+            if (k == i0 || k == i1) continue;
+            real ar = FMA(ex, cand[k].v - cand[i0].v, -(ey * (cand[k].u - cand[i0].u)));
+            if (i2 < 0 || ar > ba) { i2 = k; ba = ar; }
+        }
+        for (int k = 0; k < nc; ++k) {
+            if (k == i0 || k == i1 || k == i2) continue;
+            real ar = FMA(ex, cand[k].v - cand[i0].v, -(ey * (cand[k].u - cand[i0].u)));
+            if (i3 < 0 || ar < bb) { i3 = k; bb = ar; }
+        }
+        sel[i0] = sel[i1] = sel[i2] = sel[i3] = 1;
+    }
+    int m = 0;
+    for (int k = 0; k < nc; ++k) {
+        if (!sel[k]) continue;
+        v3 pw = madd(madd(madd(fc, u, cand[k].u), v, cand[k].v), nr, cand[k].n * RC(0.5));
+        pts[m] = pw;
+        dist[m] = cand[k].n;
+        fid[m] = cand[k].id;
+        ++m;
+    }
+    return m;
+}
+
+/* Box-box narrowphase (separating-axis test over 15 axes + face clipping or
+ * edge-edge closest points).  Normal n points from A to B.  Returns #points. */
+static int box_box(const box_t* A, const box_t* B, real margin, real edge_bias,
+                   v3* n_out, v3 pts[4], real dist[4], int ids[4]) {
+    v3 d = sub(B->c, A->c);
+    real C[3][3], AC[3][3], da[3], db[3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) { C[i][j] = dot(A->ax[i], B->ax[j]); AC[i][j] = FABS(C[i][j]); }
+    for (int i = 0; i < 3; ++i) { da[i] = dot(d, A->ax[i]); db[i] = dot(d, B->ax[i]); }
+
+    real best = RC(0);
+    int kind = 0, bi = 0, bj = 0;   /* kind 0: face of A, 1: face of B, 2: edge */
+    v3 bax = mk(RC(0), RC(0), RC(0));
+    for (int i = 0; i < 3; ++i) {
+        real pr = FMA(B->h[0], AC[i][0], FMA(B->h[1], AC[i][1], B->h[2] * AC[i][2]));
+        real s = FABS(da[i]) - (A->h[i] + pr);
+        if (s > margin) return 0;
+        if (i == 0 || s > best) { best = s; kind = 0; bi = i; }
+    }
+    for (int j = 0; j < 3; ++j) {
+        real pr = FMA(A->h[0], AC[0][j], FMA(A->h[1], AC[1][j], A->h[2] * AC[2][j]));
+        real s = FABS(db[j]) - (B->h[j] + pr);
+        if (s > margin) return 0;
+        if (s > best) { best = s; kind = 1; bj = j; }
+    }
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) {
+            v3 ax = cross(A->ax[i], B->ax[j]);
+            real L2 = dot(ax, ax);
+            if (L2 < RC(1e-6)) continue;
+            real L = SQRT(L2);
+            int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+            real ra = FMA(A->h[i1], AC[i2][j], A->h[i2] * AC[i1][j]);
+            real rb = FMA(B->h[j1], AC[i][j2], B->h[j2] * AC[i][j1]);
+            real s = (FABS(dot(d, ax)) - (ra + rb)) / L;
+            if (s > margin) return 0;
+            if (s > best + edge_bias) { best = s; kind = 2; bi = i; bj = j; bax = ax; }
+        }
+    }
+    if (kind == 0) {
+        real sg = (da[bi] >= RC(0)) ? RC(1) : RC(-1);
+        v3 nr = scl(A->ax[bi], sg);
+        *n_out = nr;
+        int m = face_contact(A, bi, nr, B, margin, pts, dist, ids);
+        for (int k = 0; k < m; ++k) ids[k] += bi * 32;
+        return m;
+    }
+    if (kind == 1) {
+        real sg = (db[bj] >= RC(0)) ? RC(-1) : RC(1);
+        v3 nr = scl(B->ax[bj], sg);
+        *n_out = neg(nr);
+        int m = face_contact(B, bj, nr, A, margin, pts, dist, ids);
+        for (int k = 0; k < m; ++k) ids[k] += (3 + bj) * 32;
+        return m;
+    }
+    /* edge-edge */
+    real L = SQRT(dot(bax, bax));
+    v3 w = mk(bax.x / L, bax.y / L, bax.z / L);
+    if (dot(w, d) < RC(0)) w = neg(w);
+    *n_out = w;
+    v3 pa = A->c, pb = B->c;
+    for (int k = 0; k < 3; ++k) {
+        if (k == bi) continue;
+        real sg = (dot(A->ax[k], w) > RC(0)) ? RC(1) : RC(-1);
+        pa = madd(pa, A->ax[k], sg * A->h[k]);
+    }
+    for (int k = 0; k < 3; ++k) {
+        if (k == bj) continue;
+        real sg = (dot(B->ax[k], w) > RC(0)) ? RC(-1) : RC(1);
+        pb = madd(pb, B->ax[k], sg * B->h[k]);
+    }
+    v3 ua = A->ax[bi], ub = B->ax[bj];
+    v3 r = sub(pb, pa);
+    real c = dot(ua, ub), ar = dot(ua, r), br = dot(ub, r);
+    real den = FMA(-c, c, RC(1));
+    real s = FMA(-c, br, ar) / den;
+    real t = FMA(c, ar, -br) / den;
+    real ha = A->h[bi], hb = B->h[bj];
+    s = s > ha ? ha : (s < -ha ? -ha : s);
+    t = t > hb ? hb : (t < -hb ? -hb : t);
+    v3 qa = madd(pa, ua, s), qb = madd(pb, ub, t);
+    pts[0] = scl(add(qa, qb), RC(0.5));
+    dist[0] = best;
+    ids[0] = 6 * 32 + 3 * bi + bj;
+    return 1;
+}
+
+static void plane_space(v3 n, v3* t1, v3* t2) {
+    if (FABS(n.z) > RC(0.7071067811865476)) {
+        real a = FMA(n.y, n.y, n.z * n.z);
+        real k = RC(1) / SQRT(a);
+        *t1 = mk(RC(0), -(n.z * k), n.y * k);
+        *t2 = mk(a * k, -(n.x * t1->z), n.x * t1->y);
+    } else {
+        real a = FMA(n.x, n.x, n.y * n.y);
+        real k = RC(1) / SQRT(a);
+        *t1 = mk(-(n.y * k), n.x * k, RC(0));
+        *t2 = mk(-(n.z * t1->y), n.z * t1->x, a * k);
+    }
+}
+
+/* effective inverse mass along direction t for pair (a,b) at lever arm rb */
+static real row_k(const sim_t* S, const cp_physics* P, int a, int b, v3 rb, v3 t) {
+    int db_ = b - 1;
+    real imb = (real)P->inv_mass[b];
+    v3 rbt = cross(rb, t);
+    v3 ib = symv(S->M[db_], rbt);
+    if (a == 0) return imb + dot(rbt, ib);
+    int da_ = a - 1;
+    real ima = (real)P->inv_mass[a];
+    v3 ra = add(rb, sub(S->x[db_], S->x[da_]));
+    v3 rat = cross(ra, t);
+    v3 ia = symv(S->M[da_], rat);
+    return ((ima + imb) + dot(rat, ia)) + dot(rbt, ib);
+}
+
+/* one PGS row (normal when lo==0 && hi<0 sentinel, friction otherwise) */
+static real solve_row(sim_t* S, const cp_physics* P, int a, int b, v3 rb, v3 t,
+                      real inv_eff, real target, real* lam, int friction, real bound) {
+    int db_ = b - 1;
+    real imb = (real)P->inv_mass[b];
+    v3 rbt = cross(rb, t);
+    v3 ib = symv(S->M[db_], rbt);
+    real vn;
+    v3 ia = mk(0, 0, 0), rat = mk(0, 0, 0);
+    int da_ = a - 1;
+    if (a == 0) {
+        vn = dot(t, S->v[db_]) + dot(S->w[db_], rbt);
+    } else {
+        v3 ra = add(rb, sub(S->x[db_], S->x[da_]));
+        rat = cross(ra, t);
+        ia = symv(S->M[da_], rat);
+        vn = (dot(t, sub(S->v[db_], S->v[da_])) + dot(S->w[db_], rbt)) - dot(S->w[da_], rat);
+    }
+    real e = target - vn;
+    real dl = e * inv_eff;
+    real l0 = *lam + dl;
+    real ln;
+    if (!friction) ln = l0 > RC(0) ? l0 : RC(0);
+    else ln = l0 > bound ? bound : (l0 < -bound ? -bound : l0);
+    dl = ln - *lam;
+    *lam = ln;
+    real sb = dl * imb;
+    S->v[db_] = madd(S->v[db_], t, sb);
+    S->w[db_] = madd(S->w[db_], ib, dl);
+    if (a != 0) {
+        real sa = dl * (real)P->inv_mass[a];
+        S->v[da_] = madd(S->v[da_], neg(t), sa);
+        S->w[da_] = madd(S->w[da_], neg(ia), dl);
+    }
+    return FABS(e * dl);
+}
+
+/* velocity change of an impulse lam along t at lever arm rb (warm start) */
+static void apply_impulse(sim_t* S, const cp_physics* P, int a, int b, v3 rb, v3 t, real lam) {
+    int db_ = b - 1;
+    v3 rbt = cross(rb, t);
+    v3 ib = symv(S->M[db_], rbt);
+    S->v[db_] = madd(S->v[db_], t, lam * (real)P->inv_mass[b]);
+    S->w[db_] = madd(S->w[db_], ib, lam);
+    if (a != 0) {
+        int da_ = a - 1;
+        v3 ra = add(rb, sub(S->x[db_], S->x[da_]));
+        v3 rat = cross(ra, t);
+        v3 ia = symv(S->M[da_], rat);
+        S->v[da_] = madd(S->v[da_], neg(t), lam * (real)P->inv_mass[a]);
+        S->w[da_] = madd(S->w[da_], neg(ia), lam);
+    }
+}
+
+/* one p.stepSimulation() of the scene (DESIGN.md §Physics model, steps 1-6) */
+static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* iters_out, int32_t* npts_out) {
+    const real dt = (real)P->dt, inv_dt = (real)P->inv_dt;
+    /* 1. orientation matrices, world inverse inertia */
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        quat_axes(S->q[d], S->ax[d]);
+        world_inv_inertia(S->ax[d], P->inv_inertia[d + 1], S->M[d]);
+    }
+    /* 2. narrowphase + row setup at the start-of-step poses */
+    manifold_t man[CP_NUM_PAIRS];
+    point_t pt[CP_MAX_POINTS];
+    fpoint_t fp[CP_MAX_FRICTION];
+    int used = 0, fused = 0;
+    for (int p = 0; p < CP_NUM_PAIRS; ++p) {
+        int a = PAIR_A[p], b = PAIR_B[p];
+        box_t A, B;
+        get_box(S, P, a, &A);
+        get_box(S, P, b, &B);
+        v3 n, pts[4];
+        real dist[4];
+        int ids[4];
+        int cnt = box_box(&A, &B, (real)P->contact_margin, (real)P->edge_bias, &n, pts, dist, ids);
+        int m = cnt < CP_MAX_POINTS - used ? cnt : CP_MAX_POINTS - used;
+        *overflow += cnt - m;
+        man[p].n = n;
+        man[p].cnt = m;
+        man[p].base = used;
+        man[p].mu = (real)P->friction[a] * (real)P->friction[b];
+        man[p].fcnt = 0;
+        man[p].fbase = fused;
+        for (int k = 0; k < m; ++k) {
+            point_t* q = &pt[used + k];
+            q->rb = sub(pts[k], S->x[b - 1]);
+            real K = row_k(S, P, a, b, q->rb, n);
+            q->inv_eff = RC(1) / K;
+            q->target = dist[k] > RC(0) ? -(dist[k] * inv_dt) : -(((real)P->erp * dist[k]) * inv_dt);
+            q->id = ids[k];
+            /* warm start: impulse of the same feature in the last substep */
+            real l0 = RC(0);
+            for (int j = 0; j < 4; ++j) {
+                if ((int)((S->ws_id[p] >> (8 * j)) & 0xFFu) == ids[k]) { l0 = S->ws_lam[p][j]; break; }
+            }
+            q->lam = (real)P->warmstart * l0;
+        }
+        if (man[p].mu > RC(0) && m > 0) {
+            int fm = m < CP_MAX_FRICTION - fused ? m : CP_MAX_FRICTION - fused;
+            *overflow += m - fm;
+            man[p].fcnt = fm;
+            v3 t1, t2;
+            plane_space(n, &t1, &t2);
+            for (int k = 0; k < fm; ++k) {
+                fpoint_t* f = &fp[fused + k];
+                f->inv_eff1 = RC(1) / row_k(S, P, a, b, pt[used + k].rb, t1);
+                f->inv_eff2 = RC(1) / row_k(S, P, a, b, pt[used + k].rb, t2);
+                f->lam1 = f->lam2 = RC(0);
+            }
+            fused += fm;
+        }
+        used += m;
+    }
+    /* 3. unconstrained velocity update: gravity + pending force + Bullet multibody
+     *    damping (-m v (k + k|v|), -I w (k + k|w|)) + gyroscopic term */
+    const real kl = (real)P->lin_damping, ka = (real)P->ang_damping;
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        int g = d + 1;
+        real im = (real)P->inv_mass[g];
+        v3 v = S->v[d], w = S->w[d], F = S->f[d];
+        real vlen = SQRT(dot(v, v));
+        real dv = FMA(kl, vlen, kl);
+        v3 acc = mk(FMA(-v.x, dv, FMA(F.x, im, (real)P->gravity[0])),
+                    FMA(-v.y, dv, FMA(F.y, im, (real)P->gravity[1])),
+                    FMA(-v.z, dv, FMA(F.z, im, (real)P->gravity[2])));
+        v3 wl = rot_t(S->ax[d], w);
+        v3 Iwl = mk((real)P->inertia[g][0] * wl.x, (real)P->inertia[g][1] * wl.y, (real)P->inertia[g][2] * wl.z);
+        v3 gl = cross(wl, Iwl);
+        v3 al = mk(-((real)P->inv_inertia[g][0] * gl.x), -((real)P->inv_inertia[g][1] * gl.y),
+                   -((real)P->inv_inertia[g][2] * gl.z));
+        v3 aw = rot(S->ax[d], al);
+        real wlen = SQRT(dot(w, w));
+        real dw = FMA(ka, wlen, ka);
+        v3 accw = mk(FMA(-w.x, dw, aw.x), FMA(-w.y, dw, aw.y), FMA(-w.z, dw, aw.z));
+        S->v[d] = madd(v, acc, dt);
+        S->w[d] = madd(w, accw, dt);
+    }
+    /* 4a. warm start: apply the cached normal impulses (row order) */
+    for (int p = 0; p < CP_NUM_PAIRS; ++p) {
+        int a = PAIR_A[p], b = PAIR_B[p];
+        for (int k = 0; k < man[p].cnt; ++k) {
+            point_t* q = &pt[man[p].base + k];
+            apply_impulse(S, P, a, b, q->rb, man[p].n, q->lam);
+        }
+    }
+    /* 4b. projected Gauss-Seidel: normal rows then friction rows per sweep */
+    int it = 0;
+    const int iters = P->solver_iterations;
+    const real thr = (real)P->residual_threshold;
+    if (used > 0) {
+        for (it = 0; it < iters;) {
+            real resid = RC(0);
+            for (int p = 0; p < CP_NUM_PAIRS; ++p) {
+                int a = PAIR_A[p], b = PAIR_B[p];
+                for (int k = 0; k < man[p].cnt; ++k) {
+                    point_t* q = &pt[man[p].base + k];
+                    real rr = solve_row(S, P, a, b, q->rb, man[p].n, q->inv_eff, q->target, &q->lam, 0, RC(0));
+#ifdef ORC_DEBUG
+                    if (getenv("ORC_DEBUG") && (it == 0 || it >= iters - 2)) fprintf(stderr, "  it %d pair %d k %d rr %g lam %g target %g rb %g %g %g n %g %g %g\n", it, p, k, (double)rr, (double)q->lam, (double)q->target, (double)q->rb.x, (double)q->rb.y, (double)q->rb.z, (double)man[p].n.x, (double)man[p].n.y, (double)man[p].n.z);
+#endif
+                    resid = resid + rr;
+                }
+            }
+            for (int p = 0; p < CP_NUM_PAIRS; ++p) {
+                if (man[p].fcnt == 0) continue;
+                int a = PAIR_A[p], b = PAIR_B[p];
+                v3 t1, t2;
+                plane_space(man[p].n, &t1, &t2);
+                for (int k = 0; k < man[p].fcnt; ++k) {
+                    point_t* q = &pt[man[p].base + k];
+                    fpoint_t* f = &fp[man[p].fbase + k];
+                    real bound = man[p].mu * q->lam;
+                    resid = resid + solve_row(S, P, a, b, q->rb, t1, f->inv_eff1, RC(0), &f->lam1, 1, bound);
+                    resid = resid + solve_row(S, P, a, b, q->rb, t2, f->inv_eff2, RC(0), &f->lam2, 1, bound);
+                }
+            }
+            ++it;
+#ifdef ORC_DEBUG
+            if (getenv("ORC_DEBUG")) fprintf(stderr, "it %d resid %g\n", it, (double)resid);
+#endif
+            if (resid <= thr) break;
+        }
+    }
+    /* 4c. refresh the warm-start cache */
+    for (int p = 0; p < CP_NUM_PAIRS; ++p) {
+        uint32_t idw = 0xFFFFFFFFu;
+        for (int k = 0; k < 4; ++k) {
+            if (k < man[p].cnt) {
+                point_t* q = &pt[man[p].base + k];
+                idw = (idw & ~(0xFFu << (8 * k))) | ((uint32_t)q->id << (8 * k));
+                S->ws_lam[p][k] = q->lam;
+            } else {
+                S->ws_lam[p][k] = RC(0);
+            }
+        }
+        S->ws_id[p] = idw;
+    }
+    /* 5. integrate positions (semi-implicit) and orientation (exponential map) */
+    const real hdt = RC(0.5) * dt;
+    const real c3 = ((dt * dt) * dt) * RC(0.020833333333);
+    const real maxang = (real)P->max_angular_step;
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        v3 v = S->v[d], w = S->w[d];
+        S->x[d] = madd(S->x[d], v, dt);
+        real ang = SQRT(dot(w, w));
+        if (ang * dt > maxang) ang = maxang * inv_dt;
+        real half = hdt * ang;
+        real sn, cs, s;
+        sincos_small(half, &sn, &cs);
+        if (ang < RC(0.001)) s = FMA(-c3, ang * ang, hdt);
+        else s = sn / ang;
+        real dx = w.x * s, dy = w.y * s, dz = w.z * s, dw = cs;
+        real* q = S->q[d];
+        real qx = q[0], qy = q[1], qz = q[2], qw = q[3];
+        real rw = FMA(dw, qw, -FMA(dx, qx, FMA(dy, qy, dz * qz)));
+        real rx = FMA(dw, qx, FMA(dx, qw, FMA(dy, qz, -(dz * qy))));
+        real ry = FMA(dw, qy, FMA(dy, qw, FMA(dz, qx, -(dx * qz))));
+        real rz = FMA(dw, qz, FMA(dz, qw, FMA(dx, qy, -(dy * qx))));
+        real n2 = FMA(rx, rx, FMA(ry, ry, FMA(rz, rz, rw * rw)));
+        real inv = RC(1) / SQRT(n2);
+        q[0] = rx * inv; q[1] = ry * inv; q[2] = rz * inv; q[3] = rw * inv;
+    }
+    /* 6. external forces are consumed by the step (pybullet clears them) */
+    for (int d = 0; d < CP_NUM_DYN; ++d) S->f[d] = mk(RC(0), RC(0), RC(0));
+    if (iters_out) *iters_out = it;
+    if (npts_out) *npts_out = used;
+}
+
+/* LINK_FRAME force at the link origin (= COM): world force = R(q) f, no torque
+ * (bullet_cartpole.py:202-207, :349-351).  Accumulates until the next step. */
+static void apply_force_link(sim_t* S, int d, real fx, real fy, real fz) {
+    v3 ax[3];
+    quat_axes(S->q[d], ax);
+    S->f[d] = add(S->f[d], rot(ax, mk(fx, fy, fz)));
+}
+
+/* ------------------------------------------------------------ world-level API */
+static void world_load(const orc_world* w, sim_t* S) {
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        S->x[d] = mk((real)w->pos[d][0], (real)w->pos[d][1], (real)w->pos[d][2]);
+        for (int k = 0; k < 4; ++k) S->q[d][k] = (real)w->quat[d][k];
+        S->v[d] = mk((real)w->vel[d][0], (real)w->vel[d][1], (real)w->vel[d][2]);
+        S->w[d] = mk((real)w->omega[d][0], (real)w->omega[d][1], (real)w->omega[d][2]);
+        S->f[d] = mk((real)w->pending[d][0], (real)w->pending[d][1], (real)w->pending[d][2]);
+    }
+    for (int p = 0; p < CP_NUM_PAIRS; ++p) {
+        S->ws_id[p] = w->ws_id[p];
+        for (int k = 0; k < 4; ++k) S->ws_lam[p][k] = (real)w->ws_lam[p][k];
+    }
+}
+static void world_store(orc_world* w, const sim_t* S) {
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        w->pos[d][0] = S->x[d].x; w->pos[d][1] = S->x[d].y; w->pos[d][2] = S->x[d].z;
+        for (int k = 0; k < 4; ++k) w->quat[d][k] = S->q[d][k];
+        w->vel[d][0] = S->v[d].x; w->vel[d][1] = S->v[d].y; w->vel[d][2] = S->v[d].z;
+        w->omega[d][0] = S->w[d].x; w->omega[d][1] = S->w[d].y; w->omega[d][2] = S->w[d].z;
+        w->pending[d][0] = S->f[d].x; w->pending[d][1] = S->f[d].y; w->pending[d][2] = S->f[d].z;
+    }
+    for (int p = 0; p < CP_NUM_PAIRS; ++p) {
+        w->ws_id[p] = S->ws_id[p];
+        for (int k = 0; k < 4; ++k) w->ws_lam[p][k] = S->ws_lam[p][k];
+    }
+}
+
+void orc_world_spawn(orc_world* w, const cp_config* cfg) {
+    memset(w, 0, sizeof(*w));
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        for (int k = 0; k < 3; ++k) w->pos[d][k] = cfg->phys.spawn_pos[d + 1][k];
+        w->quat[d][3] = 1.0;
+    }
+    for (int p = 0; p < CP_NUM_PAIRS; ++p) w->ws_id[p] = 0xFFFFFFFFu;
+}
+void orc_world_reset_pose(orc_world* w, int body, const double p[3], const double q[4]) {
+    int d = body - 1;
+    if (d < 0 || d >= CP_NUM_DYN) return;
+    for (int k = 0; k < 3; ++k) { w->pos[d][k] = (float)p[k]; w->vel[d][k] = 0; w->omega[d][k] = 0; }
+    for (int k = 0; k < 4; ++k) w->quat[d][k] = (float)q[k];
+}
+void orc_world_step(orc_world* w, const cp_config* cfg) {
+    sim_t S;
+    world_load(w, &S);
+    substep(&S, &cfg->phys, &w->overflow, &w->last_iterations, &w->last_points);
+    world_store(w, &S);
+}
+void orc_world_apply_force_link(orc_world* w, int body, double fx, double fy, double fz) {
+    int d = body - 1;
+    if (d < 0 || d >= CP_NUM_DYN) return;
+    sim_t S;
+    world_load(w, &S);
+    apply_force_link(&S, d, (real)(float)fx, (real)(float)fy, (real)(float)fz);
+    world_store(w, &S);
+}
+void orc_world_get_pose(const orc_world* w, int body, double out7[7]) {
+    int d = body - 1;
+    for (int k = 0; k < 3; ++k) out7[k] = w->pos[d][k];
+    for (int k = 0; k < 4; ++k) out7[3 + k] = w->quat[d][k];
+}
+void orc_world_get_velocity(const orc_world* w, int body, double out6[6]) {
+    int d = body - 1;
+    for (int k = 0; k < 3; ++k) { out6[k] = w->vel[d][k]; out6[3 + k] = w->omega[d][k]; }
+}
+void orc_world_get_euler(const orc_world* w, int body, double out3[3]) {
+    int d = body - 1;
+    real q[4], rpy[3];
+    for (int k = 0; k < 4; ++k) q[k] = (real)w->quat[d][k];
+    quat_euler(q, rpy);
+    for (int k = 0; k < 3; ++k) out3[k] = rpy[k];
+}
+
+/* -------------------------------------------------------------- env-level API */
+#define SF(e, f, i) ((e)->state[(size_t)(f) * (e)->B + (i)])
+
+static void env_load(const orc_envs* e, int i, sim_t* S) {
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        S->x[d] = mk(SF(e, CP_SF_BODY(d, 0), i), SF(e, CP_SF_BODY(d, 1), i), SF(e, CP_SF_BODY(d, 2), i));
+        for (int k = 0; k < 4; ++k) S->q[d][k] = SF(e, CP_SF_BODY(d, 3 + k), i);
+        S->v[d] = mk(SF(e, CP_SF_BODY(d, 7), i), SF(e, CP_SF_BODY(d, 8), i), SF(e, CP_SF_BODY(d, 9), i));
+        S->w[d] = mk(SF(e, CP_SF_BODY(d, 10), i), SF(e, CP_SF_BODY(d, 11), i), SF(e, CP_SF_BODY(d, 12), i));
+        S->f[d] = mk(RC(0), RC(0), RC(0));
+    }
+    for (int c = 0; c < 2; ++c)
+        S->f[2 * c] = mk(SF(e, CP_SF_PENDING(c, 0), i), SF(e, CP_SF_PENDING(c, 1), i), SF(e, CP_SF_PENDING(c, 2), i));
+    for (int p = 0; p < CP_NUM_PAIRS; ++p) {
+        memcpy(&S->ws_id[p], &SF(e, CP_SF_WS_ID(p), i), 4);
+        for (int k = 0; k < 4; ++k) S->ws_lam[p][k] = SF(e, CP_SF_WS_LAM(p, k), i);
+    }
+}
+static void env_store(orc_envs* e, int i, const sim_t* S) {
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        SF(e, CP_SF_BODY(d, 0), i) = (float)S->x[d].x;
+        SF(e, CP_SF_BODY(d, 1), i) = (float)S->x[d].y;
+        SF(e, CP_SF_BODY(d, 2), i) = (float)S->x[d].z;
+        for (int k = 0; k < 4; ++k) SF(e, CP_SF_BODY(d, 3 + k), i) = (float)S->q[d][k];
+        SF(e, CP_SF_BODY(d, 7), i) = (float)S->v[d].x;
+        SF(e, CP_SF_BODY(d, 8), i) = (float)S->v[d].y;
+        SF(e, CP_SF_BODY(d, 9), i) = (float)S->v[d].z;
+        SF(e, CP_SF_BODY(d, 10), i) = (float)S->w[d].x;
+        SF(e, CP_SF_BODY(d, 11), i) = (float)S->w[d].y;
+        SF(e, CP_SF_BODY(d, 12), i) = (float)S->w[d].z;
+    }
+    for (int c = 0; c < 2; ++c) {
+        SF(e, CP_SF_PENDING(c, 0), i) = (float)S->f[2 * c].x;
+        SF(e, CP_SF_PENDING(c, 1), i) = (float)S->f[2 * c].y;
+        SF(e, CP_SF_PENDING(c, 2), i) = (float)S->f[2 * c].z;
+    }
+    for (int p = 0; p < CP_NUM_PAIRS; ++p) {
+        memcpy(&SF(e, CP_SF_WS_ID(p), i), &S->ws_id[p], 4);
+        for (int k = 0; k < 4; ++k) SF(e, CP_SF_WS_LAM(p, k), i) = (float)S->ws_lam[p][k];
+    }
+}
+static int32_t get_i(const orc_envs* e, int f, int i) {
+    int32_t v;
+    memcpy(&v, &SF(e, f, i), 4);
+    return v;
+}
+static void set_i(orc_envs* e, int f, int i, int32_t v) { memcpy(&SF(e, f, i), &v, 4); }
+
+static void write_obs_row(const sim_t* S, float* dst /* 14 floats */) {
+    for (int o = 0; o < 2; ++o) {   /* o=0 cart (dyn 0), o=1 pole (dyn 1) */
+        dst[o * 7 + 0] = (float)S->x[o].x;
+        dst[o * 7 + 1] = (float)S->x[o].y;
+        dst[o * 7 + 2] = (float)S->x[o].z;
+        for (int k = 0; k < 4; ++k) dst[o * 7 + 3 + k] = (float)S->q[o][k];
+    }
+}
+
+int orc_envs_create(const cp_config* cfg, orc_envs** out) {
+    orc_envs* e = (orc_envs*)calloc(1, sizeof(orc_envs));
+    if (!e) return -1;
+    e->cfg = *cfg;
+    e->B = cfg->num_envs;
+    size_t B = (size_t)e->B;
+    int R = cfg->action_repeats;
+    e->state = (float*)calloc((size_t)CP_STATE_FIELDS * B, sizeof(float));
+    e->term_obs = (float*)calloc((size_t)R * 14 * B, sizeof(float));
+    e->bump_forces = (float*)calloc(B * (size_t)cfg->initial_force_steps * 4, sizeof(float));
+    e->ret_acc = (float*)calloc(B, sizeof(float));
+    e->last_ret = (float*)calloc(B, sizeof(float));
+    e->last_len = (int32_t*)calloc(B, sizeof(int32_t));
+    e->overflow = (int32_t*)calloc(B, sizeof(int32_t));
+    for (int i = 0; i < e->B; ++i) {
+        for (int d = 0; d < CP_NUM_DYN; ++d) {
+            for (int k = 0; k < 3; ++k) SF(e, CP_SF_BODY(d, k), i) = cfg->phys.spawn_pos[d + 1][k];
+            SF(e, CP_SF_BODY(d, 6), i) = 1.0f;
+        }
+        for (int p = 0; p < CP_NUM_PAIRS; ++p) set_i(e, CP_SF_WS_ID(p), i, -1);
+        /* done = 1 until the first reset: step before reset is an error in the
+         * reference (AttributeError); the batched API reports done. */
+        set_i(e, CP_SF_DONE, i, 1);
+    }
+    *out = e;
+    return 0;
+}
+void orc_envs_destroy(orc_envs* e) {
+    if (!e) return;
+    free(e->state); free(e->term_obs); free(e->bump_forces); free(e->ret_acc);
+    free(e->last_ret); free(e->last_len); free(e->overflow);
+    free(e);
+}
+void orc_envs_set_bump_forces(orc_envs* e, const float* f) {
+    memcpy(e->bump_forces, f, (size_t)e->B * e->cfg.initial_force_steps * 4 * sizeof(float));
+}
+void orc_envs_get_state(const orc_envs* e, float* out) {
+    memcpy(out, e->state, (size_t)CP_STATE_FIELDS * e->B * sizeof(float));
+}
+void orc_envs_set_state(orc_envs* e, const float* in) {
+    memcpy(e->state, in, (size_t)CP_STATE_FIELDS * e->B * sizeof(float));
+}
+
+/* bump force k (0..initial_force_steps-1) on cart c (0: cart, 1: cart2), LINK frame */
+static void bump_force(const orc_envs* e, int i, int episode, int k, int c, real* fx, real* fy) {
+    const cp_config* cfg = &e->cfg;
+    if (cfg->bump_mode == CP_BUMP_HOST) {
+        const float* f = e->bump_forces + (((size_t)i * cfg->initial_force_steps + k) * 2 + c) * 2;
+        *fx = f[0];
+        *fy = f[1];
+        return;
+    }
+    real F = (real)cfg->initial_force;
+    if (!cfg->random_theta) { *fx = F; *fy = F * RC(0); return; }
+    uint32_t idx = (uint32_t)(2 * k + c);
+    uint64_t gid = (uint64_t)(cfg->env_id_offset + i);
+    uint32_t ctr[4] = {idx >> 2, (uint32_t)episode, (uint32_t)gid, (uint32_t)(gid >> 32)};
+    uint32_t key[2] = {(uint32_t)cfg->seed, (uint32_t)(cfg->seed >> 32)};
+    uint32_t o[4];
+    orc_philox4x32_10(ctr, key, o);
+    real u = (real)(o[idx & 3] >> 8) * RC(5.9604644775390625e-08);
+    real s, co;
+    sincos_turns(u, &s, &co);
+    *fx = F * co;
+    *fy = F * s;
+}
+
+static void reset_one(orc_envs* e, int i, float* obs_row /* R*14 */) {
+    const cp_config* cfg = &e->cfg;
+    sim_t S;
+    env_load(e, i, &S);   /* keeps the pending forces (pybullet does not clear them) */
+    int episode = get_i(e, CP_SF_EPISODE, i);
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        S.x[d] = mk((real)cfg->phys.spawn_pos[d + 1][0], (real)cfg->phys.spawn_pos[d + 1][1],
+                    (real)cfg->phys.spawn_pos[d + 1][2]);
+        S.q[d][0] = S.q[d][1] = S.q[d][2] = RC(0);
+        S.q[d][3] = RC(1);
+        S.v[d] = S.w[d] = mk(RC(0), RC(0), RC(0));
+    }
+    for (int p = 0; p < CP_NUM_PAIRS; ++p) {
+        S.ws_id[p] = 0xFFFFFFFFu;
+        for (int k = 0; k < 4; ++k) S.ws_lam[p][k] = RC(0);
+    }
+    int32_t ov = 0;
+    for (int s = 0; s < cfg->settle_steps; ++s) substep(&S, &cfg->phys, &ov, NULL, NULL);
+    for (int k = 0; k < cfg->initial_force_steps; ++k) {
+        substep(&S, &cfg->phys, &ov, NULL, NULL);
+        for (int c = 0; c < 2; ++c) {
+            real fx, fy;
+            bump_force(e, i, episode, k, c, &fx, &fy);
+            apply_force_link(&S, 2 * c, fx, fy, RC(0));
+        }
+    }
+    e->overflow[i] += ov;
+    env_store(e, i, &S);
+    float row[14];
+    write_obs_row(&S, row);
+    for (int r = 0; r < cfg->action_repeats; ++r) memcpy(obs_row + r * 14, row, sizeof(row));
+    set_i(e, CP_SF_STEPS, i, 0);
+    set_i(e, CP_SF_DONE, i, 0);
+    set_i(e, CP_SF_EPISODE, i, episode + 1);
+    e->ret_acc[i] = 0.0f;
+}
+
+void orc_envs_reset(orc_envs* e, const uint8_t* mask, float* obs_out) {
+    int R = e->cfg.action_repeats;
+    for (int i = 0; i < e->B; ++i) {
+        if (mask && !mask[i]) continue;
+        reset_one(e, i, obs_out + (size_t)i * R * 14);
+    }
+}
+
+static const float DISCRETE_TABLE[CP_NUM_DISCRETE][2] = {{0, 0}, {-1, 0}, {1, 0}, {0, 1}, {0, -1}};
+
+static int bounds_exceeded(const orc_envs* e, const sim_t* S) {
+    const cp_config* cfg = &e->cfg;
+    v3 x = S->x[1];
+    const real* q = S->q[1];
+    if (FABS(x.x) > (real)cfg->pos_threshold || FABS(x.y) > (real)cfg->pos_threshold) return 1;
+    real qx = q[0], qy = q[1], qz = q[2], qw = q[3];
+    real Y = RC(2) * FMA(qy, qz, qw * qx);
+    real X = ((qw * qw - qx * qx) - qy * qy) + qz * qz;
+    int roll_out = (X > RC(0)) ? (FABS(Y) > X * (real)cfg->tan_angle_threshold) : !(X == RC(0) && Y == RC(0));
+    real sarg = RC(-2) * FMA(qx, qz, -(qw * qy));
+    int pitch_out = FABS(sarg) > (real)cfg->sin_angle_threshold;
+    return roll_out || pitch_out;
+}
+
+static void readback_pole(const sim_t* S, int pole_dyn, int vel_dyn, float* dst /* 12 */) {
+    real rpy[3];
+    quat_euler(S->q[pole_dyn], rpy);
+    dst[0] = (float)S->x[pole_dyn].x; dst[1] = (float)S->x[pole_dyn].y; dst[2] = (float)S->x[pole_dyn].z;
+    dst[3] = (float)rpy[0]; dst[4] = (float)rpy[1]; dst[5] = (float)rpy[2];
+    dst[6] = (float)S->v[vel_dyn].x; dst[7] = (float)S->v[vel_dyn].y; dst[8] = (float)S->v[vel_dyn].z;
+    dst[9] = (float)S->w[vel_dyn].x; dst[10] = (float)S->w[vel_dyn].y; dst[11] = (float)S->w[vel_dyn].z;
+}
+
+static void step_one(orc_envs* e, int i, const void* actions, int kind, float* obs_out, float* reward_out,
+                     uint8_t* done_out, float* term_out, float* readback, int rb_bug) {
+    const cp_config* cfg = &e->cfg;
+    const int R = cfg->action_repeats, Sn = cfg->steps_per_repeat;
+    float* obs = obs_out + (size_t)i * R * 14;
+    if (get_i(e, CP_SF_DONE, i)) {     /* bullet_cartpole.py:179-181 */
+        for (int f = 0; f < R * 14; ++f) obs[f] = e->term_obs[(size_t)f * e->B + i];
+        reward_out[i] = 0.0f;
+        done_out[i] = 1;
+        return;
+    }
+    real a[2][2];
+    if (kind == CP_ACTION_CONTINUOUS) {
+        const float* A = (const float*)actions + (size_t)i * 4;
+        a[0][0] = A[0]; a[0][1] = A[1]; a[1][0] = A[2]; a[1][1] = A[3];
+    } else {
+        const int8_t* A = (const int8_t*)actions + (size_t)i * 2;
+        for (int c = 0; c < 2; ++c) {
+            int k = A[c];
+            if (k < 0 || k >= CP_NUM_DISCRETE) k = 0;
+            a[c][0] = DISCRETE_TABLE[k][0];
+            a[c][1] = DISCRETE_TABLE[k][1];
+        }
+    }
+    const real F = (real)cfg->action_force;
+    sim_t S;
+    env_load(e, i, &S);
+    int32_t ov = 0;
+    for (int r = 0; r < R; ++r) {
+        for (int s = 0; s < Sn; ++s) {
+            substep(&S, &cfg->phys, &ov, NULL, NULL);
+            apply_force_link(&S, 0, a[0][0] * F, a[0][1] * F, RC(0));
+            apply_force_link(&S, 2, a[1][0] * F, a[1][1] * F, RC(0));
+            if (readback) {
+                size_t base = (size_t)i * 2 * R * Sn * 12;
+                readback_pole(&S, 1, 1, readback + base + ((size_t)(0 * R + r) * Sn + s) * 12);
+                readback_pole(&S, 3, rb_bug ? 1 : 3, readback + base + ((size_t)(1 * R + r) * Sn + s) * 12);
+            }
+        }
+        write_obs_row(&S, obs + r * 14);
+    }
+    e->overflow[i] += ov;
+    int steps = get_i(e, CP_SF_STEPS, i) + 1;
+    int done = steps >= cfg->max_episode_len;
+    if (cfg->done_on_bounds && bounds_exceeded(e, &S)) done = 1;
+    env_store(e, i, &S);
+    set_i(e, CP_SF_STEPS, i, steps);
+    reward_out[i] = 1.0f;            /* bullet_cartpole.py:260 */
+    done_out[i] = (uint8_t)done;
+    e->ret_acc[i] += 1.0f;
+    if (done) {
+        e->last_ret[i] = e->ret_acc[i];
+        e->last_len[i] = steps;
+        e->ret_acc[i] = 0.0f;
+        for (int f = 0; f < R * 14; ++f) e->term_obs[(size_t)f * e->B + i] = obs[f];
+        if (term_out) memcpy(term_out + (size_t)i * R * 14, obs, (size_t)R * 14 * sizeof(float));
+        set_i(e, CP_SF_DONE, i, 1);
+        if (cfg->autoreset) reset_one(e, i, obs);
+    }
+}
+
+void orc_envs_step(orc_envs* e, const void* actions, int kind, float* obs_out, float* reward_out,
+                   uint8_t* done_out, float* term_out, float* readback, int rb_bug) {
+    for (int i = 0; i < e->B; ++i)
+        step_one(e, i, actions, kind, obs_out, reward_out, done_out, term_out, readback, rb_bug);
+}
+void orc_envs_step_range(orc_envs* e, int lo, int hi, const void* actions, int kind, float* obs_out,
+                         float* reward_out, uint8_t* done_out) {
+    for (int i = lo; i < hi; ++i) step_one(e, i, actions, kind, obs_out, reward_out, done_out, NULL, NULL, 0);
+}
+int orc_envs_step_omp(orc_envs* e, const void* actions, int kind, float* obs_out, float* reward_out,
+                      uint8_t* done_out, int threads) {
+    int used = 1;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel
+    {
+#pragma omp single
+        used = omp_get_num_threads();
+#pragma omp for schedule(static)
+        for (int i = 0; i < e->B; ++i)
+            step_one(e, i, actions, kind, obs_out, reward_out, done_out, NULL, NULL, 0);
+    }
+#else
+    (void)threads;
+    orc_envs_step(e, actions, kind, obs_out, reward_out, done_out, NULL, NULL, 0);
+#endif
+    return used;
+}
+void orc_envs_episode_returns(const orc_envs* e, float* ret, int32_t* len) {
+    if (ret) memcpy(ret, e->last_ret, (size_t)e->B * sizeof(float));
+    if (len) memcpy(len, e->last_len, (size_t)e->B * sizeof(int32_t));
+}

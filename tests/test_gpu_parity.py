@@ -1,0 +1,232 @@
+"""HIP kernel (through the C-ABI) vs the CPU oracle, same config, same inputs.
+
+The kernel and the fp32 oracle perform the same fp32 operations in the same order
+(explicit fma, -ffp-contract=off on both sides, own transcendentals), so the bar is
+bit-exact equality of obs / reward / done / full state.  Full-size (B = 65,536)
+runs are checked on a random subset of envs plus size-independent properties.
+"""
+import argparse
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+from cartpoleplusplus_amd import abi, native
+from cartpoleplusplus_amd.batched import BatchedCartpole
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(O, **kw):
+    cfg = native.default_config(**kw)
+    gpu = BatchedCartpole(cfg.num_envs, 0, config=abi.cp_config.from_buffer_copy(cfg))
+    orc = O.Envs(abi.cp_config.from_buffer_copy(cfg))
+    return gpu, orc
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def _assert_same(a, b, what):
+    a, b = np.asarray(a), np.asarray(b)
+    if not np.array_equal(a, b, equal_nan=True):
+        d = np.abs(a.astype(np.float64) - b.astype(np.float64))
+        idx = np.unravel_index(np.nanargmax(d), d.shape)
+        raise AssertionError(f"{what}: {np.count_nonzero(d)} elements differ, max |diff| {np.nanmax(d):.3e} at {idx}")
+
+
+def _compare_state(gpu, orc, what):
+    _assert_same(_np(gpu.get_state()), orc.get_state(), what + " state")
+
+
+def test_reset_philox_bitexact(oracle_mod):
+    gpu, orc = _pair(oracle_mod, num_envs=200, action_repeats=3, initial_force=55.0, seed=1234)
+    _assert_same(_np(gpu.reset()), orc.reset(), "reset obs")
+    _compare_state(gpu, orc, "reset")
+    _assert_same(_np(gpu.overflow_counts()), np.zeros(200, np.int32), "overflow")
+
+
+@pytest.mark.parametrize("R,S", [(3, 1), (2, 1), (3, 4)])
+def test_continuous_random_actions_200_steps(oracle_mod, R, S):
+    B = 96
+    gpu, orc = _pair(oracle_mod, num_envs=B, action_repeats=R, steps_per_repeat=S, initial_force=55.0, seed=7)
+    _assert_same(_np(gpu.reset()), orc.reset(), "reset obs")
+    rng = np.random.default_rng(123)
+    for t in range(200):
+        a = rng.uniform(-1, 1, (B, 2, 2)).astype(np.float32)
+        go, gr, gd = gpu.step(torch.from_numpy(a).cuda())
+        oo, orw, od = orc.step(a)
+        _assert_same(_np(go), oo, f"obs step {t}")
+        _assert_same(_np(gr), orw, f"reward step {t}")
+        _assert_same(_np(gd), od, f"done step {t}")
+    _compare_state(gpu, orc, "after 200 steps")
+    assert _np(gd).all()   # max_episode_len = 200
+
+
+def test_discrete_autoreset_bounds(oracle_mod):
+    B = 130
+    gpu, orc = _pair(oracle_mod, num_envs=B, action_repeats=3, initial_force=55.0, seed=99, autoreset=1,
+                     done_on_bounds=1, max_episode_len=40)
+    _assert_same(_np(gpu.reset()), orc.reset(), "reset")
+    rng = np.random.default_rng(5)
+    for t in range(120):
+        a = rng.integers(0, 5, (B, 2)).astype(np.int8)
+        go, gr, gd = gpu.step(torch.from_numpy(a).cuda())
+        oo, orw, od, ot = orc.step(a, terminal=True)
+        _assert_same(_np(go), oo, f"obs step {t}")
+        _assert_same(_np(gd), od, f"done step {t}")
+        done = od.astype(bool)
+        _assert_same(_np(gpu.terminal_obs)[done], ot[done], f"terminal obs step {t}")
+    _compare_state(gpu, orc, "autoreset")
+    gr_, gl_ = gpu.episode_returns()
+    orr, orl = orc.episode_returns()
+    _assert_same(_np(gr_), orr, "episode returns")
+    _assert_same(_np(gl_), orl, "episode lengths")
+    assert (orl > 0).all() and (orl <= 40).all()
+
+
+def test_host_bump_mode(oracle_mod):
+    B = 33
+    gpu, orc = _pair(oracle_mod, num_envs=B, action_repeats=2, bump_mode=abi.CP_BUMP_HOST)
+    rng = np.random.default_rng(0)
+    f = rng.uniform(-200, 200, (B, 30, 2, 2)).astype(np.float32)
+    gpu.set_bump_forces(torch.from_numpy(f).cuda())
+    orc.set_bump_forces(f)
+    _assert_same(_np(gpu.reset()), orc.reset(), "reset obs")
+    for t in range(30):
+        a = rng.uniform(-1, 1, (B, 2, 2)).astype(np.float32)
+        go, _, _ = gpu.step(torch.from_numpy(a).cuda())
+        oo, _, _ = orc.step(a)
+        _assert_same(_np(go), oo, f"obs step {t}")
+
+
+@pytest.mark.parametrize("bug", [True, False])
+def test_readback_12_state(oracle_mod, bug):
+    B, R, S = 40, 3, 2
+    gpu, orc = _pair(oracle_mod, num_envs=B, action_repeats=R, steps_per_repeat=S, initial_force=55.0, seed=3)
+    gpu.enable_readback(True, reference_bug=bug)
+    gpu.reset()
+    orc.reset()
+    rng = np.random.default_rng(1)
+    for t in range(25):
+        a = rng.uniform(-1, 1, (B, 2, 2)).astype(np.float32)
+        gpu.step(torch.from_numpy(a).cuda())
+        _, _, _, rb = orc.step(a, readback=True, readback_bug=bug)
+        _assert_same(_np(gpu.readback), rb, f"readback step {t}")
+    if bug:   # bullet_cartpole.py:224 reads pole's velocity into pole2's rows
+        r = _np(gpu.readback)
+        assert np.array_equal(r[:, 1, :, :, 2:4], r[:, 0, :, :, 2:4])
+
+
+def test_step_after_done_and_mask_reset(oracle_mod):
+    B = 64
+    gpu, orc = _pair(oracle_mod, num_envs=B, action_repeats=2, max_episode_len=3, seed=11, initial_force=55.0)
+    gpu.reset()
+    orc.reset()
+    a = np.zeros((B, 2, 2), np.float32)
+    for t in range(5):   # steps 4 and 5 are after done
+        go, gr, gd = gpu.step(torch.from_numpy(a).cuda())
+        oo, orw, od = orc.step(a)
+        _assert_same(_np(go), oo, f"obs {t}")
+        _assert_same(_np(gr), orw, f"reward {t}")
+        _assert_same(_np(gd), od, f"done {t}")
+    assert (_np(gr) == 0).all() and (_np(gd) == 1).all()
+    mask = np.zeros(B, np.uint8)
+    mask[::3] = 1
+    gpu.reset(torch.from_numpy(mask).cuda())
+    orc_obs = np.zeros((B, 2, 2, 7), np.float32)
+    orc_obs[:] = _np(gpu.obs)          # unmasked rows are left untouched by both
+    orc.reset(mask, obs=orc_obs)
+    _assert_same(_np(gpu.obs), orc_obs, "masked reset obs")
+    _compare_state(gpu, orc, "masked reset")
+
+
+def test_state_roundtrip_into_oracle(oracle_mod):
+    B = 50
+    gpu, orc = _pair(oracle_mod, num_envs=B, action_repeats=3, initial_force=200.0, seed=5)
+    gpu.reset()
+    rng = np.random.default_rng(2)
+    for _ in range(20):
+        gpu.step(torch.from_numpy(rng.uniform(-1, 1, (B, 2, 2)).astype(np.float32)).cuda())
+    orc.set_state(_np(gpu.get_state()))
+    gpu2 = BatchedCartpole(B, 0, config=abi.cp_config.from_buffer_copy(gpu.cfg))
+    gpu2.set_state(gpu.get_state())
+    for t in range(10):
+        a = rng.uniform(-1, 1, (B, 2, 2)).astype(np.float32)
+        g1, _, _ = gpu.step(torch.from_numpy(a).cuda())
+        g2, _, _ = gpu2.step(torch.from_numpy(a).cuda())
+        oo, _, _ = orc.step(a)
+        _assert_same(_np(g1), oo, f"obs {t}")
+        _assert_same(_np(g2), oo, f"obs (set_state copy) {t}")
+
+
+def test_full_size_bench_config_subset_parity_and_properties(oracle_mod):
+    """B = 65,536, discrete, R = 3, autoreset (BASELINE config 3): a random subset of
+    envs is re-simulated on the oracle from the GPU state; the whole batch is checked
+    for finiteness, unit quaternions and run-to-run determinism."""
+    B = 65536
+    cfg = native.default_config(num_envs=B, action_repeats=3, initial_force=55.0, seed=1234, autoreset=1)
+    g1 = BatchedCartpole(B, 0, config=abi.cp_config.from_buffer_copy(cfg))
+    g2 = BatchedCartpole(B, 0, config=abi.cp_config.from_buffer_copy(cfg))
+    g1.reset()
+    g2.reset()
+    gen = torch.Generator(device="cuda").manual_seed(1234)
+    for t in range(12):
+        a = torch.randint(0, 5, (B, 2), device="cuda", generator=gen, dtype=torch.int8)
+        o1, _, _ = g1.step(a)
+        o2, _, _ = g2.step(a)
+    assert torch.equal(o1, o2)                                  # deterministic
+    assert torch.isfinite(o1).all()
+    q = o1[..., 3:7].double()
+    assert torch.allclose(q.norm(dim=-1), torch.ones_like(q[..., 0]), atol=1e-5)
+    # subset parity: oracle restarted from the GPU state of 512 envs
+    st = _np(g1.get_state())
+    idx = np.sort(np.random.default_rng(0).choice(B, 512, replace=False))
+    sub = abi.cp_config.from_buffer_copy(cfg)
+    sub.num_envs = 512
+    orc = oracle_mod.Envs(sub)
+    orc.set_state(np.ascontiguousarray(st[:, idx]))
+    rng = np.random.default_rng(9)
+    for t in range(8):
+        a = rng.integers(0, 5, (B, 2)).astype(np.int8)
+        go, gr, gd = g1.step(torch.from_numpy(a).cuda())
+        oo, orw, od = orc.step(np.ascontiguousarray(a[idx]))
+        _assert_same(_np(go)[idx], oo, f"subset obs {t}")
+        _assert_same(_np(gd)[idx], od, f"subset done {t}")
+
+
+def test_gym_mirror_matches_oracle_and_reference_errors(oracle_mod):
+    from cartpoleplusplus_amd.bullet_cartpole import BulletCartpole, add_opts, draw_bump_forces
+    ap = argparse.ArgumentParser()
+    add_opts(ap)
+    opts = ap.parse_args(["--initial-force", "55", "--action-repeats", "3"])
+    env = BulletCartpole(opts, discrete_actions=False)
+    with pytest.raises(AttributeError):
+        env.step(np.zeros((2, 2)))         # step before reset (reference: self.done unset)
+    np.random.seed(0)
+    obs = env.reset()
+    assert obs.shape == (3, 2, 7) and obs.dtype == np.float32
+    cfg = oracle_mod.default_config(num_envs=1, action_repeats=3, initial_force=55.0, bump_mode=abi.CP_BUMP_HOST)
+    orc = oracle_mod.Envs(cfg)
+    np.random.seed(0)
+    orc.set_bump_forces(draw_bump_forces(55.0, True)[None].astype(np.float32))
+    _assert_same(obs, orc.reset()[0], "mirror reset")
+    with pytest.raises(IndexError):
+        env.step(np.zeros((1, 2)))         # declared Box(1,2) action: the fork indexes action[1]
+    with pytest.raises(TypeError):
+        env.step(3)
+    a = np.array([[0.5, -0.25], [-1.0, 0.75]])
+    o, r, d, info = env.step(a)
+    oo, _, _ = orc.step(a.astype(np.float32).reshape(1, 2, 2))
+    _assert_same(o, oo[0], "mirror step")
+    assert r == 1.0 and d is False and info == {}
+    assert env.monkey_positions.shape == (2, 3, 1, 2, 3) and env.monkey_velocities.shape == (2, 3, 1, 2, 3)
+    denv = BulletCartpole(opts, discrete_actions=True)
+    assert denv.action_space.n == 5
+    np.random.seed(1)
+    denv.reset()
+    with pytest.raises(TypeError):
+        denv.step(2)                        # reference: 'int' object is not subscriptable
+    denv.step([1, 4])
