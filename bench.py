@@ -31,6 +31,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from cartpoleplusplus_amd.batched import BatchedCartpole  # noqa: E402
+from cartpoleplusplus_amd.dist import gather_returns, return_histogram, shard_spec  # noqa: E402
 
 METRIC = "env-steps/sec at batch=65,536, 1→8 MI355X; max |pose−pybullet| over 200 steps"
 HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s spec, 6.29 measured)
@@ -43,6 +44,21 @@ def step_kernel_bytes(R, action_bytes):
     state_write = 52 + 6 + 1           # bodies, pending forces, steps
     warm_cache = 2 * (10 + 40)         # warm-start ids + impulses, read + write once per step
     return 4 * (state_read + state_write + warm_cache) + action_bytes + 4 * 14 * R + 4 + 1 + 8
+
+
+def pmc_traffic(kernel, batch, repeats):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
+    (profiles/<tag>_pmc.json, tools/profile.sh + tools/summarize_profile.py), if it was
+    collected on this workload; else None."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
+    for p in reversed(paths):
+        with open(p) as f:
+            d = json.load(f)
+        k = d.get("kernels", {}).get(kernel)
+        if k and "hbm_bytes_per_launch" in k and d.get("batch", batch) == batch and d.get("repeats", repeats) == repeats:
+            return k["hbm_bytes_per_launch"], os.path.relpath(p, ROOT)
+    return None, None
 
 
 def log(*a):
@@ -108,11 +124,12 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     B, R, K, W = args.batch, args.repeats, args.steps, args.warmup
+    spec = shard_spec(B, rank, world, seed=1234 + rank)
     env = BatchedCartpole(B, local, action_repeats=R, steps_per_repeat=1, max_episode_len=200,
-                          initial_force=55.0, autoreset=True, seed=1234 + rank, env_id_offset=rank * B)
+                          initial_force=55.0, autoreset=True, seed=spec["seed"],
+                          env_id_offset=spec["env_id_offset"])
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     actions = torch.randint(0, 5, (W + K, B, 2), dtype=torch.int8, device=dev, generator=gen)
-    gathered = torch.empty(world * B, device=dev, dtype=torch.float32)
     env.reset()
     for t in range(W):
         env.step(actions[t])
@@ -131,12 +148,7 @@ def main():
         env.step(actions[W + t])
         if (t + 1) % WINDOW == 0:
             r, _ = env.episode_returns()
-            if world > 1:
-                dist.all_gather_into_tensor(gathered, r)
-                g = gathered
-            else:
-                g = r
-            hist = torch.bincount(g.to(torch.int64).clamp_(0, 200), minlength=201)
+            hist = return_histogram(gather_returns(r), 200)   # RCCL all-gather when world > 1
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -151,6 +163,7 @@ def main():
     per_launch_s = tm["step_ms"] / max(1, tm["step_launches"]) / 1e3
     bytes_launch = B * step_kernel_bytes(R, 2)
     achieved = bytes_launch / per_launch_s / 1e9
+    traffic, traffic_src = pmc_traffic("cp_step_kernel<discrete>", B, R)
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -170,7 +183,9 @@ def main():
                    "global_batch": world * B, "envs_per_gpu": B, "action_repeats": R, "steps_per_repeat": 1,
                    "parallelism": f"dp{world} (independent env shards, no per-step collective)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
+                     "traffic_source": traffic_src and (traffic_src + " (2*FETCH_SIZE + WRITE_SIZE) KiB*1024 "
+                                                        "per launch, rocprofv3 --pmc, separate passes"),
                      "kernel": "cp_step_kernel<discrete>",
                      "bytes_per_launch": bytes_launch,
                      "avg_launch_ms": round(per_launch_s * 1e3, 4),
