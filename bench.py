@@ -111,6 +111,8 @@ def main():
     ap.add_argument("--repeats", type=int, default=3)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--solver-iterations", type=int, default=None,
+                    help="override the PGS sweep cap (default: the model's 50; non-default runs are diagnostics)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -127,7 +129,8 @@ def main():
     spec = shard_spec(B, rank, world, seed=1234 + rank)
     env = BatchedCartpole(B, local, action_repeats=R, steps_per_repeat=1, max_episode_len=200,
                           initial_force=55.0, autoreset=True, seed=spec["seed"],
-                          env_id_offset=spec["env_id_offset"])
+                          env_id_offset=spec["env_id_offset"],
+                          **({} if args.solver_iterations is None else {"solver_iterations": args.solver_iterations}))
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     actions = torch.randint(0, 5, (W + K, B, 2), dtype=torch.int8, device=dev, generator=gen)
     env.reset()
@@ -181,7 +184,8 @@ def main():
                                "initial_force=55, fp32 (BASELINE.json configs[2]; N>1 = C4 with RCCL all-gather "
                                "of episode returns per 200-step window)",
                    "global_batch": world * B, "envs_per_gpu": B, "action_repeats": R, "steps_per_repeat": 1,
-                   "parallelism": f"dp{world} (independent env shards, no per-step collective)"},
+                   "parallelism": f"dp{world} (independent env shards, no per-step collective)",
+                   "solver_iterations": env.cfg.phys.solver_iterations},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                      "traffic_source": traffic_src and (traffic_src + " (2*FETCH_SIZE + WRITE_SIZE) KiB*1024 "

@@ -40,7 +40,26 @@ struct Bufs {
     int32_t* list;     // [B] reset list
     int32_t* count;    // [1] reset list length
     float* scratch;    // [4*CP_NUM_PAIRS][B] manifold headers of the current substep
+    uint64_t* stamps;  // [waves][8] diagnostic phase cycles (CP_STAMPS builds only)
 };
+
+// per-wave stamp accumulation into b.stamps (lane 0 writes; CP_STAMPS builds only)
+CP_DEV void flush_stamps(const Stamps& ST, uint64_t* dst, uint64_t total) {
+#ifdef CP_STAMPS
+    if ((threadIdx.x & (WAVE - 1)) == 0) {
+        atomicAdd((unsigned long long*)&dst[0], (unsigned long long)ST.narrow);
+        atomicAdd((unsigned long long*)&dst[1], (unsigned long long)ST.vel);
+        atomicAdd((unsigned long long*)&dst[2], (unsigned long long)ST.solve);
+        atomicAdd((unsigned long long*)&dst[3], (unsigned long long)ST.integ);
+        atomicAdd((unsigned long long*)&dst[4], (unsigned long long)ST.sweeps);
+        atomicAdd((unsigned long long*)&dst[5], (unsigned long long)ST.substeps);
+        atomicAdd((unsigned long long*)&dst[6], (unsigned long long)total);
+        atomicAdd((unsigned long long*)&dst[7], 1ull);
+    }
+#else
+    (void)ST; (void)dst; (void)total;
+#endif
+}
 
 CP_DEV uint32_t boff(int i) { return (uint32_t)i * 4u; }
 
@@ -187,6 +206,7 @@ __global__ void __launch_bounds__(WAVE) cp_reset_kernel(cp_config cfg, Bufs b, f
     const int i = b.list[t];
     float* pool = lds_pool + threadIdx.x;
     const Mem G{Soa::make(b.state, B, CP_STATE_FIELDS), Soa::make(b.scratch, B, 4 * CP_NUM_PAIRS), boff(i)};
+    Stamps ST;
     Sim S;
     load_sim(S, G.st, G.off);  // pending forces survive the reset (pybullet keeps them)
     const int episode = ldi(G.st, CP_SF_EPISODE, G.off);
@@ -206,7 +226,7 @@ __global__ void __launch_bounds__(WAVE) cp_reset_kernel(cp_config cfg, Bufs b, f
     int ov = 0;
     const int nsub = cfg.settle_steps + cfg.initial_force_steps;
     for (int s = 0; s < nsub; ++s) {
-        substep(S, cfg.phys, pool, ov, G);
+        substep(S, cfg.phys, pool, ov, G, ST);
         const int k = s - cfg.settle_steps;
         if (k >= 0) {
             float fx, fy;
@@ -242,6 +262,8 @@ __global__ void __launch_bounds__(WAVE) cp_step_kernel(cp_config cfg, Bufs b, co
     const int R = cfg.action_repeats, SR = cfg.steps_per_repeat;
     float* pool = lds_pool + threadIdx.x;
     bool want_reset = false;
+    Stamps ST;
+    CP_STAMP(k0);
     if (inb) {
         const Mem G{Soa::make(b.state, B, CP_STATE_FIELDS), Soa::make(b.scratch, B, 4 * CP_NUM_PAIRS), boff(i)};
         const Soa term = Soa::make(b.term_obs, B, R * 14);
@@ -270,7 +292,7 @@ __global__ void __launch_bounds__(WAVE) cp_step_kernel(cp_config cfg, Bufs b, co
             int ov = 0;
             for (int r = 0; r < R; ++r) {
                 for (int s = 0; s < SR; ++s) {
-                    substep(S, cfg.phys, pool, ov, G);
+                    substep(S, cfg.phys, pool, ov, G, ST);
                     apply_force_link<0>(S, f00, f01);
                     apply_force_link<1>(S, f10, f11);
                     if (readback) {
@@ -308,6 +330,10 @@ __global__ void __launch_bounds__(WAVE) cp_step_kernel(cp_config cfg, Bufs b, co
             }
         }
     }
+#ifdef CP_STAMPS
+    CP_STAMP(k1);
+    flush_stamps(ST, b.stamps, k1 - k0);
+#endif
     if (cfg.autoreset) {
         // wave ballot compaction of the finishing envs into the reset list
         const uint64_t bal = __ballot(want_reset);
@@ -482,7 +508,10 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     CP_ALLOC(h->b.list, B * sizeof(int32_t));
     CP_ALLOC(h->b.count, sizeof(int32_t));
     CP_ALLOC(h->b.scratch, (size_t)4 * CP_NUM_PAIRS * B * sizeof(float));
+    CP_ALLOC(h->b.stamps, 8 * sizeof(uint64_t));
 #undef CP_ALLOC
+    e = hipMemset(h->b.stamps, 0, 8 * sizeof(uint64_t));
+    if (e != hipSuccess) return fail_free(e, "hipMemset");
     e = hipMemset(h->b.term_obs, 0, (size_t)R * 14 * B * sizeof(float));
     if (e != hipSuccess) return fail_free(e, "hipMemset");
     e = hipMemset(h->b.bumps, 0, B * (size_t)(cfg->initial_force_steps > 0 ? cfg->initial_force_steps : 1) * 4 * sizeof(float));
@@ -498,18 +527,19 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
 
 void cp_destroy(cp_handle* h) {
     if (!h) return;
-    hipSetDevice(h->device);
+    (void)hipSetDevice(h->device);
     timing_free(h->timing);
-    hipFree(h->b.state);
-    hipFree(h->b.term_obs);
-    hipFree(h->b.bumps);
-    hipFree(h->b.ret_acc);
-    hipFree(h->b.last_ret);
-    hipFree(h->b.last_len);
-    hipFree(h->b.overflow);
-    hipFree(h->b.list);
-    hipFree(h->b.count);
-    hipFree(h->b.scratch);
+    (void)hipFree(h->b.state);
+    (void)hipFree(h->b.term_obs);
+    (void)hipFree(h->b.bumps);
+    (void)hipFree(h->b.ret_acc);
+    (void)hipFree(h->b.last_ret);
+    (void)hipFree(h->b.last_len);
+    (void)hipFree(h->b.overflow);
+    (void)hipFree(h->b.list);
+    (void)hipFree(h->b.count);
+    (void)hipFree(h->b.scratch);
+    (void)hipFree(h->b.stamps);
     delete h;
 }
 
@@ -607,6 +637,19 @@ int cp_overflow_counts(cp_handle* h, int32_t* out, void* stream) {
     CP_TRY(h, hipMemcpyAsync(out, h->b.overflow, (size_t)h->cfg.num_envs * sizeof(int32_t), hipMemcpyDeviceToDevice,
                              (hipStream_t)stream));
     return 0;
+}
+
+int cp_debug_stamps(cp_handle* h, uint64_t* out8, int reset) {
+    if (!h || !out8) return fail(h, "cp_debug_stamps: null argument");
+    CP_TRY(h, hipSetDevice(h->device));
+    CP_TRY(h, hipDeviceSynchronize());
+    CP_TRY(h, hipMemcpy(out8, h->b.stamps, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    if (reset) CP_TRY(h, hipMemset(h->b.stamps, 0, 8 * sizeof(uint64_t)));
+#ifdef CP_STAMPS
+    return 1;
+#else
+    return 0;
+#endif
 }
 
 int cp_timing_begin(cp_handle* h, int max_launches) {

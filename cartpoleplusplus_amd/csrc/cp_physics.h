@@ -14,6 +14,19 @@
 
 namespace cp {
 
+// Diagnostic phase stamps (built only with -DCP_STAMPS; see cp_debug_stamps).
+// Wave-uniform cycle counters from s_memtime, accumulated per wave.
+struct Stamps {
+    uint64_t narrow = 0, vel = 0, solve = 0, integ = 0, sweeps = 0, substeps = 0;
+};
+#ifdef CP_STAMPS
+#define CP_STAMP(var) uint64_t var = __builtin_amdgcn_s_memtime()
+#define CP_ACC(field, a, b) (ST.field += (b) - (a))
+#else
+#define CP_STAMP(var)
+#define CP_ACC(field, a, b)
+#endif
+
 constexpr int WAVE = 64;
 constexpr int MAXP = CP_MAX_POINTS;
 constexpr int MAXF = CP_MAX_FRICTION;
@@ -133,11 +146,18 @@ CP_DEV void face_contact(const Box& R, int ri, V3 nr, const Box& I, float margin
     // 24 candidate slots in canonical order: C1 0-3, C2 4-7, C3 8-23
     float Cu[24], Cv[24], Cn[24];
     uint32_t valid = 0;
+    int inside = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         Cu[k] = Pu[k]; Cv[k] = Pv[k]; Cn[k] = Pn[k];
-        if (fabsf(Pu[k]) <= hu && fabsf(Pv[k]) <= hv && Pn[k] <= margin) valid |= 1u << k;
+        const bool in = fabsf(Pu[k]) <= hu && fabsf(Pv[k]) <= hv;
+        inside += in ? 1 : 0;
+        if (in && Pn[k] <= margin) valid |= 1u << k;
     }
+#pragma unroll
+    for (int k = 4; k < 24; ++k) { Cu[k] = 0.0f; Cv[k] = 0.0f; Cn[k] = 0.0f; }
+    // all four incident vertices inside the reference rectangle: C1 only (oracle: same rule)
+    if (inside != 4) {
     float det = fmaf_(e1u, e2v, -(e1v * e2u));
     float idet = 1.0f / det;
 #pragma unroll
@@ -178,6 +198,7 @@ CP_DEV void face_contact(const Box& R, int ri, V3 nr, const Box& I, float margin
             if (cross_ && inr && xn <= margin) valid |= 1u << slot;
         }
     }
+    }  // inside != 4
     uint32_t sel = valid;
     if (__builtin_popcount(valid) > 4) {
         // deepest; farthest from it; max / min signed area  (oracle: same rule)
@@ -225,7 +246,24 @@ CP_DEV void face_contact(const Box& R, int ri, V3 nr, const Box& I, float margin
     // compact the selected candidates, canonical order
     out.m = 0;
 #pragma unroll
-    for (int k = 0; k < 24; ++k) {
+    for (int k = 0; k < 4; ++k) {
+        if ((sel >> k) & 1u) {
+            int m = out.m;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (m == j) {
+                    out.u[j] = Cu[k];
+                    out.v[j] = Cv[k];
+                    out.n[j] = Cn[k];
+                    out.id[j] = k;
+                }
+            }
+            out.m = m + 1;
+        }
+    }
+    if ((sel >> 4) == 0u) return;
+#pragma unroll
+    for (int k = 4; k < 24; ++k) {
         if ((sel >> k) & 1u) {
             int m = out.m;
 #pragma unroll
@@ -301,9 +339,9 @@ CP_DEV void box_box(const Box& A, const Box& B, float margin, float edge_bias, C
             const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
             float ra = fmaf_(Ah[i1], AC[i2][j], Ah[i2] * AC[i1][j]);
             float rb = fmaf_(Bh[j1], AC[i][j2], Bh[j2] * AC[i][j1]);
-            float s = (fabsf(dot(d, ax)) - (ra + rb)) / L;
-            sep = sep || (s > margin);
-            if (s > best + edge_bias) { best = s; kind = 2; bi = i; bj = j; bax = ax; }
+            float num = fabsf(dot(d, ax)) - (ra + rb);   // separation * L
+            sep = sep || (num > margin * L);
+            if (num > (best + edge_bias) * L) { best = num / L; kind = 2; bi = i; bj = j; bax = ax; }
         }
     }
     if (sep) return;
@@ -466,6 +504,110 @@ CP_DEV float solve_row(Sim& S, const Step& T, const cp_physics& P, V3 rb, V3 t, 
     return fabsf(e * dl);
 }
 
+// One PGS row committed only where `act` (selects, not branches, so that two
+// independent rows can share a basic block and interleave).  Same arithmetic as
+// solve_row; returns |e * dlambda| or 0.
+template <int A, int B, bool FRICTION>
+CP_DEV float solve_row_sel(Sim& S, const Step& T, const cp_physics& P, V3 rb, V3 t, float inv_eff, float target,
+                           float& lam, float bound, bool act) {
+    float imb = P.inv_mass[B];
+    V3 rbt = cross(rb, t);
+    V3 ib = symv(T.M[B - 1], rbt);
+    float vn;
+    V3 ia = mk(0.0f, 0.0f, 0.0f);
+    if constexpr (A == 0) {
+        vn = dot(t, S.b[B - 1].v) + dot(S.b[B - 1].w, rbt);
+    } else {
+        V3 ra = add(rb, sub(S.b[B - 1].x, S.b[A - 1].x));
+        V3 rat = cross(ra, t);
+        ia = symv(T.M[A - 1], rat);
+        vn = (dot(t, sub(S.b[B - 1].v, S.b[A - 1].v)) + dot(S.b[B - 1].w, rbt)) - dot(S.b[A - 1].w, rat);
+    }
+    float e = target - vn;
+    float dl = e * inv_eff;
+    float l0 = lam + dl;
+    float ln;
+    if constexpr (!FRICTION) ln = l0 > 0.0f ? l0 : 0.0f;
+    else ln = l0 > bound ? bound : (l0 < -bound ? -bound : l0);
+    dl = ln - lam;
+    lam = act ? ln : lam;
+    float sb = dl * imb;
+    S.b[B - 1].v = selv(act, madd(S.b[B - 1].v, t, sb), S.b[B - 1].v);
+    S.b[B - 1].w = selv(act, madd(S.b[B - 1].w, ib, dl), S.b[B - 1].w);
+    if constexpr (A != 0) {
+        float sa = dl * P.inv_mass[A];
+        S.b[A - 1].v = selv(act, madd(S.b[A - 1].v, neg(t), sa), S.b[A - 1].v);
+        S.b[A - 1].w = selv(act, madd(S.b[A - 1].w, neg(ia), dl), S.b[A - 1].w);
+    }
+    return act ? fabsf(e * dl) : 0.0f;
+}
+
+// Normal rows of two pairs from different islands, interleaved row by row.
+template <int PA, int PB>
+CP_DEV void pair2_normal_rows(Sim& S, const Step& T, const cp_physics& P, float* pool, float& resA, float& resB) {
+    const uint32_t pkA = T.pk[PA], pkB = T.pk[PB];
+    const int cA = pk_cnt(pkA), bA = pk_base(pkA), cB = pk_cnt(pkB), bB = pk_base(pkB);
+    const int n = cA > cB ? cA : cB;
+    for (int k = 0; k < n; ++k) {
+        const bool actA = k < cA, actB = k < cB;
+        const int sA = (bA + k) < MAXP ? bA + k : MAXP - 1;
+        const int sB = (bB + k) < MAXP ? bB + k : MAXP - 1;
+        V3 rbA = mk(pool_n(pool, F_RBX, sA), pool_n(pool, F_RBY, sA), pool_n(pool, F_RBZ, sA));
+        V3 rbB = mk(pool_n(pool, F_RBX, sB), pool_n(pool, F_RBY, sB), pool_n(pool, F_RBZ, sB));
+        float ieA = pool_n(pool, F_IE, sA), tgA = pool_n(pool, F_TG, sA), lamA = pool_n(pool, F_LAM, sA);
+        float ieB = pool_n(pool, F_IE, sB), tgB = pool_n(pool, F_TG, sB), lamB = pool_n(pool, F_LAM, sB);
+        float rA = solve_row_sel<pair_a(PA), pair_b(PA), false>(S, T, P, rbA, T.n[PA], ieA, tgA, lamA, 0.0f, actA);
+        float rB = solve_row_sel<pair_a(PB), pair_b(PB), false>(S, T, P, rbB, T.n[PB], ieB, tgB, lamB, 0.0f, actB);
+        resA = resA + rA;
+        resB = resB + rB;
+        if (actA) pool_n(pool, F_LAM, sA) = lamA;
+        if (actB) pool_n(pool, F_LAM, sB) = lamB;
+    }
+}
+
+// Friction rows (t1 then t2 per point) of two pairs from different islands, interleaved.
+template <int PA, int PB>
+CP_DEV void pair2_friction_rows(Sim& S, const Step& T, const cp_physics& P, float* pool, float& resA,
+                                float& resB) {
+    const uint32_t pkA = T.pk[PA], pkB = T.pk[PB];
+    const int cA = pk_fcnt(pkA), cB = pk_fcnt(pkB);
+    const int n = cA > cB ? cA : cB;
+    if (n == 0) return;
+    const int bA = pk_base(pkA), fA = pk_fbase(pkA), bB = pk_base(pkB), fB = pk_fbase(pkB);
+    const float muA = P.friction[pair_a(PA)] * P.friction[pair_b(PA)];
+    const float muB = P.friction[pair_a(PB)] * P.friction[pair_b(PB)];
+    // tangent basis inside the sweep: hoisted out of the PGS loop for every pair it
+    // would pin ~60 VGPRs for the whole solve
+    V3 nA = T.n[PA], nB = T.n[PB];
+    asm volatile("" : "+v"(nA.x), "+v"(nA.y), "+v"(nA.z), "+v"(nB.x), "+v"(nB.y), "+v"(nB.z));
+    V3 a1, a2, b1, b2;
+    plane_space(nA, a1, a2);
+    plane_space(nB, b1, b2);
+    for (int k = 0; k < n; ++k) {
+        const bool actA = k < cA, actB = k < cB;
+        const int sA = (bA + k) < MAXP ? bA + k : MAXP - 1, sB = (bB + k) < MAXP ? bB + k : MAXP - 1;
+        const int gA = (fA + k) < MAXF ? fA + k : MAXF - 1, gB = (fB + k) < MAXF ? fB + k : MAXF - 1;
+        V3 rbA = mk(pool_n(pool, F_RBX, sA), pool_n(pool, F_RBY, sA), pool_n(pool, F_RBZ, sA));
+        V3 rbB = mk(pool_n(pool, F_RBX, sB), pool_n(pool, F_RBY, sB), pool_n(pool, F_RBZ, sB));
+        const float boundA = muA * pool_n(pool, F_LAM, sA), boundB = muB * pool_n(pool, F_LAM, sB);
+        float lA1 = pool_f(pool, FF_L1, gA), lA2 = pool_f(pool, FF_L2, gA);
+        float lB1 = pool_f(pool, FF_L1, gB), lB2 = pool_f(pool, FF_L2, gB);
+        const float ieA1 = pool_f(pool, FF_IE1, gA), ieA2 = pool_f(pool, FF_IE2, gA);
+        const float ieB1 = pool_f(pool, FF_IE1, gB), ieB2 = pool_f(pool, FF_IE2, gB);
+        constexpr int AA = pair_a(PA), AB = pair_b(PA), BA = pair_a(PB), BB = pair_b(PB);
+        float rA1 = solve_row_sel<AA, AB, true>(S, T, P, rbA, a1, ieA1, 0.0f, lA1, boundA, actA);
+        float rB1 = solve_row_sel<BA, BB, true>(S, T, P, rbB, b1, ieB1, 0.0f, lB1, boundB, actB);
+        resA = resA + rA1;
+        resB = resB + rB1;
+        float rA2 = solve_row_sel<AA, AB, true>(S, T, P, rbA, a2, ieA2, 0.0f, lA2, boundA, actA);
+        float rB2 = solve_row_sel<BA, BB, true>(S, T, P, rbB, b2, ieB2, 0.0f, lB2, boundB, actB);
+        resA = resA + rA2;
+        resB = resB + rB2;
+        if (actA) { pool_f(pool, FF_L1, gA) = lA1; pool_f(pool, FF_L2, gA) = lA2; }
+        if (actB) { pool_f(pool, FF_L1, gB) = lB1; pool_f(pool, FF_L2, gB) = lB2; }
+    }
+}
+
 template <int PAIR>
 CP_DEV void pair_warmstart(Sim& S, const Step& T, const cp_physics& P, float* pool) {
     constexpr int A = pair_a(PAIR), B = pair_b(PAIR);
@@ -581,8 +723,9 @@ CP_DEV float row_k_dyn(int a, float ima, float imb, V3 xa, V3 xb, const Sym& Ma,
 }
 
 // One p.stepSimulation() for this lane's env (DESIGN.md §Physics model 1-6).
-CP_DEV void substep(Sim& S, const cp_physics& P, float* pool, int& overflow, const Mem& G) {
+CP_DEV void substep(Sim& S, const cp_physics& P, float* pool, int& overflow, const Mem& G, Stamps& ST) {
     const float dt = P.dt, inv_dt = P.inv_dt;
+    CP_STAMP(t0);
     Step T;
     // 1. orientation + world inverse inertia
 #pragma unroll
@@ -665,6 +808,8 @@ CP_DEV void substep(Sim& S, const cp_physics& P, float* pool, int& overflow, con
         T.n[p] = mk(G.lx(4 * p + 0), G.lx(4 * p + 1), G.lx(4 * p + 2));
         T.pk[p] = __float_as_uint(G.lx(4 * p + 3));
     }
+    CP_STAMP(t1);
+    CP_ACC(narrow, t0, t1);
     // 3. unconstrained velocity update
     const float kl = P.lin_damping, ka = P.ang_damping;
 #pragma unroll
@@ -688,20 +833,51 @@ CP_DEV void substep(Sim& S, const cp_physics& P, float* pool, int& overflow, con
         S.b[d].v = madd(v, acc, dt);
         S.b[d].w = madd(w, accw, dt);
     }
-    // 4a. warm start
-    CP_FOR_PAIRS(pair_warmstart, S, T, P, pool);
+    // 4a. warm start, in solver pair order (oracle SOLVE_ORDER = 0 2 1 3 4 9 5 6 7 8)
+    pair_warmstart<0>(S, T, P, pool); pair_warmstart<2>(S, T, P, pool);
+    pair_warmstart<1>(S, T, P, pool); pair_warmstart<3>(S, T, P, pool);
+    pair_warmstart<4>(S, T, P, pool); pair_warmstart<9>(S, T, P, pool);
+    pair_warmstart<5>(S, T, P, pool); pair_warmstart<6>(S, T, P, pool);
+    pair_warmstart<7>(S, T, P, pool); pair_warmstart<8>(S, T, P, pool);
+    CP_STAMP(t2);
+    CP_ACC(vel, t1, t2);
     // 4b. PGS sweeps; a lane stops after the sweep whose residual <= threshold
     bool active = used > 0;
     const float thr = P.residual_threshold;
     for (int it = 0; it < P.solver_iterations; ++it) {
         if (__ballot(active) == 0ull) break;
+#ifdef CP_STAMPS
+        ST.sweeps += 1;
+#endif
         if (active) {
-            float resid = 0.0f;
-            CP_FOR_PAIRS(pair_normal_rows, S, T, P, pool, resid);
-            CP_FOR_PAIRS(pair_friction_rows, S, T, P, pool, resid);
+            // island 1 = pairs 0,1,4 ; island 2 = pairs 2,3,9 ; cross = 5..8 (oracle SOLVE_ORDER)
+            float r1 = 0.0f, r2 = 0.0f, rc = 0.0f;
+            pair_normal_rows<0>(S, T, P, pool, r1);
+            pair_normal_rows<2>(S, T, P, pool, r2);
+            pair_normal_rows<1>(S, T, P, pool, r1);
+            pair_normal_rows<3>(S, T, P, pool, r2);
+            pair_normal_rows<4>(S, T, P, pool, r1);
+            pair_normal_rows<9>(S, T, P, pool, r2);
+            pair_normal_rows<5>(S, T, P, pool, rc);
+            pair_normal_rows<6>(S, T, P, pool, rc);
+            pair_normal_rows<7>(S, T, P, pool, rc);
+            pair_normal_rows<8>(S, T, P, pool, rc);
+            pair_friction_rows<0>(S, T, P, pool, r1);
+            pair_friction_rows<2>(S, T, P, pool, r2);
+            pair_friction_rows<1>(S, T, P, pool, r1);
+            pair_friction_rows<3>(S, T, P, pool, r2);
+            pair_friction_rows<4>(S, T, P, pool, r1);
+            pair_friction_rows<9>(S, T, P, pool, r2);
+            pair_friction_rows<5>(S, T, P, pool, rc);
+            pair_friction_rows<6>(S, T, P, pool, rc);
+            pair_friction_rows<7>(S, T, P, pool, rc);
+            pair_friction_rows<8>(S, T, P, pool, rc);
+            const float resid = (r1 + r2) + rc;
             if (resid <= thr) active = false;
         }
     }
+    CP_STAMP(t3);
+    CP_ACC(solve, t2, t3);
     // 4c. refresh the warm-start cache
     CP_FOR_PAIRS(pair_cache, T, pool, G);
     // 5. integrate positions and orientations
@@ -735,6 +911,11 @@ CP_DEV void substep(Sim& S, const cp_physics& P, float* pool, int& overflow, con
     // 6. external forces are consumed by the step
     S.f0 = mk(0.0f, 0.0f, 0.0f);
     S.f2 = mk(0.0f, 0.0f, 0.0f);
+    CP_STAMP(t4);
+    CP_ACC(integ, t3, t4);
+#ifdef CP_STAMPS
+    ST.substeps += 1;
+#endif
 }
 
 // LINK_FRAME force at the COM on cart (C = 0) or cart2 (C = 1): world = R(q) f

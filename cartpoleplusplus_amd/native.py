@@ -10,13 +10,14 @@ import os
 from . import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcartpole_hip.so")
+LIB_PATH = os.environ.get("CP_LIB_PATH") or os.path.join(HERE, "libcartpole_hip.so")
 
 # every entry point declared in include/cartpole_amd.h
 EXPORTS = (
     "cp_default_config", "cp_create", "cp_destroy", "cp_last_error", "cp_abi_version",
     "cp_reset", "cp_step", "cp_set_readback", "cp_set_bump_forces", "cp_get_state",
     "cp_set_state", "cp_episode_returns", "cp_overflow_counts", "cp_timing_begin", "cp_timing_end",
+    "cp_debug_stamps",
 )
 
 _lib = None
@@ -53,6 +54,7 @@ def load():
         "cp_episode_returns": (I, [VP, VP, VP, VP]),
         "cp_overflow_counts": (I, [VP, VP, VP]),
         "cp_timing_begin": (I, [VP, I]),
+        "cp_debug_stamps": (I, [VP, P(C.c_uint64), I]),
         "cp_timing_end": (I, [VP, P(C.c_double), P(C.c_int32), P(C.c_double), P(C.c_int32)]),
     }
     for name, (res, args) in sig.items():

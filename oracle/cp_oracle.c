@@ -244,6 +244,11 @@ void orc_default_config(cp_config* c) {
 
 static const int PAIR_A[CP_NUM_PAIRS] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3};
 static const int PAIR_B[CP_NUM_PAIRS] = {1, 2, 3, 4, 2, 3, 4, 3, 4, 4};
+/* Solver sweep order over pairs: the two cart-pole islands alternate ({ground,cart,pole}
+ * pairs 0,1,4 and {ground,cart2,pole2} pairs 2,3,9), cross-island pairs 5-8 last.
+ * Rows of different islands share no dynamic body, so the kernel may interleave them. */
+static const int SOLVE_ORDER[CP_NUM_PAIRS] = {0, 2, 1, 3, 4, 9, 5, 6, 7, 8};
+static const int ISLAND[CP_NUM_PAIRS] = {0, 0, 1, 1, 0, 2, 2, 2, 2, 1};
 
 /* --------------------------------------------------------------- simulation */
 typedef struct {
@@ -318,8 +323,15 @@ static int face_contact(const box_t* R, int ri, v3 nr, const box_t* I, real marg
     cand_t cand[24];
     int nc = 0;
     /* C1 */
-    for (int k = 0; k < 4; ++k)
-        if (FABS(P[k].u) <= hu && FABS(P[k].v) <= hv && P[k].n <= margin) cand[nc++] = P[k];
+    int inside = 0;
+    for (int k = 0; k < 4; ++k) {
+        int in = FABS(P[k].u) <= hu && FABS(P[k].v) <= hv;
+        inside += in;
+        if (in && P[k].n <= margin) cand[nc++] = P[k];
+    }
+    /* all four incident vertices inside the reference rectangle: the candidates are
+     * C1 only (C2/C3 cannot exist geometrically; the rule makes it exact) */
+    if (inside == 4) goto select;
     /* C2 */
     real det = FMA(e1u, e2v, -(e1v * e2u));
     real idet = RC(1) / det;
@@ -358,6 +370,7 @@ static int face_contact(const box_t* R, int ri, v3 nr, const box_t* I, real marg
             if (x.n <= margin) cand[nc++] = x;
         }
     }
+select:;
     int sel[24];
     for (int k = 0; k < nc; ++k) sel[k] = 1;
     if (nc > 4) {
@@ -431,9 +444,9 @@ static int box_box(const box_t* A, const box_t* B, real margin, real edge_bias,
             int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
             real ra = FMA(A->h[i1], AC[i2][j], A->h[i2] * AC[i1][j]);
             real rb = FMA(B->h[j1], AC[i][j2], B->h[j2] * AC[i][j1]);
-            real s = (FABS(dot(d, ax)) - (ra + rb)) / L;
-            if (s > margin) return 0;
-            if (s > best + edge_bias) { best = s; kind = 2; bi = i; bj = j; bax = ax; }
+            real num = FABS(dot(d, ax)) - (ra + rb);      /* separation * L */
+            if (num > margin * L) return 0;
+            if (num > (best + edge_bias) * L) { best = num / L; kind = 2; bi = i; bj = j; bax = ax; }
         }
     }
     if (kind == 0) {
@@ -651,33 +664,35 @@ static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* i
         S->v[d] = madd(v, acc, dt);
         S->w[d] = madd(w, accw, dt);
     }
-    /* 4a. warm start: apply the cached normal impulses (row order) */
-    for (int p = 0; p < CP_NUM_PAIRS; ++p) {
+    /* 4a. warm start: apply the cached normal impulses (solver row order) */
+    for (int j = 0; j < CP_NUM_PAIRS; ++j) {
+        int p = SOLVE_ORDER[j];
         int a = PAIR_A[p], b = PAIR_B[p];
         for (int k = 0; k < man[p].cnt; ++k) {
             point_t* q = &pt[man[p].base + k];
             apply_impulse(S, P, a, b, q->rb, man[p].n, q->lam);
         }
     }
-    /* 4b. projected Gauss-Seidel: normal rows then friction rows per sweep */
+    /* 4b. projected Gauss-Seidel: normal rows then friction rows per sweep, pairs in
+     * SOLVE_ORDER (island 1 and island 2 pairs alternate, cross pairs last); the
+     * residual is summed per island, then (island1 + island2) + cross */
     int it = 0;
     const int iters = P->solver_iterations;
     const real thr = (real)P->residual_threshold;
     if (used > 0) {
         for (it = 0; it < iters;) {
-            real resid = RC(0);
-            for (int p = 0; p < CP_NUM_PAIRS; ++p) {
+            real rs[3] = {RC(0), RC(0), RC(0)};
+            for (int j = 0; j < CP_NUM_PAIRS; ++j) {
+                int p = SOLVE_ORDER[j];
                 int a = PAIR_A[p], b = PAIR_B[p];
                 for (int k = 0; k < man[p].cnt; ++k) {
                     point_t* q = &pt[man[p].base + k];
                     real rr = solve_row(S, P, a, b, q->rb, man[p].n, q->inv_eff, q->target, &q->lam, 0, RC(0));
-#ifdef ORC_DEBUG
-                    if (getenv("ORC_DEBUG") && (it == 0 || it >= iters - 2)) fprintf(stderr, "  it %d pair %d k %d rr %g lam %g target %g rb %g %g %g n %g %g %g\n", it, p, k, (double)rr, (double)q->lam, (double)q->target, (double)q->rb.x, (double)q->rb.y, (double)q->rb.z, (double)man[p].n.x, (double)man[p].n.y, (double)man[p].n.z);
-#endif
-                    resid = resid + rr;
+                    rs[ISLAND[p]] = rs[ISLAND[p]] + rr;
                 }
             }
-            for (int p = 0; p < CP_NUM_PAIRS; ++p) {
+            for (int j = 0; j < CP_NUM_PAIRS; ++j) {
+                int p = SOLVE_ORDER[j];
                 if (man[p].fcnt == 0) continue;
                 int a = PAIR_A[p], b = PAIR_B[p];
                 v3 t1, t2;
@@ -686,10 +701,13 @@ static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* i
                     point_t* q = &pt[man[p].base + k];
                     fpoint_t* f = &fp[man[p].fbase + k];
                     real bound = man[p].mu * q->lam;
-                    resid = resid + solve_row(S, P, a, b, q->rb, t1, f->inv_eff1, RC(0), &f->lam1, 1, bound);
-                    resid = resid + solve_row(S, P, a, b, q->rb, t2, f->inv_eff2, RC(0), &f->lam2, 1, bound);
+                    real r1 = solve_row(S, P, a, b, q->rb, t1, f->inv_eff1, RC(0), &f->lam1, 1, bound);
+                    rs[ISLAND[p]] = rs[ISLAND[p]] + r1;
+                    real r2 = solve_row(S, P, a, b, q->rb, t2, f->inv_eff2, RC(0), &f->lam2, 1, bound);
+                    rs[ISLAND[p]] = rs[ISLAND[p]] + r2;
                 }
             }
+            real resid = (rs[0] + rs[1]) + rs[2];
             ++it;
 #ifdef ORC_DEBUG
             if (getenv("ORC_DEBUG")) fprintf(stderr, "it %d resid %g\n", it, (double)resid);
