@@ -11,9 +11,13 @@ CP_BODY_GROUND, CP_BODY_CART, CP_BODY_POLE, CP_BODY_CART2, CP_BODY_POLE2 = range
 CP_NUM_BODIES = 5
 CP_NUM_DYN = 4
 CP_NUM_PAIRS = 10
+CP_NUM_ISLANDS = 2
+CP_ISLAND_PAIRS = 5
 CP_BODY_FIELDS = 13
-CP_MAX_POINTS = 20
-CP_MAX_FRICTION = 10
+CP_ISLAND_POINTS = 10
+CP_ISLAND_FRICTION = 5
+# global pair index of island p's local pair j (own 3, then its 2 cross pairs)
+ISLAND_PAIR = ((0, 1, 4, 5, 6), (2, 3, 9, 7, 8))
 CP_NUM_DISCRETE = 5
 
 
@@ -30,12 +34,12 @@ CP_SF_EPISODE = CP_SF_STEPS + 1
 CP_SF_DONE = CP_SF_STEPS + 2
 
 
-def CP_SF_WS_ID(pair):
-    return CP_SF_STEPS + 3 + pair
+def CP_SF_WS_ID(isl, j):
+    return CP_SF_STEPS + 3 + isl * CP_ISLAND_PAIRS + j
 
 
-def CP_SF_WS_LAM(pair, k):
-    return CP_SF_STEPS + 3 + CP_NUM_PAIRS + pair * 4 + k
+def CP_SF_WS_LAM(isl, j, k):
+    return CP_SF_STEPS + 3 + CP_NUM_PAIRS + (isl * CP_ISLAND_PAIRS + j) * 4 + k
 
 
 CP_STATE_FIELDS = CP_SF_STEPS + 3 + CP_NUM_PAIRS * 5

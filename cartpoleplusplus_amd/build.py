@@ -1,6 +1,7 @@
 """Build the HIP library in-tree: cartpoleplusplus_amd/libcartpole_hip.so (gfx950).
 
     python -m cartpoleplusplus_amd.build          # or __graft_entry__.build()
+    python -m cartpoleplusplus_amd.build --stamps # + diagnostic phase-stamp build (tools/stamps.py)
 
 hipcc cross-compiles for gfx950 without a GPU.  -ffp-contract=off: only the
 explicit __builtin_fmaf calls fuse, which is what makes the kernel agree bit for
@@ -15,6 +16,7 @@ SRC = os.path.join(HERE, "csrc", "cp_kernels.hip")
 DEPS = [os.path.join(HERE, "csrc", f) for f in ("cp_kernels.hip", "cp_physics.h", "cp_math.h")] + [
     os.path.join(HERE, "..", "include", "cartpole_amd.h")]
 LIB = os.path.join(HERE, "libcartpole_hip.so")
+STAMPS_LIB = os.path.join(HERE, "libcartpole_hip_stamps.so")
 ARCH = os.environ.get("CP_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
@@ -22,25 +24,28 @@ FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=off", "-f
          "-Wno-unused-result"]
 
 
-def up_to_date():
-    if not os.path.exists(LIB):
+def up_to_date(lib=LIB):
+    if not os.path.exists(lib):
         return False
-    t = os.path.getmtime(LIB)
+    t = os.path.getmtime(lib)
     return all(os.path.getmtime(d) <= t for d in DEPS)
 
 
-def build(force=False, verbose=False):
-    if not force and up_to_date():
-        return LIB
-    cmd = [HIPCC] + FLAGS + ["-o", LIB + ".tmp", SRC]
+def build(force=False, verbose=False, stamps=False):
+    lib = STAMPS_LIB if stamps else LIB
+    if not force and up_to_date(lib):
+        return lib
+    cmd = [HIPCC] + FLAGS + (["-DCP_STAMPS"] if stamps else []) + ["-o", lib + ".tmp", SRC]
     if verbose:
         print(" ".join(cmd))
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError("hipcc failed:\n" + res.stdout + res.stderr)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(lib + ".tmp", lib)
+    return lib
 
 
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    if "--stamps" in sys.argv:
+        print(build(force="--force" in sys.argv, verbose=True, stamps=True))

@@ -1,7 +1,8 @@
 // cp_kernels.hip — batched cartpole++ env on MI355X (gfx950): kernels + C-ABI.
 //
 // Replaces bullet_cartpole.py's hot path (BulletCartpole.step/reset and the
-// pybullet calls behind them) for B independent envs, one lane per env.
+// pybullet calls behind them) for B independent envs, two lanes per env (lane
+// 2e+p owns contact island p; cp_physics.h).
 //
 //   cp_step_kernel   R x S substeps fused in one launch; force applied after each
 //                    substep (bullet_cartpole.py:199-207); obs at each repeat end
@@ -12,7 +13,7 @@
 //
 // Memory: per-env state is SoA float32 [CP_STATE_FIELDS][B] in HBM (coalesced
 // per field); inside a launch the env lives in VGPRs and its contact rows in a
-// 40 KiB-per-wave LDS pool (4 waves per CU = 160 KiB).  DESIGN.md §Kernels.
+// 20 KiB-per-wave LDS pool (8 waves per CU = 160 KiB).  DESIGN.md §Kernels.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -27,6 +28,12 @@
 
 namespace cp {
 
+// occupancy target of the physics kernels (waves per SIMD); the register budget follows
+#ifndef CP_WAVES_PER_EU
+#define CP_WAVES_PER_EU 2
+#endif
+#define CP_PHYS_ATTR __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(CP_WAVES_PER_EU, CP_WAVES_PER_EU)))
+
 __constant__ float kDiscrete[CP_NUM_DISCRETE][2] = {{0.f, 0.f}, {-1.f, 0.f}, {1.f, 0.f}, {0.f, 1.f}, {0.f, -1.f}};
 
 struct Bufs {
@@ -39,7 +46,7 @@ struct Bufs {
     int32_t* overflow; // [B]
     int32_t* list;     // [B] reset list
     int32_t* count;    // [1] reset list length
-    float* scratch;    // [4*CP_NUM_PAIRS][B] manifold headers of the current substep
+    float* scratch;    // [4*CP_ISLAND_PAIRS][2B] manifold headers of the current substep, per lane
     uint64_t* stamps;  // [waves][8] diagnostic phase cycles (CP_STAMPS builds only)
 };
 
@@ -60,6 +67,7 @@ CP_DEV void flush_stamps(const Stamps& ST, uint64_t* dst, uint64_t total) {
     (void)ST; (void)dst; (void)total;
 #endif
 }
+
 
 CP_DEV uint32_t boff(int i) { return (uint32_t)i * 4u; }
 
@@ -175,7 +183,9 @@ __global__ void __launch_bounds__(256) cp_init_kernel(cp_config cfg, Bufs b) {
         st.st(CP_SF_BODY(d, 6), o, 1.0f);
     }
 #pragma unroll
-    for (int p = 0; p < CP_NUM_PAIRS; ++p) sti(st, CP_SF_WS_ID(p), o, -1);
+    for (int p = 0; p < CP_NUM_ISLANDS; ++p)
+#pragma unroll
+        for (int j = 0; j < CP_ISLAND_PAIRS; ++j) sti(st, CP_SF_WS_ID(p, j), o, -1);
     sti(st, CP_SF_DONE, o, 1);  // not reset yet: reference raises, batched API reports done
     b.ret_acc[i] = 0.0f;
     b.last_ret[i] = 0.0f;
@@ -197,15 +207,19 @@ __global__ void __launch_bounds__(256) cp_mask_to_list_kernel(int B, const uint8
     if (want) list[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
 }
 
-__global__ void __launch_bounds__(WAVE) cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
+__global__ void CP_PHYS_ATTR cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     __shared__ float lds_pool[POOL_FLOATS * WAVE];
     const int B = cfg.num_envs;
     const int t = blockIdx.x * WAVE + threadIdx.x;
     const int n = *b.count;
-    if (t >= n) return;  // lanes past the compacted list
-    const int i = b.list[t];
+    if ((t >> 1) >= n) return;  // lane pairs past the compacted list
+    const int isl = t & 1;
+    const bool lead = isl == 0;
+    const int i = b.list[t >> 1];
     float* pool = lds_pool + threadIdx.x;
-    const Mem G{Soa::make(b.state, B, CP_STATE_FIELDS), Soa::make(b.scratch, B, 4 * CP_NUM_PAIRS), boff(i)};
+    float* pool0 = lds_pool + (threadIdx.x & ~1u);
+    const Mem G = Mem::make(b.state, b.scratch, B, i, isl);
+    const Lane L = Lane::make(isl, cfg.phys);
     Stamps ST;
     Sim S;
     load_sim(S, G.st, G.off);  // pending forces survive the reset (pybullet keeps them)
@@ -218,15 +232,15 @@ __global__ void __launch_bounds__(WAVE) cp_reset_kernel(cp_config cfg, Bufs b, f
         S.b[d].w = mk(0.0f, 0.0f, 0.0f);
     }
 #pragma unroll
-    for (int p = 0; p < CP_NUM_PAIRS; ++p) {
-        sti(G.st, CP_SF_WS_ID(p), G.off, -1);
+    for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {  // the lane's island's warm-start cache
+        G.sw(CP_SF_WS_ID(0, j), __int_as_float(-1));
 #pragma unroll
-        for (int k = 0; k < 4; ++k) G.ss(CP_SF_WS_LAM(p, k), 0.0f);
+        for (int k = 0; k < 4; ++k) G.sl(CP_SF_WS_LAM(0, j, k), 0.0f);
     }
     int ov = 0;
     const int nsub = cfg.settle_steps + cfg.initial_force_steps;
     for (int s = 0; s < nsub; ++s) {
-        substep(S, cfg.phys, pool, ov, G, ST);
+        substep(S, cfg.phys, L, pool, pool0, ov, G, ST);
         const int k = s - cfg.settle_steps;
         if (k >= 0) {
             float fx, fy;
@@ -236,6 +250,8 @@ __global__ void __launch_bounds__(WAVE) cp_reset_kernel(cp_config cfg, Bufs b, f
             apply_force_link<1>(S, fx, fy);
         }
     }
+    ov += (int)partner_u((uint32_t)ov);
+    if (!lead) return;
     store_sim(S, G.st, G.off);
     b.overflow[i] += ov;
     float row[14];
@@ -252,26 +268,32 @@ __global__ void __launch_bounds__(WAVE) cp_reset_kernel(cp_config cfg, Bufs b, f
 }
 
 template <int KIND>
-__global__ void __launch_bounds__(WAVE) cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out,
+__global__ void CP_PHYS_ATTR cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out,
                                                         float* reward_out, uint8_t* done_out, float* term_out,
                                                         float* readback, int rb_bug) {
     __shared__ float lds_pool[POOL_FLOATS * WAVE];
     const int B = cfg.num_envs;
-    const int i = blockIdx.x * WAVE + threadIdx.x;
+    const int t = blockIdx.x * WAVE + threadIdx.x;
+    const int i = t >> 1, isl = t & 1;
+    const bool lead = isl == 0;  // lane 0 of the pair writes the env's outputs
     const bool inb = i < B;
     const int R = cfg.action_repeats, SR = cfg.steps_per_repeat;
     float* pool = lds_pool + threadIdx.x;
+    float* pool0 = lds_pool + (threadIdx.x & ~1u);
     bool want_reset = false;
     Stamps ST;
     CP_STAMP(k0);
     if (inb) {
-        const Mem G{Soa::make(b.state, B, CP_STATE_FIELDS), Soa::make(b.scratch, B, 4 * CP_NUM_PAIRS), boff(i)};
+        const Mem G = Mem::make(b.state, b.scratch, B, i, isl);
+        const Lane L = Lane::make(isl, cfg.phys);
         const Soa term = Soa::make(b.term_obs, B, R * 14);
         float* obs = obs_out + (size_t)i * R * 14;
         if (ldi(G.st, CP_SF_DONE, G.off)) {  // step after done (bullet_cartpole.py:179-181)
-            for (int f = 0; f < R * 14; ++f) obs[f] = term.ld(f, G.off);
-            reward_out[i] = 0.0f;
-            done_out[i] = 1;
+            if (lead) {
+                for (int f = 0; f < R * 14; ++f) obs[f] = term.ld(f, G.off);
+                reward_out[i] = 0.0f;
+                done_out[i] = 1;
+            }
         } else {
             float a00, a01, a10, a11;
             if constexpr (KIND == CP_ACTION_CONTINUOUS) {
@@ -292,41 +314,46 @@ __global__ void __launch_bounds__(WAVE) cp_step_kernel(cp_config cfg, Bufs b, co
             int ov = 0;
             for (int r = 0; r < R; ++r) {
                 for (int s = 0; s < SR; ++s) {
-                    substep(S, cfg.phys, pool, ov, G, ST);
+                    substep(S, cfg.phys, L, pool, pool0, ov, G, ST);
                     apply_force_link<0>(S, f00, f01);
                     apply_force_link<1>(S, f10, f11);
-                    if (readback) {
+                    if (readback && lead) {
                         float* rb = readback + (size_t)i * 2 * R * SR * 12;
                         readback_pole<1, 1>(S, rb + ((size_t)(0 * R + r) * SR + s) * 12);
                         if (rb_bug) readback_pole<3, 1>(S, rb + ((size_t)(1 * R + r) * SR + s) * 12);
                         else readback_pole<3, 3>(S, rb + ((size_t)(1 * R + r) * SR + s) * 12);
                     }
                 }
-                float row[14];
-                write_obs_row(S, row);
+                if (lead) {
+                    float row[14];
+                    write_obs_row(S, row);
 #pragma unroll
-                for (int f = 0; f < 14; ++f) obs[r * 14 + f] = row[f];
+                    for (int f = 0; f < 14; ++f) obs[r * 14 + f] = row[f];
+                }
             }
-            if (ov) b.overflow[i] += ov;
+            ov += (int)partner_u((uint32_t)ov);
+            if (ov && lead) b.overflow[i] += ov;
             const int steps = ldi(G.st, CP_SF_STEPS, G.off) + 1;
             bool done = steps >= cfg.max_episode_len;
             if (cfg.done_on_bounds && bounds_exceeded(S, cfg)) done = true;
-            store_sim(S, G.st, G.off);
-            sti(G.st, CP_SF_STEPS, G.off, steps);
-            reward_out[i] = 1.0f;  // bullet_cartpole.py:260
-            done_out[i] = done ? 1 : 0;
-            const float ret = b.ret_acc[i] + 1.0f;
-            if (done) {
-                b.last_ret[i] = ret;
-                b.last_len[i] = steps;
-                b.ret_acc[i] = 0.0f;
-                for (int f = 0; f < R * 14; ++f) term.st(f, G.off, obs[f]);
-                if (term_out)
-                    for (int f = 0; f < R * 14; ++f) term_out[(size_t)i * R * 14 + f] = obs[f];
-                sti(G.st, CP_SF_DONE, G.off, 1);
-                want_reset = cfg.autoreset != 0;
-            } else {
-                b.ret_acc[i] = ret;
+            if (lead) {
+                store_sim(S, G.st, G.off);
+                sti(G.st, CP_SF_STEPS, G.off, steps);
+                reward_out[i] = 1.0f;  // bullet_cartpole.py:260
+                done_out[i] = done ? 1 : 0;
+                const float ret = b.ret_acc[i] + 1.0f;
+                if (done) {
+                    b.last_ret[i] = ret;
+                    b.last_len[i] = steps;
+                    b.ret_acc[i] = 0.0f;
+                    for (int f = 0; f < R * 14; ++f) term.st(f, G.off, obs[f]);
+                    if (term_out)
+                        for (int f = 0; f < R * 14; ++f) term_out[(size_t)i * R * 14 + f] = obs[f];
+                    sti(G.st, CP_SF_DONE, G.off, 1);
+                    want_reset = cfg.autoreset != 0;
+                } else {
+                    b.ret_acc[i] = ret;
+                }
             }
         }
     }
@@ -337,7 +364,7 @@ __global__ void __launch_bounds__(WAVE) cp_step_kernel(cp_config cfg, Bufs b, co
     if (cfg.autoreset) {
         // wave ballot compaction of the finishing envs into the reset list
         const uint64_t bal = __ballot(want_reset);
-        const int lane = threadIdx.x;
+        const int lane = threadIdx.x;  // want_reset is set on lead lanes only
         const int n = __popcll(bal);
         int base = 0;
         if (lane == 0 && n) base = atomicAdd(b.count, n);
@@ -507,7 +534,7 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     CP_ALLOC(h->b.overflow, B * sizeof(int32_t));
     CP_ALLOC(h->b.list, B * sizeof(int32_t));
     CP_ALLOC(h->b.count, sizeof(int32_t));
-    CP_ALLOC(h->b.scratch, (size_t)4 * CP_NUM_PAIRS * B * sizeof(float));
+    CP_ALLOC(h->b.scratch, (size_t)4 * CP_ISLAND_PAIRS * 2 * B * sizeof(float));
     CP_ALLOC(h->b.stamps, 8 * sizeof(uint64_t));
 #undef CP_ALLOC
     e = hipMemset(h->b.stamps, 0, 8 * sizeof(uint64_t));
@@ -547,7 +574,7 @@ static int launch_reset_from_list(cp_handle* h, float* obs_out, hipStream_t st) 
     const int B = h->cfg.num_envs;
     hipEvent_t* ev = timing_slot(h, 1);
     if (ev) CP_TRY(h, hipEventRecord(ev[0], st));
-    hipLaunchKernelGGL(cp::cp_reset_kernel, dim3(grid_for(B, cp::WAVE)), dim3(cp::WAVE), 0, st, h->cfg, h->b, obs_out);
+    hipLaunchKernelGGL(cp::cp_reset_kernel, dim3(grid_for(2 * B, cp::WAVE)), dim3(cp::WAVE), 0, st, h->cfg, h->b, obs_out);
     if (check(h, hipGetLastError(), "cp_reset_kernel")) return -1;
     if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
     return 0;
@@ -574,7 +601,7 @@ int cp_step(cp_handle* h, const void* actions, int action_kind, float* obs_out, 
     const int B = h->cfg.num_envs;
     CP_TRY(h, hipSetDevice(h->device));
     if (h->cfg.autoreset) CP_TRY(h, hipMemsetAsync(h->b.count, 0, sizeof(int32_t), st));
-    dim3 grid(grid_for(B, cp::WAVE)), block(cp::WAVE);
+    dim3 grid(grid_for(2 * B, cp::WAVE)), block(cp::WAVE);  // two lanes per env
     hipEvent_t* ev = timing_slot(h, 0);
     if (ev) CP_TRY(h, hipEventRecord(ev[0], st));
     if (action_kind == CP_ACTION_CONTINUOUS)

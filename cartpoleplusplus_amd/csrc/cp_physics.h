@@ -1,12 +1,14 @@
-// cp_physics.h — one fixed physics step of the 5-body cartpole scene, per lane.
+// cp_physics.h — one fixed physics step of the 5-body cartpole scene, per lane pair.
 //
-// One lane simulates one environment (bullet_cartpole.py's whole pybullet world:
-// ground, cart, pole, cart2, pole2 — :154-160).  Per-env body state lives in
-// VGPRs with compile-time indices; the contact rows of a substep live in a
-// per-wave LDS pool laid out [field][slot][lane] (conflict-free ds_read_b32);
-// the 10 body pairs are walked by a wave-uniform loop in the narrowphase and by
-// statically unrolled per-pair code in the solver, so the solver never selects
-// bodies at run time.  The algorithm is DESIGN.md §Physics model; the CPU
+// Two adjacent lanes simulate one environment (bullet_cartpole.py's whole pybullet
+// world: ground, cart, pole, cart2, pole2 — :154-160); lane 2e+p owns contact
+// island p.  Both lanes hold the env's body state in VGPRs with compile-time
+// indices; each lane's contact rows live in its column of a per-wave LDS pool
+// laid out [field][slot][lane] (conflict-free ds_read_b32).  A lane walks its
+// island's 5 body pairs with a wave-uniform loop in the narrowphase and solves
+// its island with statically unrolled per-pair code on a 2-body local view; an
+// env with a cross-island contact is solved by both lanes redundantly in the
+// global order.  The algorithm is DESIGN.md §Physics model; the CPU
 // oracle (oracle/cp_oracle.c) states the same arithmetic, operation for operation.
 #pragma once
 #include "../../include/cartpole_amd.h"
@@ -28,14 +30,14 @@ struct Stamps {
 #endif
 
 constexpr int WAVE = 64;
-constexpr int MAXP = CP_MAX_POINTS;
-constexpr int MAXF = CP_MAX_FRICTION;
+constexpr int MAXP = CP_ISLAND_POINTS;    // per island (= per lane)
+constexpr int MAXF = CP_ISLAND_FRICTION;
 // pool fields (per normal point): rb.xyz, inv_eff, target, lambda
 constexpr int F_RBX = 0, F_RBY = 1, F_RBZ = 2, F_IE = 3, F_TG = 4, F_LAM = 5;
 constexpr int NPF = 6;
 // friction fields (per frictional point): lambda1, lambda2, inv_eff1, inv_eff2
 constexpr int FF_L1 = 0, FF_L2 = 1, FF_IE1 = 2, FF_IE2 = 3;
-constexpr int POOL_FLOATS = NPF * MAXP + 4 * MAXF;  // 160 floats per env = 40 KiB per wave
+constexpr int POOL_FLOATS = NPF * MAXP + 4 * MAXF;  // 80 floats per lane = 20 KiB per wave
 
 CP_DEV float& pool_n(float* pool, int field, int slot) { return pool[(field * MAXP + slot) * WAVE]; }
 CP_DEV float& pool_f(float* pool, int field, int slot) { return pool[(NPF * MAXP + field * MAXF + slot) * WAVE]; }
@@ -85,12 +87,29 @@ struct Soa {
 };
 struct Mem {
     Soa st;           // state SoA [CP_STATE_FIELDS][B]
-    Soa scr;          // scratch SoA [4*CP_NUM_PAIRS][B]
+    Soa scr;          // scratch SoA [4*CP_ISLAND_PAIRS][2B], one column per lane
     uint32_t off;     // env index * 4
+    uint32_t woff;    // off + island * CP_ISLAND_PAIRS fields  (warm-start ids of the lane's island)
+    uint32_t loff;    // off + island * 4*CP_ISLAND_PAIRS fields (warm-start impulses)
+    uint32_t xoff;    // (2 * env + island) * 4
+    CP_DEV static Mem make(float* state, float* scratch, int B, int env, int isl) {
+        Mem m;
+        m.st = Soa::make(state, B, CP_STATE_FIELDS);
+        m.scr = Soa::make(scratch, 2 * B, 4 * CP_ISLAND_PAIRS);
+        m.off = (uint32_t)env * 4u;
+        m.woff = m.off + (uint32_t)(isl * CP_ISLAND_PAIRS) * m.st.fstride;
+        m.loff = m.off + (uint32_t)(isl * 4 * CP_ISLAND_PAIRS) * m.st.fstride;
+        m.xoff = (uint32_t)(2 * env + isl) * 4u;
+        return m;
+    }
     CP_DEV float ls(int f) const { return st.ld(f, off); }
     CP_DEV void ss(int f, float v) const { st.st(f, off, v); }
-    CP_DEV float lx(int f) const { return scr.ld(f, off); }
-    CP_DEV void sx(int f, float v) const { scr.st(f, off, v); }
+    CP_DEV float lw(int f) const { return st.ld(f, woff); }
+    CP_DEV void sw(int f, float v) const { st.st(f, woff, v); }
+    CP_DEV float ll(int f) const { return st.ld(f, loff); }
+    CP_DEV void sl(int f, float v) const { st.st(f, loff, v); }
+    CP_DEV float lx(int f) const { return scr.ld(f, xoff); }
+    CP_DEV void sx(int f, float v) const { scr.st(f, xoff, v); }
 };
 
 struct Box {
@@ -113,6 +132,67 @@ struct Out4 {
     int m = 0;
 };
 
+// Face-contact geometry in reference-face coordinates (u, v along the face, n
+// along its normal): incident-face centre c, half edges e1, e2, vertices P[4].
+struct FaceGeom {
+    float hu, hv, margin;
+    float cu, cv, cn, e1u, e1v, e1n, e2u, e2v, e2n;
+    float Pu[4], Pv[4], Pn[4];
+    float idet;
+    bool all_in;  // all four incident vertices inside the reference rectangle: C1 only
+};
+
+// Candidate K (compile-time slot in the canonical order: C1 0-3, C2 4-7, C3 8-23)
+// and whether it is kept.  Same arithmetic as the oracle's candidate loops; the
+// candidates are re-evaluated per pass instead of stored (72 registers saved).
+template <int K>
+CP_DEV bool cand(const FaceGeom& G, float& u, float& v, float& n) {
+    if constexpr (K < 4) {
+        u = G.Pu[K]; v = G.Pv[K]; n = G.Pn[K];
+        return fabsf(G.Pu[K]) <= G.hu && fabsf(G.Pv[K]) <= G.hv && G.Pn[K] <= G.margin;
+    } else if constexpr (K < 8) {
+        constexpr int c = K - 4;
+        const float X = (c == 0 || c == 3) ? G.hu : -G.hu;
+        const float Y = (c < 2) ? G.hv : -G.hv;
+        const float ru = X - G.cu, rv = Y - G.cv;
+        const float al = fmaf_(ru, G.e2v, -(rv * G.e2u)) * G.idet;
+        const float be = fmaf_(G.e1u, rv, -(G.e1v * ru)) * G.idet;
+        const float dn = fmaf_(be, G.e2n, fmaf_(al, G.e1n, G.cn));
+        u = X; v = Y; n = dn;
+        return !G.all_in && fabsf(al) < 1.0f && fabsf(be) < 1.0f && dn <= G.margin;
+    } else {
+        constexpr int k = (K - 8) / 4, sd = (K - 8) % 4, k1 = (k + 1) & 3;
+        const float lim = (sd & 1) ? ((sd < 2) ? -G.hu : -G.hv) : ((sd < 2) ? G.hu : G.hv);
+        const float pc = (sd < 2) ? G.Pu[k] : G.Pv[k], qc = (sd < 2) ? G.Pu[k1] : G.Pv[k1];
+        const float dp = pc - lim, dq = qc - lim;
+        const bool cross_ = (dp < 0.0f && dq > 0.0f) || (dp > 0.0f && dq < 0.0f);
+        const float t = dp / (dp - dq);
+        bool inr;
+        if constexpr (sd < 2) {
+            u = lim;
+            v = fmaf_(G.Pv[k1] - G.Pv[k], t, G.Pv[k]);
+            inr = fabsf(v) <= G.hv;
+        } else {
+            v = lim;
+            u = fmaf_(G.Pu[k1] - G.Pu[k], t, G.Pu[k]);
+            inr = fabsf(u) <= G.hu;
+        }
+        n = fmaf_(G.Pn[k1] - G.Pn[k], t, G.Pn[k]);
+        return !G.all_in && cross_ && inr && n <= G.margin;
+    }
+}
+
+// compile-time loop over the 24 candidate slots
+template <int K = 0, typename Fn>
+CP_DEV void for_cands(const FaceGeom& G, Fn&& fn) {
+    if constexpr (K < 24) {
+        float u, v, n;
+        const bool ok = cand<K>(G, u, v, n);
+        fn(K, ok, u, v, n);
+        for_cands<K + 1>(G, fn);
+    }
+}
+
 // Face contact (oracle: face_contact).  Fills up to 4 selected candidates.
 CP_DEV void face_contact(const Box& R, int ri, V3 nr, const Box& I, float margin, V3& fc, V3& u, V3& v,
                          Out4& out) {
@@ -120,7 +200,10 @@ CP_DEV void face_contact(const Box& R, int ri, V3 nr, const Box& I, float margin
     fc = madd(R.c, nr, h_of(R, ri));
     u = axis_of(R.ax, r1);
     v = axis_of(R.ax, r2);
-    float hu = h_of(R, r1), hv = h_of(R, r2);
+    FaceGeom G;
+    G.margin = margin;
+    G.hu = h_of(R, r1);
+    G.hv = h_of(R, r2);
     float e0 = dot(nr, I.ax.a0), e1d = dot(nr, I.ax.a1), e2d = dot(nr, I.ax.a2);
     int j = 0;
     float best = fabsf(e0);
@@ -133,151 +216,77 @@ CP_DEV void face_contact(const Box& R, int ri, V3 nr, const Box& I, float margin
     V3 E1 = scl(axis_of(I.ax, j1), h_of(I, j1));
     V3 E2 = scl(axis_of(I.ax, j2), h_of(I, j2));
     V3 icr = sub(ic, fc);
-    float cu = dot(icr, u), cv = dot(icr, v), cn = dot(icr, nr);
-    float e1u = dot(E1, u), e1v = dot(E1, v), e1n = dot(E1, nr);
-    float e2u = dot(E2, u), e2v = dot(E2, v), e2n = dot(E2, nr);
-
-    float Pu[4], Pv[4], Pn[4];
-    Pu[0] = (cu + e1u) + e2u; Pv[0] = (cv + e1v) + e2v; Pn[0] = (cn + e1n) + e2n;
-    Pu[1] = (cu - e1u) + e2u; Pv[1] = (cv - e1v) + e2v; Pn[1] = (cn - e1n) + e2n;
-    Pu[2] = (cu - e1u) - e2u; Pv[2] = (cv - e1v) - e2v; Pn[2] = (cn - e1n) - e2n;
-    Pu[3] = (cu + e1u) - e2u; Pv[3] = (cv + e1v) - e2v; Pn[3] = (cn + e1n) - e2n;
-
-    // 24 candidate slots in canonical order: C1 0-3, C2 4-7, C3 8-23
-    float Cu[24], Cv[24], Cn[24];
-    uint32_t valid = 0;
+    G.cu = dot(icr, u); G.cv = dot(icr, v); G.cn = dot(icr, nr);
+    G.e1u = dot(E1, u); G.e1v = dot(E1, v); G.e1n = dot(E1, nr);
+    G.e2u = dot(E2, u); G.e2v = dot(E2, v); G.e2n = dot(E2, nr);
+    G.Pu[0] = (G.cu + G.e1u) + G.e2u; G.Pv[0] = (G.cv + G.e1v) + G.e2v; G.Pn[0] = (G.cn + G.e1n) + G.e2n;
+    G.Pu[1] = (G.cu - G.e1u) + G.e2u; G.Pv[1] = (G.cv - G.e1v) + G.e2v; G.Pn[1] = (G.cn - G.e1n) + G.e2n;
+    G.Pu[2] = (G.cu - G.e1u) - G.e2u; G.Pv[2] = (G.cv - G.e1v) - G.e2v; G.Pn[2] = (G.cn - G.e1n) - G.e2n;
+    G.Pu[3] = (G.cu + G.e1u) - G.e2u; G.Pv[3] = (G.cv + G.e1v) - G.e2v; G.Pn[3] = (G.cn + G.e1n) - G.e2n;
     int inside = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        Cu[k] = Pu[k]; Cv[k] = Pv[k]; Cn[k] = Pn[k];
-        const bool in = fabsf(Pu[k]) <= hu && fabsf(Pv[k]) <= hv;
-        inside += in ? 1 : 0;
-        if (in && Pn[k] <= margin) valid |= 1u << k;
+    for (int k = 0; k < 4; ++k) inside += (fabsf(G.Pu[k]) <= G.hu && fabsf(G.Pv[k]) <= G.hv) ? 1 : 0;
+    G.all_in = inside == 4;
+    G.idet = 0.0f;
+    if (!G.all_in) {
+        float det = fmaf_(G.e1u, G.e2v, -(G.e1v * G.e2u));
+        G.idet = 1.0f / det;
     }
-#pragma unroll
-    for (int k = 4; k < 24; ++k) { Cu[k] = 0.0f; Cv[k] = 0.0f; Cn[k] = 0.0f; }
-    // all four incident vertices inside the reference rectangle: C1 only (oracle: same rule)
-    if (inside != 4) {
-    float det = fmaf_(e1u, e2v, -(e1v * e2u));
-    float idet = 1.0f / det;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        float X = (c == 0 || c == 3) ? hu : -hu;
-        float Y = (c < 2) ? hv : -hv;
-        float ru = X - cu, rv = Y - cv;
-        float al = fmaf_(ru, e2v, -(rv * e2u)) * idet;
-        float be = fmaf_(e1u, rv, -(e1v * ru)) * idet;
-        float dn = fmaf_(be, e2n, fmaf_(al, e1n, cn));
-        Cu[4 + c] = X; Cv[4 + c] = Y; Cn[4 + c] = dn;
-        if (fabsf(al) < 1.0f && fabsf(be) < 1.0f && dn <= margin) valid |= 1u << (4 + c);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int k1 = (k + 1) & 3;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int slot = 8 + 4 * k + s;
-            float lim = (s & 1) ? ((s < 2) ? -hu : -hv) : ((s < 2) ? hu : hv);
-            float pc = (s < 2) ? Pu[k] : Pv[k], qc = (s < 2) ? Pu[k1] : Pv[k1];
-            float dp = pc - lim, dq = qc - lim;
-            bool cross_ = (dp < 0.0f && dq > 0.0f) || (dp > 0.0f && dq < 0.0f);
-            float t = dp / (dp - dq);
-            float xu, xv;
-            bool inr;
-            if (s < 2) {
-                xu = lim;
-                xv = fmaf_(Pv[k1] - Pv[k], t, Pv[k]);
-                inr = fabsf(xv) <= hv;
-            } else {
-                xv = lim;
-                xu = fmaf_(Pu[k1] - Pu[k], t, Pu[k]);
-                inr = fabsf(xu) <= hu;
-            }
-            float xn = fmaf_(Pn[k1] - Pn[k], t, Pn[k]);
-            Cu[slot] = xu; Cv[slot] = xv; Cn[slot] = xn;
-            if (cross_ && inr && xn <= margin) valid |= 1u << slot;
+    // pass 1: valid set and the deepest candidate (first minimum in canonical order)
+    uint32_t valid = 0;
+    int i0 = -1;
+    float bn = 0.0f, u0 = 0.0f, v0 = 0.0f;
+    for_cands(G, [&](int k, bool ok, float cu_, float cv_, float cn_) {
+        if (ok) {
+            valid |= 1u << k;
+            if (i0 < 0 || cn_ < bn) { i0 = k; bn = cn_; u0 = cu_; v0 = cv_; }
         }
-    }
-    }  // inside != 4
+    });
     uint32_t sel = valid;
     if (__builtin_popcount(valid) > 4) {
         // deepest; farthest from it; max / min signed area  (oracle: same rule)
-        int i0 = -1;
-        float bn = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 24; ++k)
-            if (((valid >> k) & 1u) && (i0 < 0 || Cn[k] < bn)) { i0 = k; bn = Cn[k]; }
-        float u0 = 0.0f, v0 = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 24; ++k)
-            if (k == i0) { u0 = Cu[k]; v0 = Cv[k]; }
         int i1 = -1;
-        float bd = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 24; ++k) {
-            if (!((valid >> k) & 1u) || k == i0) continue;
-            float du = Cu[k] - u0, dv = Cv[k] - v0;
+        float bd = 0.0f, u1 = 0.0f, v1 = 0.0f;
+        for_cands(G, [&](int k, bool ok, float cu_, float cv_, float) {
+            if (!ok || k == i0) return;
+            float du = cu_ - u0, dv = cv_ - v0;
             float d2 = fmaf_(du, du, dv * dv);
-            if (i1 < 0 || d2 > bd) { i1 = k; bd = d2; }
-        }
-        float u1 = 0.0f, v1 = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 24; ++k)
-            if (k == i1) { u1 = Cu[k]; v1 = Cv[k]; }
-        float ex = u1 - u0, ey = v1 - v0;
+            if (i1 < 0 || d2 > bd) { i1 = k; bd = d2; u1 = cu_; v1 = cv_; }
+        });
+        const float ex = u1 - u0, ey = v1 - v0;
         int i2 = -1;
         float ba = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 24; ++k) {
-            if (!((valid >> k) & 1u) || k == i0 || k == i1) continue;
-            float ar = fmaf_(ex, Cv[k] - v0, -(ey * (Cu[k] - u0)));
+        for_cands(G, [&](int k, bool ok, float cu_, float cv_, float) {
+            if (!ok || k == i0 || k == i1) return;
+            float ar = fmaf_(ex, cv_ - v0, -(ey * (cu_ - u0)));
             if (i2 < 0 || ar > ba) { i2 = k; ba = ar; }
-        }
+        });
         int i3 = -1;
         float bb = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 24; ++k) {
-            if (!((valid >> k) & 1u) || k == i0 || k == i1 || k == i2) continue;
-            float ar = fmaf_(ex, Cv[k] - v0, -(ey * (Cu[k] - u0)));
+        for_cands(G, [&](int k, bool ok, float cu_, float cv_, float) {
+            if (!ok || k == i0 || k == i1 || k == i2) return;
+            float ar = fmaf_(ex, cv_ - v0, -(ey * (cu_ - u0)));
             if (i3 < 0 || ar < bb) { i3 = k; bb = ar; }
-        }
+        });
         sel = (1u << i0) | (1u << i1) | (1u << i2) | (1u << i3);
     }
-    // compact the selected candidates, canonical order
+    // emit the selected candidates in canonical order
     out.m = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for_cands(G, [&](int k, bool, float cu_, float cv_, float cn_) {
         if ((sel >> k) & 1u) {
-            int m = out.m;
+            const int m = out.m;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if (m == j) {
-                    out.u[j] = Cu[k];
-                    out.v[j] = Cv[k];
-                    out.n[j] = Cn[k];
-                    out.id[j] = k;
+            for (int q = 0; q < 4; ++q) {
+                if (m == q) {
+                    out.u[q] = cu_;
+                    out.v[q] = cv_;
+                    out.n[q] = cn_;
+                    out.id[q] = k;
                 }
             }
             out.m = m + 1;
         }
-    }
-    if ((sel >> 4) == 0u) return;
-#pragma unroll
-    for (int k = 4; k < 24; ++k) {
-        if ((sel >> k) & 1u) {
-            int m = out.m;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if (m == j) {
-                    out.u[j] = Cu[k];
-                    out.v[j] = Cv[k];
-                    out.n[j] = Cn[k];
-                    out.id[j] = k;
-                }
-            }
-            out.m = m + 1;
-        }
-    }
+    });
 }
 
 // Contact result of one box pair in world space.
@@ -424,35 +433,210 @@ CP_DEV void plane_space(V3 n, V3& t1, V3& t2) {
 }
 
 // ----------------------------------------------------------------------------
+// Lane pairs.  Two adjacent lanes simulate one env: lane 2e+p owns contact island
+// p: island 0 = ground, cart, pole (pairs 0 1 4) plus the
+// cross pairs 5 6; island 1 = ground, cart2, pole2 (pairs 2 3 9) plus 7 8.  Both
+// lanes keep the whole env state; they exchange results through DPP swaps.
+CP_DEV float partner(float x) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
+}
+CP_DEV uint32_t partner_u(uint32_t x) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false); }
+CP_DEV V3 partner(V3 v) { return mk(partner(v.x), partner(v.y), partner(v.z)); }
+
+// global pair of island `isl`'s local pair j (oracle: ISLAND_PAIR)
+CP_DEV int island_pair(int isl, int j) { return (int)(((isl ? 0x87932u : 0x65410u) >> (4 * j)) & 15u); }
+__host__ __device__ constexpr int island_of(int p) { return (p == 2 || p == 3 || p >= 7) ? 1 : 0; }
+__host__ __device__ constexpr int local_of(int p) {
+    return p < 2 ? p : (p < 4 ? p - 2 : (p == 4 ? 2 : (p == 9 ? 2 : (p == 5 || p == 7 ? 3 : 4))));
+}
+
+// Per-lane constants of the lane's island (lane-varying copies of cp_physics fields).
+struct Lane {
+    int isl;
+    float im1, im2;      // inverse masses of the island's cart, pole
+    float ii1[3], ii2[3];  // their body-frame inverse inertias
+    float mu0, mu1, mu2; // friction products of local pairs 0..2
+    CP_DEV static Lane make(int isl, const cp_physics& P) {
+        Lane L;
+        L.isl = isl;
+        L.im1 = isl ? P.inv_mass[3] : P.inv_mass[1];
+        L.im2 = isl ? P.inv_mass[4] : P.inv_mass[2];
+        for (int k = 0; k < 3; ++k) {
+            L.ii1[k] = isl ? P.inv_inertia[3][k] : P.inv_inertia[1][k];
+            L.ii2[k] = isl ? P.inv_inertia[4][k] : P.inv_inertia[2][k];
+        }
+        const float fc = isl ? P.friction[3] : P.friction[1], fq = isl ? P.friction[4] : P.friction[2];
+        L.mu0 = P.friction[0] * fc;
+        L.mu1 = P.friction[0] * fq;
+        L.mu2 = fc * fq;
+        return L;
+    }
+};
+
 // Per-substep context (registers).
 struct Step {
-    Axes ax[CP_NUM_DYN];
-    Sym M[CP_NUM_DYN];
-    V3 n[CP_NUM_PAIRS];
-    uint32_t pk[CP_NUM_PAIRS];  // cnt | base<<3 | fcnt<<8 | fbase<<11
+    Sym M[CP_NUM_DYN];            // whole-env world inverse inertias (merged solve only)
+    V3 n[CP_ISLAND_PAIRS];        // own island's manifold normals
+    uint32_t pk[CP_ISLAND_PAIRS]; // cnt | base<<3 | fcnt<<8 | fbase<<11
 };
 CP_DEV int pk_cnt(uint32_t pk) { return (int)(pk & 7u); }
 CP_DEV int pk_base(uint32_t pk) { return (int)((pk >> 3) & 31u); }
 CP_DEV int pk_fcnt(uint32_t pk) { return (int)((pk >> 8) & 7u); }
 CP_DEV int pk_fbase(uint32_t pk) { return (int)((pk >> 11) & 15u); }
 
-// effective inverse mass along t (oracle: row_k); A == 0 is the static ground
+// ---- independent island solve: the island's two dynamic bodies in local slots
+// 1 (cart) and 2 (pole); slot 0 is the static ground.  Same arithmetic as the
+// oracle's solve_row / apply_impulse on the global bodies.
+struct Dyn {
+    V3 x, v, w;
+    Sym M;
+};
+struct Isl {
+    Dyn d1, d2;
+    float im1, im2;
+};
+template <int K>
+CP_DEV Dyn& dyn(Isl& I) {
+    if constexpr (K == 1) return I.d1;
+    else return I.d2;
+}
+template <int K>
+CP_DEV float dyn_im(const Isl& I) {
+    if constexpr (K == 1) return I.im1;
+    else return I.im2;
+}
+
 template <int A, int B>
-CP_DEV float row_k(const Sim& S, const Step& T, const cp_physics& P, V3 rb, V3 t) {
-    float imb = P.inv_mass[B];
+CP_DEV void isl_impulse(Isl& I, V3 rb, V3 t, float lam) {
+    Dyn& b = dyn<B>(I);
     V3 rbt = cross(rb, t);
-    V3 ib = symv(T.M[B - 1], rbt);
-    if constexpr (A == 0) {
-        return imb + dot(rbt, ib);
-    } else {
-        float ima = P.inv_mass[A];
-        V3 ra = add(rb, sub(S.b[B - 1].x, S.b[A - 1].x));
+    V3 ib = symv(b.M, rbt);
+    b.v = madd(b.v, t, lam * dyn_im<B>(I));
+    b.w = madd(b.w, ib, lam);
+    if constexpr (A != 0) {
+        Dyn& a = dyn<A>(I);
+        V3 ra = add(rb, sub(b.x, a.x));
         V3 rat = cross(ra, t);
-        V3 ia = symv(T.M[A - 1], rat);
-        return ((ima + imb) + dot(rat, ia)) + dot(rbt, ib);
+        V3 ia = symv(a.M, rat);
+        a.v = madd(a.v, neg(t), lam * dyn_im<A>(I));
+        a.w = madd(a.w, neg(ia), lam);
     }
 }
 
+template <int A, int B, bool FRICTION>
+CP_DEV float isl_row(Isl& I, V3 rb, V3 t, float inv_eff, float target, float& lam, float bound) {
+    Dyn& b = dyn<B>(I);
+    const float imb = dyn_im<B>(I);
+    V3 rbt = cross(rb, t);
+    V3 ib = symv(b.M, rbt);
+    float vn;
+    V3 ia = mk(0.0f, 0.0f, 0.0f);
+    if constexpr (A == 0) {
+        vn = dot(t, b.v) + dot(b.w, rbt);
+    } else {
+        Dyn& a = dyn<A>(I);
+        V3 ra = add(rb, sub(b.x, a.x));
+        V3 rat = cross(ra, t);
+        ia = symv(a.M, rat);
+        vn = (dot(t, sub(b.v, a.v)) + dot(b.w, rbt)) - dot(a.w, rat);
+    }
+    float e = target - vn;
+    float dl = e * inv_eff;
+    float l0 = lam + dl;
+    float ln;
+    if constexpr (!FRICTION) ln = l0 > 0.0f ? l0 : 0.0f;
+    else ln = l0 > bound ? bound : (l0 < -bound ? -bound : l0);
+    dl = ln - lam;
+    lam = ln;
+    float sb = dl * imb;
+    b.v = madd(b.v, t, sb);
+    b.w = madd(b.w, ib, dl);
+    if constexpr (A != 0) {
+        Dyn& a = dyn<A>(I);
+        float sa = dl * dyn_im<A>(I);
+        a.v = madd(a.v, neg(t), sa);
+        a.w = madd(a.w, neg(ia), dl);
+    }
+    return fabsf(e * dl);
+}
+
+// local pair j (0..2) of the island: (ground, cart), (ground, pole), (cart, pole)
+template <int J> constexpr int loc_a() { return J == 2 ? 1 : 0; }
+template <int J> constexpr int loc_b() { return J == 0 ? 1 : 2; }
+
+template <int J>
+CP_DEV void isl_warmstart(Isl& I, const Step& T, float* pool) {
+    const uint32_t pk = T.pk[J];
+    const int cnt = pk_cnt(pk), base = pk_base(pk);
+    for (int k = 0; k < cnt; ++k) {
+        const int s = base + k;
+        V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
+        isl_impulse<loc_a<J>(), loc_b<J>()>(I, rb, T.n[J], pool_n(pool, F_LAM, s));
+    }
+}
+
+template <int J>
+CP_DEV void isl_normal_rows(Isl& I, const Step& T, float* pool, float& resid) {
+    const uint32_t pk = T.pk[J];
+    const int cnt = pk_cnt(pk), base = pk_base(pk);
+    for (int k = 0; k < cnt; ++k) {
+        const int s = base + k;
+        V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
+        float lam = pool_n(pool, F_LAM, s);
+        float r = isl_row<loc_a<J>(), loc_b<J>(), false>(I, rb, T.n[J], pool_n(pool, F_IE, s),
+                                                         pool_n(pool, F_TG, s), lam, 0.0f);
+        pool_n(pool, F_LAM, s) = lam;
+        resid = resid + r;
+    }
+}
+
+template <int J>
+CP_DEV void isl_friction_rows(Isl& I, const Step& T, float mu, float* pool, float& resid) {
+    const uint32_t pk = T.pk[J];
+    const int fcnt = pk_fcnt(pk);
+    if (fcnt == 0) return;
+    const int base = pk_base(pk), fbase = pk_fbase(pk);
+    // tangent basis inside the sweep (hoisted out of the PGS loop it pins VGPRs)
+    V3 n = T.n[J];
+    asm volatile("" : "+v"(n.x), "+v"(n.y), "+v"(n.z));
+    V3 t1, t2;
+    plane_space(n, t1, t2);
+    for (int k = 0; k < fcnt; ++k) {
+        const int s = base + k, fs = fbase + k;
+        V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
+        float bound = mu * pool_n(pool, F_LAM, s);
+        float l1 = pool_f(pool, FF_L1, fs), l2 = pool_f(pool, FF_L2, fs);
+        float r1 = isl_row<loc_a<J>(), loc_b<J>(), true>(I, rb, t1, pool_f(pool, FF_IE1, fs), 0.0f, l1, bound);
+        resid = resid + r1;
+        float r2 = isl_row<loc_a<J>(), loc_b<J>(), true>(I, rb, t2, pool_f(pool, FF_IE2, fs), 0.0f, l2, bound);
+        resid = resid + r2;
+        pool_f(pool, FF_L1, fs) = l1;
+        pool_f(pool, FF_L2, fs) = l2;
+    }
+}
+
+// ---- merged solve (an env with a cross-island contact): both lanes run the
+// oracle's global-order solve redundantly on the whole env, reading each
+// island's rows from that island's lane column of the LDS pool and its manifold
+// header from that island's lane registers (DPP; both lanes of a merged env are
+// active, so the partner read is defined).
+struct Hdr {
+    V3 n;
+    uint32_t pk;
+};
+template <int PAIR>
+CP_DEV Hdr pair_hdr(const Step& T, bool second) {
+    constexpr int j = local_of(PAIR);
+    const bool mine = (island_of(PAIR) != 0) == second;
+    const V3 on = partner(T.n[j]);
+    const uint32_t opk = partner_u(T.pk[j]);
+    Hdr h;
+    h.n = selv(mine, T.n[j], on);
+    h.pk = mine ? T.pk[j] : opk;
+    return h;
+}
+
+// impulse lam along t at rb (oracle: apply_impulse); A == 0 is the static ground
 template <int A, int B>
 CP_DEV void apply_impulse(Sim& S, const Step& T, const cp_physics& P, V3 rb, V3 t, float lam) {
     V3 rbt = cross(rb, t);
@@ -504,132 +688,33 @@ CP_DEV float solve_row(Sim& S, const Step& T, const cp_physics& P, V3 rb, V3 t, 
     return fabsf(e * dl);
 }
 
-// One PGS row committed only where `act` (selects, not branches, so that two
-// independent rows can share a basic block and interleave).  Same arithmetic as
-// solve_row; returns |e * dlambda| or 0.
-template <int A, int B, bool FRICTION>
-CP_DEV float solve_row_sel(Sim& S, const Step& T, const cp_physics& P, V3 rb, V3 t, float inv_eff, float target,
-                           float& lam, float bound, bool act) {
-    float imb = P.inv_mass[B];
-    V3 rbt = cross(rb, t);
-    V3 ib = symv(T.M[B - 1], rbt);
-    float vn;
-    V3 ia = mk(0.0f, 0.0f, 0.0f);
-    if constexpr (A == 0) {
-        vn = dot(t, S.b[B - 1].v) + dot(S.b[B - 1].w, rbt);
-    } else {
-        V3 ra = add(rb, sub(S.b[B - 1].x, S.b[A - 1].x));
-        V3 rat = cross(ra, t);
-        ia = symv(T.M[A - 1], rat);
-        vn = (dot(t, sub(S.b[B - 1].v, S.b[A - 1].v)) + dot(S.b[B - 1].w, rbt)) - dot(S.b[A - 1].w, rat);
-    }
-    float e = target - vn;
-    float dl = e * inv_eff;
-    float l0 = lam + dl;
-    float ln;
-    if constexpr (!FRICTION) ln = l0 > 0.0f ? l0 : 0.0f;
-    else ln = l0 > bound ? bound : (l0 < -bound ? -bound : l0);
-    dl = ln - lam;
-    lam = act ? ln : lam;
-    float sb = dl * imb;
-    S.b[B - 1].v = selv(act, madd(S.b[B - 1].v, t, sb), S.b[B - 1].v);
-    S.b[B - 1].w = selv(act, madd(S.b[B - 1].w, ib, dl), S.b[B - 1].w);
-    if constexpr (A != 0) {
-        float sa = dl * P.inv_mass[A];
-        S.b[A - 1].v = selv(act, madd(S.b[A - 1].v, neg(t), sa), S.b[A - 1].v);
-        S.b[A - 1].w = selv(act, madd(S.b[A - 1].w, neg(ia), dl), S.b[A - 1].w);
-    }
-    return act ? fabsf(e * dl) : 0.0f;
-}
-
-// Normal rows of two pairs from different islands, interleaved row by row.
-template <int PA, int PB>
-CP_DEV void pair2_normal_rows(Sim& S, const Step& T, const cp_physics& P, float* pool, float& resA, float& resB) {
-    const uint32_t pkA = T.pk[PA], pkB = T.pk[PB];
-    const int cA = pk_cnt(pkA), bA = pk_base(pkA), cB = pk_cnt(pkB), bB = pk_base(pkB);
-    const int n = cA > cB ? cA : cB;
-    for (int k = 0; k < n; ++k) {
-        const bool actA = k < cA, actB = k < cB;
-        const int sA = (bA + k) < MAXP ? bA + k : MAXP - 1;
-        const int sB = (bB + k) < MAXP ? bB + k : MAXP - 1;
-        V3 rbA = mk(pool_n(pool, F_RBX, sA), pool_n(pool, F_RBY, sA), pool_n(pool, F_RBZ, sA));
-        V3 rbB = mk(pool_n(pool, F_RBX, sB), pool_n(pool, F_RBY, sB), pool_n(pool, F_RBZ, sB));
-        float ieA = pool_n(pool, F_IE, sA), tgA = pool_n(pool, F_TG, sA), lamA = pool_n(pool, F_LAM, sA);
-        float ieB = pool_n(pool, F_IE, sB), tgB = pool_n(pool, F_TG, sB), lamB = pool_n(pool, F_LAM, sB);
-        float rA = solve_row_sel<pair_a(PA), pair_b(PA), false>(S, T, P, rbA, T.n[PA], ieA, tgA, lamA, 0.0f, actA);
-        float rB = solve_row_sel<pair_a(PB), pair_b(PB), false>(S, T, P, rbB, T.n[PB], ieB, tgB, lamB, 0.0f, actB);
-        resA = resA + rA;
-        resB = resB + rB;
-        if (actA) pool_n(pool, F_LAM, sA) = lamA;
-        if (actB) pool_n(pool, F_LAM, sB) = lamB;
-    }
-}
-
-// Friction rows (t1 then t2 per point) of two pairs from different islands, interleaved.
-template <int PA, int PB>
-CP_DEV void pair2_friction_rows(Sim& S, const Step& T, const cp_physics& P, float* pool, float& resA,
-                                float& resB) {
-    const uint32_t pkA = T.pk[PA], pkB = T.pk[PB];
-    const int cA = pk_fcnt(pkA), cB = pk_fcnt(pkB);
-    const int n = cA > cB ? cA : cB;
-    if (n == 0) return;
-    const int bA = pk_base(pkA), fA = pk_fbase(pkA), bB = pk_base(pkB), fB = pk_fbase(pkB);
-    const float muA = P.friction[pair_a(PA)] * P.friction[pair_b(PA)];
-    const float muB = P.friction[pair_a(PB)] * P.friction[pair_b(PB)];
-    // tangent basis inside the sweep: hoisted out of the PGS loop for every pair it
-    // would pin ~60 VGPRs for the whole solve
-    V3 nA = T.n[PA], nB = T.n[PB];
-    asm volatile("" : "+v"(nA.x), "+v"(nA.y), "+v"(nA.z), "+v"(nB.x), "+v"(nB.y), "+v"(nB.z));
-    V3 a1, a2, b1, b2;
-    plane_space(nA, a1, a2);
-    plane_space(nB, b1, b2);
-    for (int k = 0; k < n; ++k) {
-        const bool actA = k < cA, actB = k < cB;
-        const int sA = (bA + k) < MAXP ? bA + k : MAXP - 1, sB = (bB + k) < MAXP ? bB + k : MAXP - 1;
-        const int gA = (fA + k) < MAXF ? fA + k : MAXF - 1, gB = (fB + k) < MAXF ? fB + k : MAXF - 1;
-        V3 rbA = mk(pool_n(pool, F_RBX, sA), pool_n(pool, F_RBY, sA), pool_n(pool, F_RBZ, sA));
-        V3 rbB = mk(pool_n(pool, F_RBX, sB), pool_n(pool, F_RBY, sB), pool_n(pool, F_RBZ, sB));
-        const float boundA = muA * pool_n(pool, F_LAM, sA), boundB = muB * pool_n(pool, F_LAM, sB);
-        float lA1 = pool_f(pool, FF_L1, gA), lA2 = pool_f(pool, FF_L2, gA);
-        float lB1 = pool_f(pool, FF_L1, gB), lB2 = pool_f(pool, FF_L2, gB);
-        const float ieA1 = pool_f(pool, FF_IE1, gA), ieA2 = pool_f(pool, FF_IE2, gA);
-        const float ieB1 = pool_f(pool, FF_IE1, gB), ieB2 = pool_f(pool, FF_IE2, gB);
-        constexpr int AA = pair_a(PA), AB = pair_b(PA), BA = pair_a(PB), BB = pair_b(PB);
-        float rA1 = solve_row_sel<AA, AB, true>(S, T, P, rbA, a1, ieA1, 0.0f, lA1, boundA, actA);
-        float rB1 = solve_row_sel<BA, BB, true>(S, T, P, rbB, b1, ieB1, 0.0f, lB1, boundB, actB);
-        resA = resA + rA1;
-        resB = resB + rB1;
-        float rA2 = solve_row_sel<AA, AB, true>(S, T, P, rbA, a2, ieA2, 0.0f, lA2, boundA, actA);
-        float rB2 = solve_row_sel<BA, BB, true>(S, T, P, rbB, b2, ieB2, 0.0f, lB2, boundB, actB);
-        resA = resA + rA2;
-        resB = resB + rB2;
-        if (actA) { pool_f(pool, FF_L1, gA) = lA1; pool_f(pool, FF_L2, gA) = lA2; }
-        if (actB) { pool_f(pool, FF_L1, gB) = lB1; pool_f(pool, FF_L2, gB) = lB2; }
-    }
-}
-
 template <int PAIR>
-CP_DEV void pair_warmstart(Sim& S, const Step& T, const cp_physics& P, float* pool) {
+CP_DEV void pair_warmstart(Sim& S, const Step& T, bool second, const cp_physics& P, float* pool0) {
     constexpr int A = pair_a(PAIR), B = pair_b(PAIR);
-    const uint32_t pk = T.pk[PAIR];
+    float* pool = pool0 + island_of(PAIR);
+    const Hdr H = pair_hdr<PAIR>(T, second);
+    const uint32_t pk = H.pk;
     const int cnt = pk_cnt(pk), base = pk_base(pk);
     for (int k = 0; k < cnt; ++k) {
         const int s = base + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
-        apply_impulse<A, B>(S, T, P, rb, T.n[PAIR], pool_n(pool, F_LAM, s));
+        apply_impulse<A, B>(S, T, P, rb, H.n, pool_n(pool, F_LAM, s));
     }
 }
 
 template <int PAIR>
-CP_DEV void pair_normal_rows(Sim& S, const Step& T, const cp_physics& P, float* pool, float& resid) {
+CP_DEV void pair_normal_rows(Sim& S, const Step& T, bool second, const cp_physics& P, float* pool0,
+                             float& resid) {
     constexpr int A = pair_a(PAIR), B = pair_b(PAIR);
-    const uint32_t pk = T.pk[PAIR];
+    float* pool = pool0 + island_of(PAIR);
+    const Hdr H = pair_hdr<PAIR>(T, second);
+    const uint32_t pk = H.pk;
     const int cnt = pk_cnt(pk), base = pk_base(pk);
     for (int k = 0; k < cnt; ++k) {
         const int s = base + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
         float lam = pool_n(pool, F_LAM, s);
-        float r = solve_row<A, B, false>(S, T, P, rb, T.n[PAIR], pool_n(pool, F_IE, s), pool_n(pool, F_TG, s),
+        float r = solve_row<A, B, false>(S, T, P, rb, H.n, pool_n(pool, F_IE, s), pool_n(pool, F_TG, s),
                                          lam, 0.0f);
         pool_n(pool, F_LAM, s) = lam;
         resid = resid + r;
@@ -637,16 +722,17 @@ CP_DEV void pair_normal_rows(Sim& S, const Step& T, const cp_physics& P, float* 
 }
 
 template <int PAIR>
-CP_DEV void pair_friction_rows(Sim& S, const Step& T, const cp_physics& P, float* pool, float& resid) {
+CP_DEV void pair_friction_rows(Sim& S, const Step& T, bool second, const cp_physics& P, float* pool0,
+                               float& resid) {
     constexpr int A = pair_a(PAIR), B = pair_b(PAIR);
-    const uint32_t pk = T.pk[PAIR];
+    float* pool = pool0 + island_of(PAIR);
+    const Hdr H = pair_hdr<PAIR>(T, second);
+    const uint32_t pk = H.pk;
     const int fcnt = pk_fcnt(pk);
     if (fcnt == 0) return;
     const int base = pk_base(pk), fbase = pk_fbase(pk);
     const float mu = P.friction[A] * P.friction[B];
-    // keep the tangent basis inside the sweep: hoisted out of the PGS loop for all
-    // 10 pairs it would pin ~60 VGPRs for the whole solve
-    V3 n = T.n[PAIR];
+    V3 n = H.n;
     asm volatile("" : "+v"(n.x), "+v"(n.y), "+v"(n.z));
     V3 t1, t2;
     plane_space(n, t1, t2);
@@ -664,19 +750,7 @@ CP_DEV void pair_friction_rows(Sim& S, const Step& T, const cp_physics& P, float
     }
 }
 
-template <int PAIR>
-CP_DEV void pair_cache(const Step& T, float* pool, const Mem& G) {
-    const uint32_t pk = T.pk[PAIR];
-    const int cnt = pk_cnt(pk), base = pk_base(pk);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) G.ss(CP_SF_WS_LAM(PAIR, k), (k < cnt) ? pool_n(pool, F_LAM, base + k) : 0.0f);
-}
-
-#define CP_FOR_PAIRS(F, ...) \
-    F<0>(__VA_ARGS__); F<1>(__VA_ARGS__); F<2>(__VA_ARGS__); F<3>(__VA_ARGS__); F<4>(__VA_ARGS__); \
-    F<5>(__VA_ARGS__); F<6>(__VA_ARGS__); F<7>(__VA_ARGS__); F<8>(__VA_ARGS__); F<9>(__VA_ARGS__)
-
-// ---- uniform-index accessors for the wave-uniform narrowphase pair loop ----
+// ---- uniform-index accessors for the narrowphase pair loop (g may vary by lane) ----
 CP_DEV V3 sel5v(int g, V3 z, V3 a, V3 b, V3 c, V3 d) {
     return mk(g == 1 ? a.x : g == 2 ? b.x : g == 3 ? c.x : g == 4 ? d.x : z.x,
               g == 1 ? a.y : g == 2 ? b.y : g == 3 ? c.y : g == 4 ? d.y : z.y,
@@ -685,27 +759,44 @@ CP_DEV V3 sel5v(int g, V3 z, V3 a, V3 b, V3 c, V3 d) {
 CP_DEV float sel5(int g, float z, float a, float b, float c, float d) {
     return g == 1 ? a : g == 2 ? b : g == 3 ? c : g == 4 ? d : z;
 }
-CP_DEV Box box_of(int g, const Sim& S, const Step& T, const cp_physics& P) {
+CP_DEV float sel5p(int g, const float* v) { return sel5(g, v[0], v[1], v[2], v[3], v[4]); }
+// Box of body g (lane-varying) with its world inverse inertia, from the pose in S:
+// the axes are rebuilt from the quaternion here rather than kept live through the
+// narrowphase (same arithmetic as the per-body quat_axes / world_inv_inertia).
+CP_DEV Box box_sel(int g, const Sim& S, const cp_physics& P) {
     Box b;
-    b.h0 = P.half_extents[g][0];
-    b.h1 = P.half_extents[g][1];
-    b.h2 = P.half_extents[g][2];
-    const V3 z = mk(0.0f, 0.0f, 0.0f);
-    b.c = sel5v(g, z, S.b[0].x, S.b[1].x, S.b[2].x, S.b[3].x);
-    b.ax.a0 = sel5v(g, mk(1.0f, 0.0f, 0.0f), T.ax[0].a0, T.ax[1].a0, T.ax[2].a0, T.ax[3].a0);
-    b.ax.a1 = sel5v(g, mk(0.0f, 1.0f, 0.0f), T.ax[0].a1, T.ax[1].a1, T.ax[2].a1, T.ax[3].a1);
-    b.ax.a2 = sel5v(g, mk(0.0f, 0.0f, 1.0f), T.ax[0].a2, T.ax[1].a2, T.ax[2].a2, T.ax[3].a2);
+    b.h0 = sel5(g, P.half_extents[0][0], P.half_extents[1][0], P.half_extents[2][0], P.half_extents[3][0],
+                P.half_extents[4][0]);
+    b.h1 = sel5(g, P.half_extents[0][1], P.half_extents[1][1], P.half_extents[2][1], P.half_extents[3][1],
+                P.half_extents[4][1]);
+    b.h2 = sel5(g, P.half_extents[0][2], P.half_extents[1][2], P.half_extents[2][2], P.half_extents[3][2],
+                P.half_extents[4][2]);
+    b.c = sel5v(g, mk(0.0f, 0.0f, 0.0f), S.b[0].x, S.b[1].x, S.b[2].x, S.b[3].x);
+    const float qx = sel5(g, 0.0f, S.b[0].q[0], S.b[1].q[0], S.b[2].q[0], S.b[3].q[0]);
+    const float qy = sel5(g, 0.0f, S.b[0].q[1], S.b[1].q[1], S.b[2].q[1], S.b[3].q[1]);
+    const float qz = sel5(g, 0.0f, S.b[0].q[2], S.b[1].q[2], S.b[2].q[2], S.b[3].q[2]);
+    const float qw = sel5(g, 1.0f, S.b[0].q[3], S.b[1].q[3], S.b[2].q[3], S.b[3].q[3]);
+    b.ax = quat_axes(qx, qy, qz, qw);  // identity, exactly, for the ground
     return b;
 }
-CP_DEV Sym sym_of(int g, const Step& T) {
-    Sym m;
-    m.m0 = sel5(g, 0.0f, T.M[0].m0, T.M[1].m0, T.M[2].m0, T.M[3].m0);
-    m.m1 = sel5(g, 0.0f, T.M[0].m1, T.M[1].m1, T.M[2].m1, T.M[3].m1);
-    m.m2 = sel5(g, 0.0f, T.M[0].m2, T.M[1].m2, T.M[2].m2, T.M[3].m2);
-    m.m3 = sel5(g, 0.0f, T.M[0].m3, T.M[1].m3, T.M[2].m3, T.M[3].m3);
-    m.m4 = sel5(g, 0.0f, T.M[0].m4, T.M[1].m4, T.M[2].m4, T.M[3].m4);
-    m.m5 = sel5(g, 0.0f, T.M[0].m5, T.M[1].m5, T.M[2].m5, T.M[3].m5);
-    return m;
+CP_DEV Sym inertia_sel(int g, const Box& b, const cp_physics& P) {
+    return world_inv_inertia(b.ax, sel5(g, P.inv_inertia[0][0], P.inv_inertia[1][0], P.inv_inertia[2][0],
+                                        P.inv_inertia[3][0], P.inv_inertia[4][0]),
+                             sel5(g, P.inv_inertia[0][1], P.inv_inertia[1][1], P.inv_inertia[2][1],
+                                  P.inv_inertia[3][1], P.inv_inertia[4][1]),
+                             sel5(g, P.inv_inertia[0][2], P.inv_inertia[1][2], P.inv_inertia[2][2],
+                                  P.inv_inertia[3][2], P.inv_inertia[4][2]));
+}
+
+// Broadphase: true when a face axis of A already separates the pair by more than
+// the margin (bounding radius of B as its projection, plus 1e-3 m of slack for
+// rounding), i.e. when box_box would return no contact from its face-axis test.
+CP_DEV bool face_separated(const Box& A, const Box& B, float margin) {
+    const V3 d = sub(B.c, A.c);
+    const float rb = sqrtf(fmaf_(B.h0, B.h0, fmaf_(B.h1, B.h1, B.h2 * B.h2)));
+    const float lim = (margin + 1e-3f) + rb;
+    return (fabsf(dot(d, A.ax.a0)) - A.h0 > lim) || (fabsf(dot(d, A.ax.a1)) - A.h1 > lim) ||
+           (fabsf(dot(d, A.ax.a2)) - A.h2 > lim);
 }
 CP_DEV V3 pos_of(int g, const Sim& S) {
     return sel5v(g, mk(0.0f, 0.0f, 0.0f), S.b[0].x, S.b[1].x, S.b[2].x, S.b[3].x);
@@ -722,33 +813,85 @@ CP_DEV float row_k_dyn(int a, float ima, float imb, V3 xa, V3 xb, const Sym& Ma,
     return ((ima + imb) + dot(rat, ia)) + dot(rbt, ib);
 }
 
+// select the island's (cart, pole) out of the env (island 1 -> cart2, pole2)
+CP_DEV Dyn dyn_sel(bool second, const Body& a, const Sym& Ma, const Body& b, const Sym& Mb) {
+    Dyn d;
+    d.x = selv(second, b.x, a.x);
+    d.v = selv(second, b.v, a.v);
+    d.w = selv(second, b.w, a.w);
+    d.M.m0 = second ? Mb.m0 : Ma.m0;
+    d.M.m1 = second ? Mb.m1 : Ma.m1;
+    d.M.m2 = second ? Mb.m2 : Ma.m2;
+    d.M.m3 = second ? Mb.m3 : Ma.m3;
+    d.M.m4 = second ? Mb.m4 : Ma.m4;
+    d.M.m5 = second ? Mb.m5 : Ma.m5;
+    return d;
+}
+
+// whole-env view for the cross rows: velocities and inverse inertias of the own
+// island's bodies from this lane, the other island's from the partner lane (both
+// lanes of a merged env are active wherever this runs); positions are in S.
+CP_DEV Sym partner_sym(const Sym& m) {
+    Sym r;
+    r.m0 = partner(m.m0); r.m1 = partner(m.m1); r.m2 = partner(m.m2);
+    r.m3 = partner(m.m3); r.m4 = partner(m.m4); r.m5 = partner(m.m5);
+    return r;
+}
+CP_DEV Sym sel_sym(bool t, const Sym& a, const Sym& b) {
+    Sym r;
+    r.m0 = t ? a.m0 : b.m0; r.m1 = t ? a.m1 : b.m1; r.m2 = t ? a.m2 : b.m2;
+    r.m3 = t ? a.m3 : b.m3; r.m4 = t ? a.m4 : b.m4; r.m5 = t ? a.m5 : b.m5;
+    return r;
+}
+CP_DEV void cross_view(Sim& S, Step& T, const Isl& I, bool second) {
+    const V3 v1 = partner(I.d1.v), w1 = partner(I.d1.w), v2 = partner(I.d2.v), w2 = partner(I.d2.w);
+    const Sym M1 = partner_sym(I.d1.M), M2 = partner_sym(I.d2.M);
+    S.b[0].v = selv(second, v1, I.d1.v);
+    S.b[0].w = selv(second, w1, I.d1.w);
+    S.b[1].v = selv(second, v2, I.d2.v);
+    S.b[1].w = selv(second, w2, I.d2.w);
+    S.b[2].v = selv(second, I.d1.v, v1);
+    S.b[2].w = selv(second, I.d1.w, w1);
+    S.b[3].v = selv(second, I.d2.v, v2);
+    S.b[3].w = selv(second, I.d2.w, w2);
+    T.M[0] = sel_sym(second, M1, I.d1.M);
+    T.M[1] = sel_sym(second, M2, I.d2.M);
+    T.M[2] = sel_sym(second, I.d1.M, M1);
+    T.M[3] = sel_sym(second, I.d2.M, M2);
+}
+CP_DEV void cross_back(Isl& I, const Sim& S, bool second) {
+    I.d1.v = selv(second, S.b[2].v, S.b[0].v);
+    I.d1.w = selv(second, S.b[2].w, S.b[0].w);
+    I.d2.v = selv(second, S.b[3].v, S.b[1].v);
+    I.d2.w = selv(second, S.b[3].w, S.b[1].w);
+}
+
 // One p.stepSimulation() for this lane's env (DESIGN.md §Physics model 1-6).
-CP_DEV void substep(Sim& S, const cp_physics& P, float* pool, int& overflow, const Mem& G, Stamps& ST) {
+// pool = this lane's LDS column, pool0 = the env's island-0 column (pool0 + 1 is island 1's).
+CP_DEV void substep(Sim& S, const cp_physics& P, const Lane& L, float* pool, float* pool0, int& overflow,
+                    const Mem& G, Stamps& ST) {
     const float dt = P.dt, inv_dt = P.inv_dt;
     CP_STAMP(t0);
     Step T;
-    // 1. orientation + world inverse inertia
-#pragma unroll
-    for (int d = 0; d < CP_NUM_DYN; ++d) {
-        T.ax[d] = quat_axes(S.b[d].q[0], S.b[d].q[1], S.b[d].q[2], S.b[d].q[3]);
-        T.M[d] = world_inv_inertia(T.ax[d], P.inv_inertia[d + 1][0], P.inv_inertia[d + 1][1],
-                                   P.inv_inertia[d + 1][2]);
-    }
-    // 2. narrowphase + row setup, wave-uniform loop over the 10 pairs
+    // 2. narrowphase + row setup of the lane's island: wave-uniform loop over its 5
+    //    local pairs (the global pair, hence the bodies, differ between the two lanes)
     int used = 0, fused = 0;
 #pragma unroll 1
-    for (int p = 0; p < CP_NUM_PAIRS; ++p) {
-        const int a = pair_a(p), b = pair_b(p);
-        Box A = box_of(a, S, T, P), Bx = box_of(b, S, T, P);
+    for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
+        const int g = island_pair(L.isl, j);
+        const int a = pair_a(g), b = pair_b(g);
+        const Box A = box_sel(a, S, P), Bx = box_sel(b, S, P);
         Contact C;
-        box_box(A, Bx, P.contact_margin, P.edge_bias, C);
-        const float mu = P.friction[a] * P.friction[b];
-        const float ima = P.inv_mass[a], imb = P.inv_mass[b];
-        const V3 xa = pos_of(a, S), xb = pos_of(b, S);
-        const Sym Ma = sym_of(a, T), Mb = sym_of(b, T);
-        const uint32_t oid = __float_as_uint(G.ls(CP_SF_WS_ID(p)));
-        const float ol0 = G.ls(CP_SF_WS_LAM(p, 0)), ol1 = G.ls(CP_SF_WS_LAM(p, 1));
-        const float ol2 = G.ls(CP_SF_WS_LAM(p, 2)), ol3 = G.ls(CP_SF_WS_LAM(p, 3));
+        C.m = 0;
+        C.n = mk(0.0f, 0.0f, 1.0f);
+        if (!face_separated(A, Bx, P.contact_margin)) box_box(A, Bx, P.contact_margin, P.edge_bias, C);
+        const float mu = sel5p(a, P.friction) * sel5p(b, P.friction);
+        const float ima = sel5p(a, P.inv_mass), imb = sel5p(b, P.inv_mass);
+        const V3 xa = A.c, xb = Bx.c;
+        const Sym Ma = inertia_sel(a, A, P), Mb = inertia_sel(b, Bx, P);
+        const uint32_t oid = __float_as_uint(G.lw(CP_SF_WS_ID(0, j)));
+        const float ol0 = G.ll(CP_SF_WS_LAM(0, j, 0)), ol1 = G.ll(CP_SF_WS_LAM(0, j, 1));
+        const float ol2 = G.ll(CP_SF_WS_LAM(0, j, 2)), ol3 = G.ll(CP_SF_WS_LAM(0, j, 3));
         const int base = used, fbase = fused;
         int m = 0, fm = 0;
         uint32_t nid = 0xFFFFFFFFu;
@@ -758,7 +901,7 @@ CP_DEV void substep(Sim& S, const cp_physics& P, float* pool, int& overflow, con
         for (int k = 0; k < 4; ++k) {
             if (k < C.m) {
                 if (base + m >= MAXP) {
-                    overflow += 1;  // dropped by the pool cap (oracle: same count)
+                    overflow += 1;  // dropped by the island pool cap (oracle: same count)
                 } else {
                     const int s = base + m;
                     V3 rb = sub(C.p[k], xb);
@@ -797,90 +940,149 @@ CP_DEV void substep(Sim& S, const cp_physics& P, float* pool, int& overflow, con
         used = base + m;
         fused = fbase + fm;
         const uint32_t pk = (uint32_t)m | ((uint32_t)base << 3) | ((uint32_t)fm << 8) | ((uint32_t)fbase << 11);
-        G.sx(4 * p + 0, C.n.x);
-        G.sx(4 * p + 1, C.n.y);
-        G.sx(4 * p + 2, C.n.z);
-        G.sx(4 * p + 3, __uint_as_float(pk));
-        G.ss(CP_SF_WS_ID(p), __uint_as_float(nid));
+        G.sx(4 * j + 0, C.n.x);
+        G.sx(4 * j + 1, C.n.y);
+        G.sx(4 * j + 2, C.n.z);
+        G.sx(4 * j + 3, __uint_as_float(pk));
+        G.sw(CP_SF_WS_ID(0, j), __uint_as_float(nid));
     }
 #pragma unroll
-    for (int p = 0; p < CP_NUM_PAIRS; ++p) {
-        T.n[p] = mk(G.lx(4 * p + 0), G.lx(4 * p + 1), G.lx(4 * p + 2));
-        T.pk[p] = __float_as_uint(G.lx(4 * p + 3));
+    for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
+        T.n[j] = mk(G.lx(4 * j + 0), G.lx(4 * j + 1), G.lx(4 * j + 2));
+        T.pk[j] = __float_as_uint(G.lx(4 * j + 3));
     }
     CP_STAMP(t1);
     CP_ACC(narrow, t0, t1);
-    // 3. unconstrained velocity update
+    // 3. unconstrained velocity update (both lanes, whole env)
     const float kl = P.lin_damping, ka = P.ang_damping;
 #pragma unroll
     for (int d = 0; d < CP_NUM_DYN; ++d) {
         const int g = d + 1;
         const float im = P.inv_mass[g];
+        const Axes ax = quat_axes(S.b[d].q[0], S.b[d].q[1], S.b[d].q[2], S.b[d].q[3]);
         V3 v = S.b[d].v, w = S.b[d].w;
         V3 F = (d == 0) ? S.f0 : ((d == 2) ? S.f2 : mk(0.0f, 0.0f, 0.0f));
         float vlen = sqrtf(dot(v, v));
         float dv = fmaf_(kl, vlen, kl);
         V3 acc = mk(fmaf_(-v.x, dv, fmaf_(F.x, im, P.gravity[0])), fmaf_(-v.y, dv, fmaf_(F.y, im, P.gravity[1])),
                     fmaf_(-v.z, dv, fmaf_(F.z, im, P.gravity[2])));
-        V3 wl = rot_t(T.ax[d], w);
+        V3 wl = rot_t(ax, w);
         V3 Iwl = mk(P.inertia[g][0] * wl.x, P.inertia[g][1] * wl.y, P.inertia[g][2] * wl.z);
         V3 gl = cross(wl, Iwl);
         V3 al = mk(-(P.inv_inertia[g][0] * gl.x), -(P.inv_inertia[g][1] * gl.y), -(P.inv_inertia[g][2] * gl.z));
-        V3 aw = rot(T.ax[d], al);
+        V3 aw = rot(ax, al);
         float wlen = sqrtf(dot(w, w));
         float dw = fmaf_(ka, wlen, ka);
         V3 accw = mk(fmaf_(-w.x, dw, aw.x), fmaf_(-w.y, dw, aw.y), fmaf_(-w.z, dw, aw.z));
         S.b[d].v = madd(v, acc, dt);
         S.b[d].w = madd(w, accw, dt);
     }
-    // 4a. warm start, in solver pair order (oracle SOLVE_ORDER = 0 2 1 3 4 9 5 6 7 8)
-    pair_warmstart<0>(S, T, P, pool); pair_warmstart<2>(S, T, P, pool);
-    pair_warmstart<1>(S, T, P, pool); pair_warmstart<3>(S, T, P, pool);
-    pair_warmstart<4>(S, T, P, pool); pair_warmstart<9>(S, T, P, pool);
-    pair_warmstart<5>(S, T, P, pool); pair_warmstart<6>(S, T, P, pool);
-    pair_warmstart<7>(S, T, P, pool); pair_warmstart<8>(S, T, P, pool);
+    S.f0 = mk(0.0f, 0.0f, 0.0f);  // 6. external forces are consumed by the step
+    S.f2 = mk(0.0f, 0.0f, 0.0f);
+    // 4. solve.  No cross-island contact: each lane solves its own island
+    //    (oracle: independent islands).  Otherwise both lanes run the merged solve.
+    //    (DPP reads the partner lane's register: evaluate it in converged code, never
+    //    under a short-circuit or branch where the partner may be inactive.)
+    const uint32_t own_cross = (pk_cnt(T.pk[3]) + pk_cnt(T.pk[4])) > 0 ? 1u : 0u;
+    const uint32_t any_cross = own_cross | partner_u(own_cross);
+    const bool merged = any_cross != 0u;
+    const int tot = used + (int)partner_u((uint32_t)used);
+    const bool second = L.isl != 0;
+    const float thr = P.residual_threshold;
+    // the island's two bodies (cart, pole or cart2, pole2) with their world inverse inertia
+    Isl I;
+    {
+        I.d1.x = selv(second, S.b[2].x, S.b[0].x);
+        I.d1.v = selv(second, S.b[2].v, S.b[0].v);
+        I.d1.w = selv(second, S.b[2].w, S.b[0].w);
+        I.d2.x = selv(second, S.b[3].x, S.b[1].x);
+        I.d2.v = selv(second, S.b[3].v, S.b[1].v);
+        I.d2.w = selv(second, S.b[3].w, S.b[1].w);
+        const float cq0 = second ? S.b[2].q[0] : S.b[0].q[0], cq1 = second ? S.b[2].q[1] : S.b[0].q[1];
+        const float cq2 = second ? S.b[2].q[2] : S.b[0].q[2], cq3 = second ? S.b[2].q[3] : S.b[0].q[3];
+        const float pq0 = second ? S.b[3].q[0] : S.b[1].q[0], pq1 = second ? S.b[3].q[1] : S.b[1].q[1];
+        const float pq2 = second ? S.b[3].q[2] : S.b[1].q[2], pq3 = second ? S.b[3].q[3] : S.b[1].q[3];
+        I.d1.M = world_inv_inertia(quat_axes(cq0, cq1, cq2, cq3), L.ii1[0], L.ii1[1], L.ii1[2]);
+        I.d2.M = world_inv_inertia(quat_axes(pq0, pq1, pq2, pq3), L.ii2[0], L.ii2[1], L.ii2[2]);
+        I.im1 = L.im1;
+        I.im2 = L.im2;
+    }
     CP_STAMP(t2);
     CP_ACC(vel, t1, t2);
-    // 4b. PGS sweeps; a lane stops after the sweep whose residual <= threshold
-    bool active = used > 0;
-    const float thr = P.residual_threshold;
+    // Island rows run per lane; the rows of the two islands touch disjoint bodies,
+    // so running them side by side equals the oracle's interleaved order.  Cross
+    // rows (an env with a cross-island contact: "merged") run on both lanes on the
+    // whole-env view after the island rows of the same kind, as in the oracle; a
+    // merged env stops on the joint residual (island 0 + island 1) + cross.
+    isl_warmstart<0>(I, T, pool);
+    isl_warmstart<1>(I, T, pool);
+    isl_warmstart<2>(I, T, pool);
+    if (__ballot(merged) != 0ull && merged) {
+        cross_view(S, T, I, second);
+        pair_warmstart<5>(S, T, second, P, pool0); pair_warmstart<6>(S, T, second, P, pool0);
+        pair_warmstart<7>(S, T, second, P, pool0); pair_warmstart<8>(S, T, second, P, pool0);
+        cross_back(I, S, second);
+    }
+    bool active = merged ? tot > 0 : used > 0;
     for (int it = 0; it < P.solver_iterations; ++it) {
         if (__ballot(active) == 0ull) break;
 #ifdef CP_STAMPS
         ST.sweeps += 1;
 #endif
+        float r = 0.0f, rc = 0.0f;
         if (active) {
-            // island 1 = pairs 0,1,4 ; island 2 = pairs 2,3,9 ; cross = 5..8 (oracle SOLVE_ORDER)
-            float r1 = 0.0f, r2 = 0.0f, rc = 0.0f;
-            pair_normal_rows<0>(S, T, P, pool, r1);
-            pair_normal_rows<2>(S, T, P, pool, r2);
-            pair_normal_rows<1>(S, T, P, pool, r1);
-            pair_normal_rows<3>(S, T, P, pool, r2);
-            pair_normal_rows<4>(S, T, P, pool, r1);
-            pair_normal_rows<9>(S, T, P, pool, r2);
-            pair_normal_rows<5>(S, T, P, pool, rc);
-            pair_normal_rows<6>(S, T, P, pool, rc);
-            pair_normal_rows<7>(S, T, P, pool, rc);
-            pair_normal_rows<8>(S, T, P, pool, rc);
-            pair_friction_rows<0>(S, T, P, pool, r1);
-            pair_friction_rows<2>(S, T, P, pool, r2);
-            pair_friction_rows<1>(S, T, P, pool, r1);
-            pair_friction_rows<3>(S, T, P, pool, r2);
-            pair_friction_rows<4>(S, T, P, pool, r1);
-            pair_friction_rows<9>(S, T, P, pool, r2);
-            pair_friction_rows<5>(S, T, P, pool, rc);
-            pair_friction_rows<6>(S, T, P, pool, rc);
-            pair_friction_rows<7>(S, T, P, pool, rc);
-            pair_friction_rows<8>(S, T, P, pool, rc);
-            const float resid = (r1 + r2) + rc;
-            if (resid <= thr) active = false;
+            isl_normal_rows<0>(I, T, pool, r);
+            isl_normal_rows<1>(I, T, pool, r);
+            isl_normal_rows<2>(I, T, pool, r);
         }
+        const bool cross = active && merged;  // same on both lanes of an env
+        if (__ballot(cross) != 0ull && cross) {
+            cross_view(S, T, I, second);
+            pair_normal_rows<5>(S, T, second, P, pool0, rc);
+            pair_normal_rows<6>(S, T, second, P, pool0, rc);
+            pair_normal_rows<7>(S, T, second, P, pool0, rc);
+            pair_normal_rows<8>(S, T, second, P, pool0, rc);
+            cross_back(I, S, second);
+        }
+        if (active) {
+            isl_friction_rows<0>(I, T, L.mu0, pool, r);
+            isl_friction_rows<1>(I, T, L.mu1, pool, r);
+            isl_friction_rows<2>(I, T, L.mu2, pool, r);
+        }
+        if (__ballot(cross) != 0ull && cross) {
+            cross_view(S, T, I, second);
+            pair_friction_rows<5>(S, T, second, P, pool0, rc);
+            pair_friction_rows<6>(S, T, second, P, pool0, rc);
+            pair_friction_rows<7>(S, T, second, P, pool0, rc);
+            pair_friction_rows<8>(S, T, second, P, pool0, rc);
+            cross_back(I, S, second);
+        }
+        const float rp = partner(r);  // converged: every lane that entered the loop is here
+        const float joint = second ? (rp + r) + rc : (r + rp) + rc;
+        if (active && (merged ? joint : r) <= thr) active = false;
+    }
+    // whole-env velocities from the two lanes' islands (converged point: both lanes active)
+    {
+        const V3 v1 = partner(I.d1.v), w1 = partner(I.d1.w), v2 = partner(I.d2.v), w2 = partner(I.d2.w);
+        S.b[0].v = selv(second, v1, I.d1.v);
+        S.b[0].w = selv(second, w1, I.d1.w);
+        S.b[1].v = selv(second, v2, I.d2.v);
+        S.b[1].w = selv(second, w2, I.d2.w);
+        S.b[2].v = selv(second, I.d1.v, v1);
+        S.b[2].w = selv(second, I.d1.w, w1);
+        S.b[3].v = selv(second, I.d2.v, v2);
+        S.b[3].w = selv(second, I.d2.w, w2);
     }
     CP_STAMP(t3);
     CP_ACC(solve, t2, t3);
-    // 4c. refresh the warm-start cache
-    CP_FOR_PAIRS(pair_cache, T, pool, G);
-    // 5. integrate positions and orientations
+    // 4c. refresh the warm-start cache of the lane's island
+#pragma unroll
+    for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
+        const int cnt = pk_cnt(T.pk[j]), base = pk_base(T.pk[j]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) G.sl(CP_SF_WS_LAM(0, j, k), (k < cnt) ? pool_n(pool, F_LAM, base + k) : 0.0f);
+    }
+    // 5. integrate positions and orientations (both lanes, whole env)
     const float hdt = 0.5f * dt;
     const float c3 = ((dt * dt) * dt) * (float)0.020833333333;
     const float maxang = P.max_angular_step;
@@ -908,9 +1110,6 @@ CP_DEV void substep(Sim& S, const cp_physics& P, float* pool, int& overflow, con
         S.b[d].q[2] = rz * inv;
         S.b[d].q[3] = rw * inv;
     }
-    // 6. external forces are consumed by the step
-    S.f0 = mk(0.0f, 0.0f, 0.0f);
-    S.f2 = mk(0.0f, 0.0f, 0.0f);
     CP_STAMP(t4);
     CP_ACC(integ, t3, t4);
 #ifdef CP_STAMPS

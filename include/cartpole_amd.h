@@ -46,6 +46,12 @@ extern "C" {
 #define CP_NUM_BODIES  5
 #define CP_NUM_DYN     4          /* dynamic bodies: cart, pole, cart2, pole2 */
 #define CP_NUM_PAIRS   10         /* all body pairs (a<b) */
+/* Islands: {cart, pole} and {cart2, pole2} (the ground is static and joins nothing).
+ * Each island owns 5 local pairs: (ground,cart_p) (ground,pole_p) (cart_p,pole_p) and
+ * two cross pairs -- island 0: (cart,cart2) (cart,pole2); island 1: (pole,cart2)
+ * (pole,pole2).  The kernel runs one island per lane (2 lanes per env). */
+#define CP_NUM_ISLANDS  2
+#define CP_ISLAND_PAIRS 5
 
 /* Per-body dynamic state: pos(3) quat xyzw(4) linvel(3) angvel(3). */
 #define CP_BODY_FIELDS 13
@@ -57,16 +63,16 @@ extern "C" {
 #define CP_SF_STEPS   (CP_NUM_DYN * CP_BODY_FIELDS + 6)
 #define CP_SF_EPISODE (CP_SF_STEPS + 1)
 #define CP_SF_DONE    (CP_SF_STEPS + 2)
-/* warm-start cache (persistent contact impulses, DESIGN.md §Physics model):
- * per pair one packed word of 4 feature ids (bytes, 0xFF = empty slot), and
- * the 4 accumulated normal impulses of the last substep */
-#define CP_SF_WS_ID(pair)      (CP_SF_STEPS + 3 + (pair))
-#define CP_SF_WS_LAM(pair, k)  (CP_SF_STEPS + 3 + CP_NUM_PAIRS + (pair) * 4 + (k))
+/* warm-start cache (persistent contact impulses, DESIGN.md §Physics model): per
+ * island and local pair one packed word of 4 feature ids (bytes, 0xFF = empty
+ * slot), and the 4 accumulated normal impulses of the last substep */
+#define CP_SF_WS_ID(isl, j)      (CP_SF_STEPS + 3 + (isl) * CP_ISLAND_PAIRS + (j))
+#define CP_SF_WS_LAM(isl, j, k)  (CP_SF_STEPS + 3 + CP_NUM_PAIRS + ((isl) * CP_ISLAND_PAIRS + (j)) * 4 + (k))
 #define CP_STATE_FIELDS (CP_SF_STEPS + 3 + CP_NUM_PAIRS * 5)
 
-/* Contact pools per env (LDS-resident in the kernel; same caps in the oracle). */
-#define CP_MAX_POINTS   20        /* normal-contact rows per substep */
-#define CP_MAX_FRICTION 10        /* contact points that carry 2 friction rows */
+/* Contact pools per island (LDS-resident in the kernel; same caps in the oracle). */
+#define CP_ISLAND_POINTS   10     /* normal-contact rows per island per substep */
+#define CP_ISLAND_FRICTION 5      /* contact points that carry 2 friction rows */
 
 /* Discrete action table (the fork dropped upstream's mapping; the comment at
  * bullet_cartpole.py:84,89 names the order "no push, left, right, up, down").

@@ -249,6 +249,8 @@ static const int PAIR_B[CP_NUM_PAIRS] = {1, 2, 3, 4, 2, 3, 4, 3, 4, 4};
  * Rows of different islands share no dynamic body, so the kernel may interleave them. */
 static const int SOLVE_ORDER[CP_NUM_PAIRS] = {0, 2, 1, 3, 4, 9, 5, 6, 7, 8};
 static const int ISLAND[CP_NUM_PAIRS] = {0, 0, 1, 1, 0, 2, 2, 2, 2, 1};
+/* island p's local pairs j = 0..4 -> global pair (own 3, then the 2 cross pairs it owns) */
+static const int ISLAND_PAIR[CP_NUM_ISLANDS][CP_ISLAND_PAIRS] = {{0, 1, 4, 5, 6}, {2, 3, 9, 7, 8}};
 
 /* --------------------------------------------------------------- simulation */
 typedef struct {
@@ -258,8 +260,8 @@ typedef struct {
     v3 f[CP_NUM_DYN];          /* pending world force */
     v3 ax[CP_NUM_DYN][3];
     real M[CP_NUM_DYN][6];
-    uint32_t ws_id[CP_NUM_PAIRS];    /* warm-start cache (4 packed feature ids per pair) */
-    real ws_lam[CP_NUM_PAIRS][4];
+    uint32_t ws_id[CP_NUM_ISLANDS][CP_ISLAND_PAIRS];   /* warm-start cache (4 packed feature ids) */
+    real ws_lam[CP_NUM_ISLANDS][CP_ISLAND_PAIRS][4];
 } sim_t;
 
 typedef struct { v3 n; int cnt, base, fcnt, fbase; real mu; } manifold_t;
@@ -560,7 +562,11 @@ static real solve_row(sim_t* S, const cp_physics* P, int a, int b, v3 rb, v3 t,
         S->v[da_] = madd(S->v[da_], neg(t), sa);
         S->w[da_] = madd(S->w[da_], neg(ia), dl);
     }
+#ifdef ORC_RESID_MAX
+    { real vr = dl / inv_eff; return vr * vr; }
+#else
     return FABS(e * dl);
+#endif
 }
 
 /* velocity change of an impulse lam along t at lever arm rb (warm start) */
@@ -580,65 +586,131 @@ static void apply_impulse(sim_t* S, const cp_physics* P, int a, int b, v3 rb, v3
     }
 }
 
-/* one p.stepSimulation() of the scene (DESIGN.md §Physics model, steps 1-6) */
-static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* iters_out, int32_t* npts_out) {
+/* per-island contact storage (one kernel lane's LDS pool) */
+typedef struct {
+    manifold_t man[CP_ISLAND_PAIRS];
+    point_t pt[CP_ISLAND_POINTS];
+    fpoint_t fp[CP_ISLAND_FRICTION];
+    int used, fused;
+} island_t;
+
+/* row sweep helpers: all normal rows, then all friction rows, of local pairs [j0, j1) */
+static void sweep_normal(sim_t* S, const cp_physics* P, island_t* I, int isl, int j, real* r) {
+    int g = ISLAND_PAIR[isl][j];
+    int a = PAIR_A[g], b = PAIR_B[g];
+    manifold_t* m = &I->man[j];
+    for (int k = 0; k < m->cnt; ++k) {
+        point_t* q = &I->pt[m->base + k];
+        { real rr_ = solve_row(S, P, a, b, q->rb, m->n, q->inv_eff, q->target, &q->lam, 0, RC(0));
+#ifdef ORC_RESID_MAX
+        *r = rr_ > *r ? rr_ : *r;
+#else
+        *r = *r + rr_;
+#endif
+        }
+    }
+}
+static void sweep_friction(sim_t* S, const cp_physics* P, island_t* I, int isl, int j, real* r) {
+    manifold_t* m = &I->man[j];
+    if (m->fcnt == 0) return;
+    int g = ISLAND_PAIR[isl][j];
+    int a = PAIR_A[g], b = PAIR_B[g];
+    v3 t1, t2;
+    plane_space(m->n, &t1, &t2);
+    for (int k = 0; k < m->fcnt; ++k) {
+        point_t* q = &I->pt[m->base + k];
+        fpoint_t* f = &I->fp[m->fbase + k];
+        real bound = m->mu * q->lam;
+        { real rr_ = solve_row(S, P, a, b, q->rb, t1, f->inv_eff1, RC(0), &f->lam1, 1, bound);
+#ifdef ORC_RESID_MAX
+        *r = rr_ > *r ? rr_ : *r;
+#else
+        *r = *r + rr_;
+#endif
+        }
+        { real rr_ = solve_row(S, P, a, b, q->rb, t2, f->inv_eff2, RC(0), &f->lam2, 1, bound);
+#ifdef ORC_RESID_MAX
+        *r = rr_ > *r ? rr_ : *r;
+#else
+        *r = *r + rr_;
+#endif
+        }
+    }
+}
+static void warm_pair(sim_t* S, const cp_physics* P, island_t* I, int isl, int j) {
+    int g = ISLAND_PAIR[isl][j];
+    int a = PAIR_A[g], b = PAIR_B[g];
+    manifold_t* m = &I->man[j];
+    for (int k = 0; k < m->cnt; ++k) {
+        point_t* q = &I->pt[m->base + k];
+        apply_impulse(S, P, a, b, q->rb, m->n, q->lam);
+    }
+}
+
+/* one p.stepSimulation() of the scene (DESIGN.md §Physics model, steps 1-8) */
+static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* iters_out, int32_t* npts_out,
+                    int32_t* isl_iters) {
     const real dt = (real)P->dt, inv_dt = (real)P->inv_dt;
     /* 1. orientation matrices, world inverse inertia */
     for (int d = 0; d < CP_NUM_DYN; ++d) {
         quat_axes(S->q[d], S->ax[d]);
         world_inv_inertia(S->ax[d], P->inv_inertia[d + 1], S->M[d]);
     }
-    /* 2. narrowphase + row setup at the start-of-step poses */
-    manifold_t man[CP_NUM_PAIRS];
-    point_t pt[CP_MAX_POINTS];
-    fpoint_t fp[CP_MAX_FRICTION];
-    int used = 0, fused = 0;
-    for (int p = 0; p < CP_NUM_PAIRS; ++p) {
-        int a = PAIR_A[p], b = PAIR_B[p];
-        box_t A, B;
-        get_box(S, P, a, &A);
-        get_box(S, P, b, &B);
-        v3 n, pts[4];
-        real dist[4];
-        int ids[4];
-        int cnt = box_box(&A, &B, (real)P->contact_margin, (real)P->edge_bias, &n, pts, dist, ids);
-        int m = cnt < CP_MAX_POINTS - used ? cnt : CP_MAX_POINTS - used;
-        *overflow += cnt - m;
-        man[p].n = n;
-        man[p].cnt = m;
-        man[p].base = used;
-        man[p].mu = (real)P->friction[a] * (real)P->friction[b];
-        man[p].fcnt = 0;
-        man[p].fbase = fused;
-        for (int k = 0; k < m; ++k) {
-            point_t* q = &pt[used + k];
-            q->rb = sub(pts[k], S->x[b - 1]);
-            real K = row_k(S, P, a, b, q->rb, n);
-            q->inv_eff = RC(1) / K;
-            q->target = dist[k] > RC(0) ? -(dist[k] * inv_dt) : -(((real)P->erp * dist[k]) * inv_dt);
-            q->id = ids[k];
-            /* warm start: impulse of the same feature in the last substep */
-            real l0 = RC(0);
-            for (int j = 0; j < 4; ++j) {
-                if ((int)((S->ws_id[p] >> (8 * j)) & 0xFFu) == ids[k]) { l0 = S->ws_lam[p][j]; break; }
+    /* 2. narrowphase + row setup at the start-of-step poses, per island: its 3 own
+     *    pairs then its 2 cross pairs, into its own capped pool */
+    island_t isl[CP_NUM_ISLANDS];
+    for (int p = 0; p < CP_NUM_ISLANDS; ++p) {
+        island_t* I = &isl[p];
+        I->used = I->fused = 0;
+        for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
+            int g = ISLAND_PAIR[p][j];
+            int a = PAIR_A[g], b = PAIR_B[g];
+            box_t A, B;
+            get_box(S, P, a, &A);
+            get_box(S, P, b, &B);
+            v3 n, pts[4];
+            real dist[4];
+            int ids[4];
+            int cnt = box_box(&A, &B, (real)P->contact_margin, (real)P->edge_bias, &n, pts, dist, ids);
+            int m = cnt < CP_ISLAND_POINTS - I->used ? cnt : CP_ISLAND_POINTS - I->used;
+            *overflow += cnt - m;
+            manifold_t* man = &I->man[j];
+            man->n = n;
+            man->cnt = m;
+            man->base = I->used;
+            man->mu = (real)P->friction[a] * (real)P->friction[b];
+            man->fcnt = 0;
+            man->fbase = I->fused;
+            for (int k = 0; k < m; ++k) {
+                point_t* q = &I->pt[I->used + k];
+                q->rb = sub(pts[k], S->x[b - 1]);
+                real K = row_k(S, P, a, b, q->rb, n);
+                q->inv_eff = RC(1) / K;
+                q->target = dist[k] > RC(0) ? -(dist[k] * inv_dt) : -(((real)P->erp * dist[k]) * inv_dt);
+                q->id = ids[k];
+                /* warm start: impulse of the same feature in the last substep */
+                real l0 = RC(0);
+                for (int q4 = 0; q4 < 4; ++q4) {
+                    if ((int)((S->ws_id[p][j] >> (8 * q4)) & 0xFFu) == ids[k]) { l0 = S->ws_lam[p][j][q4]; break; }
+                }
+                q->lam = (real)P->warmstart * l0;
             }
-            q->lam = (real)P->warmstart * l0;
-        }
-        if (man[p].mu > RC(0) && m > 0) {
-            int fm = m < CP_MAX_FRICTION - fused ? m : CP_MAX_FRICTION - fused;
-            *overflow += m - fm;
-            man[p].fcnt = fm;
-            v3 t1, t2;
-            plane_space(n, &t1, &t2);
-            for (int k = 0; k < fm; ++k) {
-                fpoint_t* f = &fp[fused + k];
-                f->inv_eff1 = RC(1) / row_k(S, P, a, b, pt[used + k].rb, t1);
-                f->inv_eff2 = RC(1) / row_k(S, P, a, b, pt[used + k].rb, t2);
-                f->lam1 = f->lam2 = RC(0);
+            if (man->mu > RC(0) && m > 0) {
+                int fm = m < CP_ISLAND_FRICTION - I->fused ? m : CP_ISLAND_FRICTION - I->fused;
+                *overflow += m - fm;
+                man->fcnt = fm;
+                v3 t1, t2;
+                plane_space(n, &t1, &t2);
+                for (int k = 0; k < fm; ++k) {
+                    fpoint_t* f = &I->fp[I->fused + k];
+                    f->inv_eff1 = RC(1) / row_k(S, P, a, b, I->pt[I->used + k].rb, t1);
+                    f->inv_eff2 = RC(1) / row_k(S, P, a, b, I->pt[I->used + k].rb, t2);
+                    f->lam1 = f->lam2 = RC(0);
+                }
+                I->fused += fm;
             }
-            fused += fm;
+            I->used += m;
         }
-        used += m;
     }
     /* 3. unconstrained velocity update: gravity + pending force + Bullet multibody
      *    damping (-m v (k + k|v|), -I w (k + k|w|)) + gyroscopic term */
@@ -664,70 +736,76 @@ static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* i
         S->v[d] = madd(v, acc, dt);
         S->w[d] = madd(w, accw, dt);
     }
-    /* 4a. warm start: apply the cached normal impulses (solver row order) */
-    for (int j = 0; j < CP_NUM_PAIRS; ++j) {
-        int p = SOLVE_ORDER[j];
-        int a = PAIR_A[p], b = PAIR_B[p];
-        for (int k = 0; k < man[p].cnt; ++k) {
-            point_t* q = &pt[man[p].base + k];
-            apply_impulse(S, P, a, b, q->rb, man[p].n, q->lam);
-        }
-    }
-    /* 4b. projected Gauss-Seidel: normal rows then friction rows per sweep, pairs in
-     * SOLVE_ORDER (island 1 and island 2 pairs alternate, cross pairs last); the
-     * residual is summed per island, then (island1 + island2) + cross */
-    int it = 0;
+    /* 4. warm start + projected Gauss-Seidel.  Islands without a cross-island contact
+     *    are solved independently (own sweeps, own residual, like Bullet's island
+     *    solving); any cross contact merges everything into one solve in the global
+     *    order 0 2 1 3 4 9 5 6 7 8 with residual (island0 + island1) + cross. */
     const int iters = P->solver_iterations;
     const real thr = (real)P->residual_threshold;
-    if (used > 0) {
-        for (it = 0; it < iters;) {
-            real rs[3] = {RC(0), RC(0), RC(0)};
-            for (int j = 0; j < CP_NUM_PAIRS; ++j) {
-                int p = SOLVE_ORDER[j];
-                int a = PAIR_A[p], b = PAIR_B[p];
-                for (int k = 0; k < man[p].cnt; ++k) {
-                    point_t* q = &pt[man[p].base + k];
-                    real rr = solve_row(S, P, a, b, q->rb, man[p].n, q->inv_eff, q->target, &q->lam, 0, RC(0));
-                    rs[ISLAND[p]] = rs[ISLAND[p]] + rr;
+    int merged = 0;
+    for (int p = 0; p < CP_NUM_ISLANDS; ++p) merged |= (isl[p].man[3].cnt + isl[p].man[4].cnt) > 0;
+    int it_max = 0;
+    if (!merged) {
+        for (int p = 0; p < CP_NUM_ISLANDS; ++p) {
+            island_t* I = &isl[p];
+            for (int j = 0; j < 3; ++j) warm_pair(S, P, I, p, j);
+            int it = 0;
+            if (I->used > 0) {
+                for (it = 0; it < iters;) {
+                    real r = RC(0);
+                    for (int j = 0; j < 3; ++j) sweep_normal(S, P, I, p, j, &r);
+                    for (int j = 0; j < 3; ++j) sweep_friction(S, P, I, p, j, &r);
+                    ++it;
+#ifdef ORC_DEBUG
+                    if (getenv("ORC_DEBUG")) fprintf(stderr, "isl %d it %d resid %g\n", p, it, (double)r);
+#endif
+                    if (r <= thr) break;
                 }
             }
-            for (int j = 0; j < CP_NUM_PAIRS; ++j) {
-                int p = SOLVE_ORDER[j];
-                if (man[p].fcnt == 0) continue;
-                int a = PAIR_A[p], b = PAIR_B[p];
-                v3 t1, t2;
-                plane_space(man[p].n, &t1, &t2);
-                for (int k = 0; k < man[p].fcnt; ++k) {
-                    point_t* q = &pt[man[p].base + k];
-                    fpoint_t* f = &fp[man[p].fbase + k];
-                    real bound = man[p].mu * q->lam;
-                    real r1 = solve_row(S, P, a, b, q->rb, t1, f->inv_eff1, RC(0), &f->lam1, 1, bound);
-                    rs[ISLAND[p]] = rs[ISLAND[p]] + r1;
-                    real r2 = solve_row(S, P, a, b, q->rb, t2, f->inv_eff2, RC(0), &f->lam2, 1, bound);
-                    rs[ISLAND[p]] = rs[ISLAND[p]] + r2;
-                }
+            if (it > it_max) it_max = it;
+            if (isl_iters && it > isl_iters[p]) isl_iters[p] = it;
+        }
+    } else {
+        /* global order: (0,0) (1,0) (0,1) (1,1) (0,2) (1,2) then cross (0,3) (0,4) (1,3) (1,4) */
+        static const int ORD_I[10] = {0, 1, 0, 1, 0, 1, 0, 0, 1, 1};
+        static const int ORD_J[10] = {0, 0, 1, 1, 2, 2, 3, 4, 3, 4};
+        for (int o = 0; o < 10; ++o) warm_pair(S, P, &isl[ORD_I[o]], ORD_I[o], ORD_J[o]);
+        int it = 0;
+        for (it = 0; it < iters;) {
+            real rs[3] = {RC(0), RC(0), RC(0)};
+            for (int o = 0; o < 10; ++o) {
+                int p = ORD_I[o], j = ORD_J[o];
+                sweep_normal(S, P, &isl[p], p, j, &rs[j < 3 ? p : 2]);
+            }
+            for (int o = 0; o < 10; ++o) {
+                int p = ORD_I[o], j = ORD_J[o];
+                sweep_friction(S, P, &isl[p], p, j, &rs[j < 3 ? p : 2]);
             }
             real resid = (rs[0] + rs[1]) + rs[2];
             ++it;
-#ifdef ORC_DEBUG
-            if (getenv("ORC_DEBUG")) fprintf(stderr, "it %d resid %g\n", it, (double)resid);
-#endif
             if (resid <= thr) break;
         }
+        it_max = it;
+        if (isl_iters)
+            for (int p = 0; p < CP_NUM_ISLANDS; ++p)
+                if (it > isl_iters[p]) isl_iters[p] = it;
     }
     /* 4c. refresh the warm-start cache */
-    for (int p = 0; p < CP_NUM_PAIRS; ++p) {
-        uint32_t idw = 0xFFFFFFFFu;
-        for (int k = 0; k < 4; ++k) {
-            if (k < man[p].cnt) {
-                point_t* q = &pt[man[p].base + k];
-                idw = (idw & ~(0xFFu << (8 * k))) | ((uint32_t)q->id << (8 * k));
-                S->ws_lam[p][k] = q->lam;
-            } else {
-                S->ws_lam[p][k] = RC(0);
+    for (int p = 0; p < CP_NUM_ISLANDS; ++p) {
+        for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
+            manifold_t* m = &isl[p].man[j];
+            uint32_t idw = 0xFFFFFFFFu;
+            for (int k = 0; k < 4; ++k) {
+                if (k < m->cnt) {
+                    point_t* q = &isl[p].pt[m->base + k];
+                    idw = (idw & ~(0xFFu << (8 * k))) | ((uint32_t)q->id << (8 * k));
+                    S->ws_lam[p][j][k] = q->lam;
+                } else {
+                    S->ws_lam[p][j][k] = RC(0);
+                }
             }
+            S->ws_id[p][j] = idw;
         }
-        S->ws_id[p] = idw;
     }
     /* 5. integrate positions (semi-implicit) and orientation (exponential map) */
     const real hdt = RC(0.5) * dt;
@@ -756,8 +834,8 @@ static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* i
     }
     /* 6. external forces are consumed by the step (pybullet clears them) */
     for (int d = 0; d < CP_NUM_DYN; ++d) S->f[d] = mk(RC(0), RC(0), RC(0));
-    if (iters_out) *iters_out = it;
-    if (npts_out) *npts_out = used;
+    if (iters_out) *iters_out = it_max;
+    if (npts_out) *npts_out = isl[0].used + isl[1].used;
 }
 
 /* LINK_FRAME force at the link origin (= COM): world force = R(q) f, no torque
@@ -777,10 +855,11 @@ static void world_load(const orc_world* w, sim_t* S) {
         S->w[d] = mk((real)w->omega[d][0], (real)w->omega[d][1], (real)w->omega[d][2]);
         S->f[d] = mk((real)w->pending[d][0], (real)w->pending[d][1], (real)w->pending[d][2]);
     }
-    for (int p = 0; p < CP_NUM_PAIRS; ++p) {
-        S->ws_id[p] = w->ws_id[p];
-        for (int k = 0; k < 4; ++k) S->ws_lam[p][k] = (real)w->ws_lam[p][k];
-    }
+    for (int p = 0; p < CP_NUM_ISLANDS; ++p)
+        for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
+            S->ws_id[p][j] = w->ws_id[p * CP_ISLAND_PAIRS + j];
+            for (int k = 0; k < 4; ++k) S->ws_lam[p][j][k] = (real)w->ws_lam[p * CP_ISLAND_PAIRS + j][k];
+        }
 }
 static void world_store(orc_world* w, const sim_t* S) {
     for (int d = 0; d < CP_NUM_DYN; ++d) {
@@ -790,10 +869,11 @@ static void world_store(orc_world* w, const sim_t* S) {
         w->omega[d][0] = S->w[d].x; w->omega[d][1] = S->w[d].y; w->omega[d][2] = S->w[d].z;
         w->pending[d][0] = S->f[d].x; w->pending[d][1] = S->f[d].y; w->pending[d][2] = S->f[d].z;
     }
-    for (int p = 0; p < CP_NUM_PAIRS; ++p) {
-        w->ws_id[p] = S->ws_id[p];
-        for (int k = 0; k < 4; ++k) w->ws_lam[p][k] = S->ws_lam[p][k];
-    }
+    for (int p = 0; p < CP_NUM_ISLANDS; ++p)
+        for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
+            w->ws_id[p * CP_ISLAND_PAIRS + j] = S->ws_id[p][j];
+            for (int k = 0; k < 4; ++k) w->ws_lam[p * CP_ISLAND_PAIRS + j][k] = S->ws_lam[p][j][k];
+        }
 }
 
 void orc_world_spawn(orc_world* w, const cp_config* cfg) {
@@ -813,7 +893,7 @@ void orc_world_reset_pose(orc_world* w, int body, const double p[3], const doubl
 void orc_world_step(orc_world* w, const cp_config* cfg) {
     sim_t S;
     world_load(w, &S);
-    substep(&S, &cfg->phys, &w->overflow, &w->last_iterations, &w->last_points);
+    substep(&S, &cfg->phys, &w->overflow, &w->last_iterations, &w->last_points, NULL);
     world_store(w, &S);
 }
 void orc_world_apply_force_link(orc_world* w, int body, double fx, double fy, double fz) {
@@ -854,10 +934,11 @@ static void env_load(const orc_envs* e, int i, sim_t* S) {
     }
     for (int c = 0; c < 2; ++c)
         S->f[2 * c] = mk(SF(e, CP_SF_PENDING(c, 0), i), SF(e, CP_SF_PENDING(c, 1), i), SF(e, CP_SF_PENDING(c, 2), i));
-    for (int p = 0; p < CP_NUM_PAIRS; ++p) {
-        memcpy(&S->ws_id[p], &SF(e, CP_SF_WS_ID(p), i), 4);
-        for (int k = 0; k < 4; ++k) S->ws_lam[p][k] = SF(e, CP_SF_WS_LAM(p, k), i);
-    }
+    for (int p = 0; p < CP_NUM_ISLANDS; ++p)
+        for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
+            memcpy(&S->ws_id[p][j], &SF(e, CP_SF_WS_ID(p, j), i), 4);
+            for (int k = 0; k < 4; ++k) S->ws_lam[p][j][k] = SF(e, CP_SF_WS_LAM(p, j, k), i);
+        }
 }
 static void env_store(orc_envs* e, int i, const sim_t* S) {
     for (int d = 0; d < CP_NUM_DYN; ++d) {
@@ -877,10 +958,11 @@ static void env_store(orc_envs* e, int i, const sim_t* S) {
         SF(e, CP_SF_PENDING(c, 1), i) = (float)S->f[2 * c].y;
         SF(e, CP_SF_PENDING(c, 2), i) = (float)S->f[2 * c].z;
     }
-    for (int p = 0; p < CP_NUM_PAIRS; ++p) {
-        memcpy(&SF(e, CP_SF_WS_ID(p), i), &S->ws_id[p], 4);
-        for (int k = 0; k < 4; ++k) SF(e, CP_SF_WS_LAM(p, k), i) = (float)S->ws_lam[p][k];
-    }
+    for (int p = 0; p < CP_NUM_ISLANDS; ++p)
+        for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
+            memcpy(&SF(e, CP_SF_WS_ID(p, j), i), &S->ws_id[p][j], 4);
+            for (int k = 0; k < 4; ++k) SF(e, CP_SF_WS_LAM(p, j, k), i) = (float)S->ws_lam[p][j][k];
+        }
 }
 static int32_t get_i(const orc_envs* e, int f, int i) {
     int32_t v;
@@ -912,12 +994,14 @@ int orc_envs_create(const cp_config* cfg, orc_envs** out) {
     e->last_ret = (float*)calloc(B, sizeof(float));
     e->last_len = (int32_t*)calloc(B, sizeof(int32_t));
     e->overflow = (int32_t*)calloc(B, sizeof(int32_t));
+    e->sweeps = (int32_t*)calloc((size_t)B * 2, sizeof(int32_t));
     for (int i = 0; i < e->B; ++i) {
         for (int d = 0; d < CP_NUM_DYN; ++d) {
             for (int k = 0; k < 3; ++k) SF(e, CP_SF_BODY(d, k), i) = cfg->phys.spawn_pos[d + 1][k];
             SF(e, CP_SF_BODY(d, 6), i) = 1.0f;
         }
-        for (int p = 0; p < CP_NUM_PAIRS; ++p) set_i(e, CP_SF_WS_ID(p), i, -1);
+        for (int p = 0; p < CP_NUM_ISLANDS; ++p)
+            for (int j = 0; j < CP_ISLAND_PAIRS; ++j) set_i(e, CP_SF_WS_ID(p, j), i, -1);
         /* done = 1 until the first reset: step before reset is an error in the
          * reference (AttributeError); the batched API reports done. */
         set_i(e, CP_SF_DONE, i, 1);
@@ -928,7 +1012,7 @@ int orc_envs_create(const cp_config* cfg, orc_envs** out) {
 void orc_envs_destroy(orc_envs* e) {
     if (!e) return;
     free(e->state); free(e->term_obs); free(e->bump_forces); free(e->ret_acc);
-    free(e->last_ret); free(e->last_len); free(e->overflow);
+    free(e->last_ret); free(e->last_len); free(e->overflow); free(e->sweeps);
     free(e);
 }
 void orc_envs_set_bump_forces(orc_envs* e, const float* f) {
@@ -977,14 +1061,15 @@ static void reset_one(orc_envs* e, int i, float* obs_row /* R*14 */) {
         S.q[d][3] = RC(1);
         S.v[d] = S.w[d] = mk(RC(0), RC(0), RC(0));
     }
-    for (int p = 0; p < CP_NUM_PAIRS; ++p) {
-        S.ws_id[p] = 0xFFFFFFFFu;
-        for (int k = 0; k < 4; ++k) S.ws_lam[p][k] = RC(0);
-    }
+    for (int p = 0; p < CP_NUM_ISLANDS; ++p)
+        for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
+            S.ws_id[p][j] = 0xFFFFFFFFu;
+            for (int k = 0; k < 4; ++k) S.ws_lam[p][j][k] = RC(0);
+        }
     int32_t ov = 0;
-    for (int s = 0; s < cfg->settle_steps; ++s) substep(&S, &cfg->phys, &ov, NULL, NULL);
+    for (int s = 0; s < cfg->settle_steps; ++s) substep(&S, &cfg->phys, &ov, NULL, NULL, NULL);
     for (int k = 0; k < cfg->initial_force_steps; ++k) {
-        substep(&S, &cfg->phys, &ov, NULL, NULL);
+        substep(&S, &cfg->phys, &ov, NULL, NULL, NULL);
         for (int c = 0; c < 2; ++c) {
             real fx, fy;
             bump_force(e, i, episode, k, c, &fx, &fy);
@@ -1063,9 +1148,11 @@ static void step_one(orc_envs* e, int i, const void* actions, int kind, float* o
     sim_t S;
     env_load(e, i, &S);
     int32_t ov = 0;
+    int32_t* sw = e->sweeps + (size_t)i * 2;
+    sw[0] = sw[1] = 0;
     for (int r = 0; r < R; ++r) {
         for (int s = 0; s < Sn; ++s) {
-            substep(&S, &cfg->phys, &ov, NULL, NULL);
+            substep(&S, &cfg->phys, &ov, NULL, NULL, sw);
             apply_force_link(&S, 0, a[0][0] * F, a[0][1] * F, RC(0));
             apply_force_link(&S, 2, a[1][0] * F, a[1][1] * F, RC(0));
             if (readback) {
@@ -1124,6 +1211,7 @@ int orc_envs_step_omp(orc_envs* e, const void* actions, int kind, float* obs_out
 #endif
     return used;
 }
+void orc_envs_sweeps(const orc_envs* e, int32_t* out) { memcpy(out, e->sweeps, (size_t)e->B * 2 * sizeof(int32_t)); }
 void orc_envs_episode_returns(const orc_envs* e, float* ret, int32_t* len) {
     if (ret) memcpy(ret, e->last_ret, (size_t)e->B * sizeof(float));
     if (len) memcpy(len, e->last_len, (size_t)e->B * sizeof(int32_t));

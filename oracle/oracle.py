@@ -73,6 +73,7 @@ def load(precision="f32"):
         "orc_envs_step": (None, [VP, VP, C.c_int, VP, VP, VP, VP, VP, C.c_int]),
         "orc_envs_step_omp": (C.c_int, [VP, VP, C.c_int, VP, VP, VP, C.c_int]),
         "orc_envs_episode_returns": (None, [VP, VP, VP]),
+        "orc_envs_sweeps": (None, [VP, VP]),
         "orc_philox4x32_10": (None, [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]),
         "orc_sincos_turns": (None, [C.c_float, P(C.c_float), P(C.c_float)]),
         "orc_sizeof_real": (C.c_int, []),
@@ -210,6 +211,12 @@ class Envs:
         n = np.zeros(self.B, np.int32)
         self.lib.orc_envs_episode_returns(self.h, _ptr(r), _ptr(n))
         return r, n
+
+    def sweeps(self):
+        """(B, 2) diagnostic: max PGS sweeps per island over the last step."""
+        out = np.zeros((self.B, 2), np.int32)
+        self.lib.orc_envs_sweeps(self.h, _ptr(out))
+        return out
 
 
 def philox4x32_10(ctr, key):

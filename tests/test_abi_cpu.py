@@ -77,7 +77,7 @@ int main(void) {{
   printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(cp_config), sizeof(cp_physics),
          offsetof(cp_config, seed), offsetof(cp_config, phys), offsetof(cp_physics, half_extents),
          offsetof(cp_physics, spawn_pos), offsetof(cp_physics, warmstart));
-  printf("%d %d\\n", CP_STATE_FIELDS, CP_SF_WS_LAM(9, 3));
+  printf("%d %d\\n", CP_STATE_FIELDS, CP_SF_WS_LAM(1, 4, 3));
   return 0;
 }}""")
     exe = tmp_path / "layout"
@@ -88,7 +88,7 @@ int main(void) {{
            abi.cp_config.phys.offset, abi.cp_physics.half_extents.offset, abi.cp_physics.spawn_pos.offset,
            abi.cp_physics.warmstart.offset]
     assert got == exp
-    assert list(map(int, out[1].split())) == [abi.CP_STATE_FIELDS, abi.CP_SF_WS_LAM(9, 3)]
+    assert list(map(int, out[1].split())) == [abi.CP_STATE_FIELDS, abi.CP_SF_WS_LAM(1, 4, 3)]
 
 
 def test_create_without_gpu_fails_loudly():
