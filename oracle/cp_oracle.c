@@ -244,12 +244,12 @@ void orc_default_config(cp_config* c) {
 
 static const int PAIR_A[CP_NUM_PAIRS] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3};
 static const int PAIR_B[CP_NUM_PAIRS] = {1, 2, 3, 4, 2, 3, 4, 3, 4, 4};
-/* Solver sweep order over pairs: the two cart-pole islands alternate ({ground,cart,pole}
- * pairs 0,1,4 and {ground,cart2,pole2} pairs 2,3,9), cross-island pairs 5-8 last.
- * Rows of different islands share no dynamic body, so the kernel may interleave them. */
-static const int SOLVE_ORDER[CP_NUM_PAIRS] = {0, 2, 1, 3, 4, 9, 5, 6, 7, 8};
-static const int ISLAND[CP_NUM_PAIRS] = {0, 0, 1, 1, 0, 2, 2, 2, 2, 1};
-/* island p's local pairs j = 0..4 -> global pair (own 3, then the 2 cross pairs it owns) */
+/* Contact islands: island 0 = {ground, cart, pole} (pairs 0, 1, 4), island 1 =
+ * {ground, cart2, pole2} (pairs 2, 3, 9); the cross pairs 5, 6 (cart-cart2, cart-pole2)
+ * are stored with island 0 and 7, 8 (pole-cart2, pole-pole2) with island 1.  Merged
+ * solve order over pairs: 0 2 1 3 4 9 5 6 7 8 (rows of different islands share no
+ * dynamic body, so the kernel runs the two islands' rows side by side).
+ * island p's local pairs j = 0..4 -> global pair (own 3, then the 2 cross pairs it stores) */
 static const int ISLAND_PAIR[CP_NUM_ISLANDS][CP_ISLAND_PAIRS] = {{0, 1, 4, 5, 6}, {2, 3, 9, 7, 8}};
 
 /* --------------------------------------------------------------- simulation */
@@ -562,11 +562,7 @@ static real solve_row(sim_t* S, const cp_physics* P, int a, int b, v3 rb, v3 t,
         S->v[da_] = madd(S->v[da_], neg(t), sa);
         S->w[da_] = madd(S->w[da_], neg(ia), dl);
     }
-#ifdef ORC_RESID_MAX
-    { real vr = dl / inv_eff; return vr * vr; }
-#else
     return FABS(e * dl);
-#endif
 }
 
 /* velocity change of an impulse lam along t at lever arm rb (warm start) */
@@ -601,13 +597,7 @@ static void sweep_normal(sim_t* S, const cp_physics* P, island_t* I, int isl, in
     manifold_t* m = &I->man[j];
     for (int k = 0; k < m->cnt; ++k) {
         point_t* q = &I->pt[m->base + k];
-        { real rr_ = solve_row(S, P, a, b, q->rb, m->n, q->inv_eff, q->target, &q->lam, 0, RC(0));
-#ifdef ORC_RESID_MAX
-        *r = rr_ > *r ? rr_ : *r;
-#else
-        *r = *r + rr_;
-#endif
-        }
+        *r = *r + solve_row(S, P, a, b, q->rb, m->n, q->inv_eff, q->target, &q->lam, 0, RC(0));
     }
 }
 static void sweep_friction(sim_t* S, const cp_physics* P, island_t* I, int isl, int j, real* r) {
@@ -621,20 +611,8 @@ static void sweep_friction(sim_t* S, const cp_physics* P, island_t* I, int isl, 
         point_t* q = &I->pt[m->base + k];
         fpoint_t* f = &I->fp[m->fbase + k];
         real bound = m->mu * q->lam;
-        { real rr_ = solve_row(S, P, a, b, q->rb, t1, f->inv_eff1, RC(0), &f->lam1, 1, bound);
-#ifdef ORC_RESID_MAX
-        *r = rr_ > *r ? rr_ : *r;
-#else
-        *r = *r + rr_;
-#endif
-        }
-        { real rr_ = solve_row(S, P, a, b, q->rb, t2, f->inv_eff2, RC(0), &f->lam2, 1, bound);
-#ifdef ORC_RESID_MAX
-        *r = rr_ > *r ? rr_ : *r;
-#else
-        *r = *r + rr_;
-#endif
-        }
+        *r = *r + solve_row(S, P, a, b, q->rb, t1, f->inv_eff1, RC(0), &f->lam1, 1, bound);
+        *r = *r + solve_row(S, P, a, b, q->rb, t2, f->inv_eff2, RC(0), &f->lam2, 1, bound);
     }
 }
 static void warm_pair(sim_t* S, const cp_physics* P, island_t* I, int isl, int j) {
