@@ -828,9 +828,9 @@ CP_DEV Dyn dyn_sel(bool second, const Body& a, const Sym& Ma, const Body& b, con
     return d;
 }
 
-// whole-env view for the cross rows: velocities and inverse inertias of the own
-// island's bodies from this lane, the other island's from the partner lane (both
-// lanes of a merged env are active wherever this runs); positions are in S.
+// whole-env view for the cross rows: positions, velocities and inverse inertias of
+// the own island's bodies from this lane, the other island's from the partner lane
+// (both lanes of a merged env are active wherever this runs).
 CP_DEV Sym partner_sym(const Sym& m) {
     Sym r;
     r.m0 = partner(m.m0); r.m1 = partner(m.m1); r.m2 = partner(m.m2);
@@ -845,7 +845,12 @@ CP_DEV Sym sel_sym(bool t, const Sym& a, const Sym& b) {
 }
 CP_DEV void cross_view(Sim& S, Step& T, const Isl& I, bool second) {
     const V3 v1 = partner(I.d1.v), w1 = partner(I.d1.w), v2 = partner(I.d2.v), w2 = partner(I.d2.w);
+    const V3 x1 = partner(I.d1.x), x2 = partner(I.d2.x);
     const Sym M1 = partner_sym(I.d1.M), M2 = partner_sym(I.d2.M);
+    S.b[0].x = selv(second, x1, I.d1.x);  // (a lane that adopted the env has no S of its own)
+    S.b[1].x = selv(second, x2, I.d2.x);
+    S.b[2].x = selv(second, I.d1.x, x1);
+    S.b[3].x = selv(second, I.d2.x, x2);
     S.b[0].v = selv(second, v1, I.d1.v);
     S.b[0].w = selv(second, w1, I.d1.w);
     S.b[1].v = selv(second, v2, I.d2.v);
@@ -866,13 +871,72 @@ CP_DEV void cross_back(Isl& I, const Sim& S, bool second) {
     I.d2.w = selv(second, S.b[3].w, S.b[1].w);
 }
 
-// One p.stepSimulation() for this lane's env (DESIGN.md §Physics model 1-6).
-// pool = this lane's LDS column, pool0 = the env's island-0 column (pool0 + 1 is island 1's).
-CP_DEV void substep(Sim& S, const cp_physics& P, const Lane& L, float* pool, float* pool0, int& overflow,
-                    const Mem& G, Stamps& ST) {
+// Per-lane solve state of one substep, between its phases (prep -> sweeps ->
+// [migration] -> finish).  Everything a lane needs to continue its island's PGS
+// sweeps lives in here (plus its LDS pool column), so another lane of the
+// workgroup can adopt it (cp_kernels.hip: straggler migration).
+struct Ctx {
+    Step T;          // own island's manifold headers (+ whole-env M for the cross rows)
+    Isl I;           // own island's bodies
+    float mu0, mu1, mu2;
+    int used, tot;   // rows of the own island, of the env
+    bool merged, active;
+};
+
+// One PGS sweep range [it0, it1) over the lane's island (+ the cross rows of a merged
+// env).  S supplies positions for the cross rows and is scratch for their whole-env
+// view.  Lanes stop after the sweep whose residual is <= the threshold.
+CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, float* pool, float* pool0, bool second, int it0, int it1,
+                   Stamps& ST) {
+    const float thr = P.residual_threshold;
+    for (int it = it0; it < it1; ++it) {
+        if (__ballot(c.active) == 0ull) break;
+#ifdef CP_STAMPS
+        ST.sweeps += 1;
+#endif
+        float r = 0.0f, rc = 0.0f;
+        if (c.active) {
+            isl_normal_rows<0>(c.I, c.T, pool, r);
+            isl_normal_rows<1>(c.I, c.T, pool, r);
+            isl_normal_rows<2>(c.I, c.T, pool, r);
+        }
+        const bool cross = c.active && c.merged;  // same on both lanes of an env
+        if (__ballot(cross) != 0ull && cross) {
+            cross_view(S, c.T, c.I, second);
+            pair_normal_rows<5>(S, c.T, second, P, pool0, rc);
+            pair_normal_rows<6>(S, c.T, second, P, pool0, rc);
+            pair_normal_rows<7>(S, c.T, second, P, pool0, rc);
+            pair_normal_rows<8>(S, c.T, second, P, pool0, rc);
+            cross_back(c.I, S, second);
+        }
+        if (c.active) {
+            isl_friction_rows<0>(c.I, c.T, c.mu0, pool, r);
+            isl_friction_rows<1>(c.I, c.T, c.mu1, pool, r);
+            isl_friction_rows<2>(c.I, c.T, c.mu2, pool, r);
+        }
+        if (__ballot(cross) != 0ull && cross) {
+            cross_view(S, c.T, c.I, second);
+            pair_friction_rows<5>(S, c.T, second, P, pool0, rc);
+            pair_friction_rows<6>(S, c.T, second, P, pool0, rc);
+            pair_friction_rows<7>(S, c.T, second, P, pool0, rc);
+            pair_friction_rows<8>(S, c.T, second, P, pool0, rc);
+            cross_back(c.I, S, second);
+        }
+        const float rp = partner(r);  // every lane that entered the loop is here (pairs together)
+        const float joint = second ? (rp + r) + rc : (r + rp) + rc;
+        if (c.active && (c.merged ? joint : r) <= thr) c.active = false;
+    }
+}
+
+// Phase 1 of one p.stepSimulation() (DESIGN.md §Physics model 1-5a): narrowphase and
+// row setup of the lane's island, unconstrained velocity update of the whole env,
+// the island view and the warm start.  A lane with live == false (done env, padding)
+// makes no contacts and writes nothing.
+CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, float* pool, float* pool0, int& overflow,
+                         const Mem& G, Stamps& ST, bool live, Ctx& c) {
     const float dt = P.dt, inv_dt = P.inv_dt;
     CP_STAMP(t0);
-    Step T;
+    Step& T = c.T;
     // 2. narrowphase + row setup of the lane's island: wave-uniform loop over its 5
     //    local pairs (the global pair, hence the bodies, differ between the two lanes)
     int used = 0, fused = 0;
@@ -884,7 +948,7 @@ CP_DEV void substep(Sim& S, const cp_physics& P, const Lane& L, float* pool, flo
         Contact C;
         C.m = 0;
         C.n = mk(0.0f, 0.0f, 1.0f);
-        if (!face_separated(A, Bx, P.contact_margin)) box_box(A, Bx, P.contact_margin, P.edge_bias, C);
+        if (live && !face_separated(A, Bx, P.contact_margin)) box_box(A, Bx, P.contact_margin, P.edge_bias, C);
         const float mu = sel5p(a, P.friction) * sel5p(b, P.friction);
         const float ima = sel5p(a, P.inv_mass), imb = sel5p(b, P.inv_mass);
         const V3 xa = A.c, xb = Bx.c;
@@ -944,7 +1008,7 @@ CP_DEV void substep(Sim& S, const cp_physics& P, const Lane& L, float* pool, flo
         G.sx(4 * j + 1, C.n.y);
         G.sx(4 * j + 2, C.n.z);
         G.sx(4 * j + 3, __uint_as_float(pk));
-        G.sw(CP_SF_WS_ID(0, j), __uint_as_float(nid));
+        if (live) G.sw(CP_SF_WS_ID(0, j), __uint_as_float(nid));
     }
 #pragma unroll
     for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
@@ -979,18 +1043,18 @@ CP_DEV void substep(Sim& S, const cp_physics& P, const Lane& L, float* pool, flo
     }
     S.f0 = mk(0.0f, 0.0f, 0.0f);  // 6. external forces are consumed by the step
     S.f2 = mk(0.0f, 0.0f, 0.0f);
-    // 4. solve.  No cross-island contact: each lane solves its own island
-    //    (oracle: independent islands).  Otherwise both lanes run the merged solve.
-    //    (DPP reads the partner lane's register: evaluate it in converged code, never
-    //    under a short-circuit or branch where the partner may be inactive.)
+    // 4. solve setup.  No cross-island contact: each lane solves its own island
+    //    (oracle: independent islands); otherwise the env is "merged" and its cross
+    //    rows run on both lanes.  (DPP reads the partner lane's register: evaluate it
+    //    in converged code, never under a branch where the partner may be inactive.)
     const uint32_t own_cross = (pk_cnt(T.pk[3]) + pk_cnt(T.pk[4])) > 0 ? 1u : 0u;
     const uint32_t any_cross = own_cross | partner_u(own_cross);
-    const bool merged = any_cross != 0u;
-    const int tot = used + (int)partner_u((uint32_t)used);
+    c.merged = any_cross != 0u;
+    c.used = used;
+    c.tot = used + (int)partner_u((uint32_t)used);
     const bool second = L.isl != 0;
-    const float thr = P.residual_threshold;
     // the island's two bodies (cart, pole or cart2, pole2) with their world inverse inertia
-    Isl I;
+    Isl& I = c.I;
     {
         I.d1.x = selv(second, S.b[2].x, S.b[0].x);
         I.d1.v = selv(second, S.b[2].v, S.b[0].v);
@@ -1007,62 +1071,38 @@ CP_DEV void substep(Sim& S, const cp_physics& P, const Lane& L, float* pool, flo
         I.im1 = L.im1;
         I.im2 = L.im2;
     }
+    c.mu0 = L.mu0;
+    c.mu1 = L.mu1;
+    c.mu2 = L.mu2;
     CP_STAMP(t2);
     CP_ACC(vel, t1, t2);
     // Island rows run per lane; the rows of the two islands touch disjoint bodies,
     // so running them side by side equals the oracle's interleaved order.  Cross
-    // rows (an env with a cross-island contact: "merged") run on both lanes on the
-    // whole-env view after the island rows of the same kind, as in the oracle; a
-    // merged env stops on the joint residual (island 0 + island 1) + cross.
+    // rows (merged env) run on both lanes on the whole-env view after the island
+    // rows of the same kind, as in the oracle; a merged env stops on the joint
+    // residual (island 0 + island 1) + cross.
     isl_warmstart<0>(I, T, pool);
     isl_warmstart<1>(I, T, pool);
     isl_warmstart<2>(I, T, pool);
-    if (__ballot(merged) != 0ull && merged) {
+    if (__ballot(c.merged) != 0ull && c.merged) {
         cross_view(S, T, I, second);
         pair_warmstart<5>(S, T, second, P, pool0); pair_warmstart<6>(S, T, second, P, pool0);
         pair_warmstart<7>(S, T, second, P, pool0); pair_warmstart<8>(S, T, second, P, pool0);
         cross_back(I, S, second);
     }
-    bool active = merged ? tot > 0 : used > 0;
-    for (int it = 0; it < P.solver_iterations; ++it) {
-        if (__ballot(active) == 0ull) break;
-#ifdef CP_STAMPS
-        ST.sweeps += 1;
-#endif
-        float r = 0.0f, rc = 0.0f;
-        if (active) {
-            isl_normal_rows<0>(I, T, pool, r);
-            isl_normal_rows<1>(I, T, pool, r);
-            isl_normal_rows<2>(I, T, pool, r);
-        }
-        const bool cross = active && merged;  // same on both lanes of an env
-        if (__ballot(cross) != 0ull && cross) {
-            cross_view(S, T, I, second);
-            pair_normal_rows<5>(S, T, second, P, pool0, rc);
-            pair_normal_rows<6>(S, T, second, P, pool0, rc);
-            pair_normal_rows<7>(S, T, second, P, pool0, rc);
-            pair_normal_rows<8>(S, T, second, P, pool0, rc);
-            cross_back(I, S, second);
-        }
-        if (active) {
-            isl_friction_rows<0>(I, T, L.mu0, pool, r);
-            isl_friction_rows<1>(I, T, L.mu1, pool, r);
-            isl_friction_rows<2>(I, T, L.mu2, pool, r);
-        }
-        if (__ballot(cross) != 0ull && cross) {
-            cross_view(S, T, I, second);
-            pair_friction_rows<5>(S, T, second, P, pool0, rc);
-            pair_friction_rows<6>(S, T, second, P, pool0, rc);
-            pair_friction_rows<7>(S, T, second, P, pool0, rc);
-            pair_friction_rows<8>(S, T, second, P, pool0, rc);
-            cross_back(I, S, second);
-        }
-        const float rp = partner(r);  // converged: every lane that entered the loop is here
-        const float joint = second ? (rp + r) + rc : (r + rp) + rc;
-        if (active && (merged ? joint : r) <= thr) active = false;
-    }
-    // whole-env velocities from the two lanes' islands (converged point: both lanes active)
+    c.active = c.merged ? c.tot > 0 : used > 0;
+}
+
+// Phase 3: whole-env velocities from the two lanes' islands (both lanes of every
+// env active), the warm-start cache refresh and the integration (DESIGN.md
+// §Physics model 5b-7).
+CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx& c, float* pool, const Mem& G,
+                           Stamps& ST, bool live) {
+    const float dt = P.dt, inv_dt = P.inv_dt;
+    const bool second = L.isl != 0;
+    CP_STAMP(t3);
     {
+        const Isl& I = c.I;
         const V3 v1 = partner(I.d1.v), w1 = partner(I.d1.w), v2 = partner(I.d2.v), w2 = partner(I.d2.w);
         S.b[0].v = selv(second, v1, I.d1.v);
         S.b[0].w = selv(second, w1, I.d1.w);
@@ -1073,14 +1113,15 @@ CP_DEV void substep(Sim& S, const cp_physics& P, const Lane& L, float* pool, flo
         S.b[3].v = selv(second, I.d2.v, v2);
         S.b[3].w = selv(second, I.d2.w, w2);
     }
-    CP_STAMP(t3);
-    CP_ACC(solve, t2, t3);
-    // 4c. refresh the warm-start cache of the lane's island
+    // refresh the warm-start cache of the lane's island
+    if (live) {
 #pragma unroll
-    for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
-        const int cnt = pk_cnt(T.pk[j]), base = pk_base(T.pk[j]);
+        for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
+            const int cnt = pk_cnt(c.T.pk[j]), base = pk_base(c.T.pk[j]);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) G.sl(CP_SF_WS_LAM(0, j, k), (k < cnt) ? pool_n(pool, F_LAM, base + k) : 0.0f);
+            for (int k = 0; k < 4; ++k)
+                G.sl(CP_SF_WS_LAM(0, j, k), (k < cnt) ? pool_n(pool, F_LAM, base + k) : 0.0f);
+        }
     }
     // 5. integrate positions and orientations (both lanes, whole env)
     const float hdt = 0.5f * dt;
@@ -1115,6 +1156,19 @@ CP_DEV void substep(Sim& S, const cp_physics& P, const Lane& L, float* pool, flo
 #ifdef CP_STAMPS
     ST.substeps += 1;
 #endif
+}
+
+
+// One p.stepSimulation() for this lane's env, without migration (all sweeps in place).
+CP_DEV void substep(Sim& S, const cp_physics& P, const Lane& L, float* pool, float* pool0, int& overflow,
+                    const Mem& G, Stamps& ST, bool live = true) {
+    Ctx c;
+    substep_prep(S, P, L, pool, pool0, overflow, G, ST, live, c);
+    CP_STAMP(t2);
+    sweeps(c, S, P, pool, pool0, L.isl != 0, 0, P.solver_iterations, ST);
+    CP_STAMP(t3);
+    CP_ACC(solve, t2, t3);
+    substep_finish(S, P, L, c, pool, G, ST, live);
 }
 
 // LINK_FRAME force at the COM on cart (C = 0) or cart2 (C = 1): world = R(q) f

@@ -51,6 +51,11 @@ def main(prof_dir, tag, out_dir):
     res = {"tag": tag, "source": os.path.relpath(prof_dir), "kernels": {}}
     dur = durations(os.path.join(prof_dir, "trace", "run_kernel_trace.csv"))
     sq, n_sq = counters(os.path.join(prof_dir, "sq", "run_counter_collection.csv"))
+    p2 = os.path.join(prof_dir, "sq2", "run_counter_collection.csv")
+    if os.path.exists(p2):
+        sq2, _ = counters(p2)
+        for k, cs in sq2.items():
+            sq.setdefault(k, {}).update(cs)
     fe, _ = counters(os.path.join(prof_dir, "fetch", "run_counter_collection.csv"))
     wr, _ = counters(os.path.join(prof_dir, "write", "run_counter_collection.csv"))
     for k in dur:
