@@ -46,6 +46,12 @@ def step_kernel_bytes(R, action_bytes):
     return 4 * (state_read + state_write + warm_cache) + action_bytes + 4 * 14 * R + 4 + 1 + 8
 
 
+def render_kernel_bytes(H, W, C, R):
+    """Algorithmic HBM bytes of one env's raster obs (render kernel): the float16 image
+    (H, W, 3, C, R) written once, the R x 4 repeat-end poses read, one list entry."""
+    return 2 * H * W * 3 * C * R + 4 * R * 4 * 7 + 4
+
+
 def pmc_traffic(kernel, batch, repeats):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
     (profiles/<tag>_pmc.json, tools/profile.sh + tools/summarize_profile.py), if it was
@@ -111,6 +117,9 @@ def main():
     ap.add_argument("--repeats", type=int, default=3)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--raster", action="store_true",
+                    help="BASELINE.json configs[4] (C5): + in-kernel 50x50x3 fp16 raster obs per repeat")
+    ap.add_argument("--cameras", type=int, default=1)
     ap.add_argument("--solver-iterations", type=int, default=None,
                     help="override the PGS sweep cap (default: the model's 50; non-default runs are diagnostics)")
     args = ap.parse_args()
@@ -131,6 +140,8 @@ def main():
                           initial_force=55.0, autoreset=True, seed=spec["seed"],
                           env_id_offset=spec["env_id_offset"],
                           **({} if args.solver_iterations is None else {"solver_iterations": args.solver_iterations}))
+    if args.raster:
+        env.enable_raster(True, num_cameras=args.cameras)
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     actions = torch.randint(0, 5, (W + K, B, 2), dtype=torch.int8, device=dev, generator=gen)
     env.reset()
@@ -166,7 +177,16 @@ def main():
     per_launch_s = tm["step_ms"] / max(1, tm["step_launches"]) / 1e3
     bytes_launch = B * step_kernel_bytes(R, 2)
     achieved = bytes_launch / per_launch_s / 1e9
-    traffic, traffic_src = pmc_traffic("cp_step_kernel<discrete>", B, R)
+    kernel = "cp_step_kernel<discrete>"
+    traffic, traffic_src = pmc_traffic(kernel, B, R)
+    if args.raster:
+        # C5: the render kernel writes 2.9 GB per step and is the dominant HBM consumer
+        rc = env.raster_cfg
+        per_launch_s = tm["render_ms"] / max(1, tm["render_launches"]) / 1e3  # one launch per step
+        bytes_launch = B * render_kernel_bytes(rc.height, rc.width, rc.num_cameras, R)
+        achieved = bytes_launch / per_launch_s / 1e9
+        kernel = "cp_render_kernel"
+        traffic, traffic_src = pmc_traffic(kernel, B, R)
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -180,9 +200,12 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (random discrete actions, Philox bump pushes; no pybullet, see DESIGN.md)",
-        "config": {"workload": "C3: batch=65,536 envs/GPU, discrete 5-action, R=3, S=1, autoreset at 200, "
-                               "initial_force=55, fp32 (BASELINE.json configs[2]; N>1 = C4 with RCCL all-gather "
-                               "of episode returns per 200-step window)",
+        "config": {"workload": ("C5: batch=65,536 envs/GPU, discrete 5-action, R=3, S=1, autoreset at 200, "
+                                "initial_force=55, fp32 physics + in-kernel raster obs 50x50x3xR fp16 to HBM "
+                                f"({args.cameras} camera(s); BASELINE.json configs[4])") if args.raster else
+                               ("C3: batch=65,536 envs/GPU, discrete 5-action, R=3, S=1, autoreset at 200, "
+                                "initial_force=55, fp32 (BASELINE.json configs[2]; N>1 = C4 with RCCL all-gather "
+                                "of episode returns per 200-step window)"),
                    "global_batch": world * B, "envs_per_gpu": B, "action_repeats": R, "steps_per_repeat": 1,
                    "parallelism": f"dp{world} (independent env shards, no per-step collective)",
                    "solver_iterations": env.cfg.phys.solver_iterations},
@@ -190,11 +213,13 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                      "traffic_source": traffic_src and (traffic_src + " (2*FETCH_SIZE + WRITE_SIZE) KiB*1024 "
                                                         "per launch, rocprofv3 --pmc, separate passes"),
-                     "kernel": "cp_step_kernel<discrete>",
+                     "kernel": kernel,
                      "bytes_per_launch": bytes_launch,
                      "avg_launch_ms": round(per_launch_s * 1e3, 4),
                      "launches": tm["step_launches"],
-                     "reset_kernel_avg_ms": round(tm["reset_ms"] / max(1, tm["reset_launches"]), 4)},
+                     "reset_kernel_avg_ms": round(tm["reset_ms"] / max(1, tm["reset_launches"]), 4),
+                     **({"step_kernel_avg_ms": round(tm["step_ms"] / max(1, tm["step_launches"]), 4),
+                         "render_launches": tm["render_launches"]} if args.raster else {})},
         "episode_return_hist_nonzero": None if hist is None else int((hist > 0).sum().item()),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -103,6 +103,30 @@ class cp_config(C.Structure):
     ]
 
 
+class cp_raster_config(C.Structure):
+    """include/cartpole_amd.h: cp_raster_config (raster obs, bullet_cartpole.py:277-306)."""
+    _fields_ = [
+        ("width", C.c_int32),
+        ("height", C.c_int32),
+        ("num_cameras", C.c_int32),
+        ("eye", _F3 * 2),
+        ("target", _F3),
+        ("up", _F3),
+        ("tan_half_fov", C.c_float),
+        ("far_plane", C.c_float),
+        ("light", _F3),
+        ("ambient", C.c_float),
+        ("diffuse", C.c_float),
+        ("background", _F3),
+        ("color", _F3 * CP_NUM_BODIES),
+    ]
+
+
+def pixels_shape(B, H, W, C_, R):
+    """Raster obs per env (H, W, 3, C, R), bullet_cartpole.py:299-306 (camera before repeat)."""
+    return (B, H, W, 3, C_, R)
+
+
 def obs_shape(B, R):
     return (B, R, 2, 7)
 

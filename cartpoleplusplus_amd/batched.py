@@ -51,6 +51,7 @@ class BatchedCartpole:
         self.done = torch.zeros(self.B, device=self.device, dtype=torch.uint8)
         self.terminal_obs = torch.zeros_like(self.obs) if config.autoreset else None
         self.readback = None
+        self.pixels = None
 
     # -------------------------------------------------------------- plumbing
     def _stream(self):
@@ -107,6 +108,20 @@ class BatchedCartpole:
         native.check(self.h, self.lib.cp_set_readback(self.h, _ptr(self.readback), int(bool(reference_bug))),
                      "cp_set_readback")
 
+    def enable_raster(self, on=True, raster_config=None, **kw):
+        """Raster obs (--use-raw-pixels, bullet_cartpole.py:277-306) into self.pixels,
+        float16 (B, H, W, 3, C, R); rendered by every later step / reset."""
+        if not on:
+            self.pixels = None
+            native.check(self.h, self.lib.cp_set_raster(self.h, None, None), "cp_set_raster")
+            return None
+        rc = raster_config if raster_config is not None else native.default_raster_config(**kw)
+        self.raster_cfg = rc
+        self.pixels = torch.zeros(abi.pixels_shape(self.B, rc.height, rc.width, rc.num_cameras, self.R),
+                                  device=self.device, dtype=torch.float16)
+        native.check(self.h, self.lib.cp_set_raster(self.h, C.byref(rc), _ptr(self.pixels)), "cp_set_raster")
+        return self.pixels
+
     def set_bump_forces(self, forces):
         """Parity mode (bump_mode='host'): LINK-frame bump forces (B, 30, 2, 2)."""
         f = torch.as_tensor(forces, dtype=torch.float32, device=self.device).contiguous()
@@ -140,7 +155,11 @@ class BatchedCartpole:
         sn, rn = C.c_int32(), C.c_int32()
         native.check(self.h, self.lib.cp_timing_end(self.h, C.byref(sm), C.byref(sn), C.byref(rm), C.byref(rn)),
                      "cp_timing_end")
-        return dict(step_ms=sm.value, step_launches=sn.value, reset_ms=rm.value, reset_launches=rn.value)
+        out = dict(step_ms=sm.value, step_launches=sn.value, reset_ms=rm.value, reset_launches=rn.value)
+        pm, pn = C.c_double(), C.c_int32()
+        native.check(self.h, self.lib.cp_timing_render(self.h, C.byref(pm), C.byref(pn)), "cp_timing_render")
+        out.update(render_ms=pm.value, render_launches=pn.value)
+        return out
 
     def overflow_counts(self):
         o = torch.empty(self.B, device=self.device, dtype=torch.int32)

@@ -87,8 +87,10 @@ class BulletCartpole(Env):
         self.use_raw_pixels = opts.use_raw_pixels
         self.render_width, self.render_height = opts.render_width, opts.render_height
         if self.use_raw_pixels:
-            raise NotImplementedError("--use-raw-pixels: in-kernel raster obs is a later row (DESIGN.md §Scope)")
-        state_shape = (self.repeats, 2, 7)
+            # (H, W, 3, C, R), :121-126; filled by the in-kernel ray caster (cp_set_raster)
+            state_shape = (self.render_height, self.render_width, 3, self.num_cameras, self.repeats)
+        else:
+            state_shape = (self.repeats, 2, 7)
         fmax = np.finfo(np.float32).max
         self.observation_space = Box(-fmax, fmax, state_shape)
         assert opts.reward_calc in ['fixed', 'angle', 'action', 'angle_action']
@@ -100,7 +102,18 @@ class BulletCartpole(Env):
             max_episode_len=self.max_episode_len, action_force=self.action_force,
             initial_force=self.initial_force, random_theta=self.random_theta, bump_mode="host")
         self._env.enable_readback(True, reference_bug=True)
+        if self.use_raw_pixels:
+            self._env.enable_raster(True, width=self.render_width, height=self.render_height,
+                                    num_cameras=self.num_cameras)
         self._act = torch.zeros((1, 2, 2), dtype=torch.float32, device=self._env.device)
+
+    def _capture(self, obs):
+        # set_state_element_for_repeat (:298-311): pixels (float16 values, float32 state)
+        # or the (R, 2, 7) poses
+        if self.use_raw_pixels:
+            self.state[...] = self._env.pixels[0].float().cpu().numpy()
+        else:
+            self.state[...] = obs[0].cpu().numpy()
 
     def configure(self, display=None):
         pass
@@ -117,7 +130,7 @@ class BulletCartpole(Env):
         self._env.set_bump_forces(
             draw_bump_forces(self.initial_force, self.random_theta, self.initial_force_steps)[None])
         obs = self._env.reset()
-        self.state[...] = obs[0].cpu().numpy()
+        self._capture(obs)
         return np.copy(self.state)
 
     def step(self, action):
@@ -137,7 +150,7 @@ class BulletCartpole(Env):
         obs, _, done = self._env.step(self._act)
         if self.delay > 0:
             time.sleep(self.delay * self.repeats * self.steps_per_repeat)
-        self.state[...] = obs[0].cpu().numpy()
+        self._capture(obs)
         rb = self._env.readback[0].cpu().numpy()     # (2, R, S, 4, 3)
         self.monkey_positions = np.ascontiguousarray(rb[:, :, :, 0:2, :]).astype(np.float64)
         self.monkey_velocities = np.ascontiguousarray(rb[:, :, :, 2:4, :]).astype(np.float64)

@@ -25,6 +25,7 @@
 
 #include "../../include/cartpole_amd.h"
 #include "cp_physics.h"
+#include "cp_raster.h"
 
 namespace cp {
 
@@ -48,7 +49,20 @@ struct Bufs {
     int32_t* count;    // [1] reset list length
     float* scratch;    // [4*CP_ISLAND_PAIRS][2B] manifold headers of the current substep, per lane
     uint64_t* stamps;  // [waves][8] diagnostic phase cycles (CP_STAMPS builds only)
+    float* rposes;     // [B][R][4][7] repeat-end poses for the raster obs (NULL: raster off)
+    int32_t* rlist;    // [B] envs to render after the step kernel
+    int32_t* rcount;   // [1]
 };
+
+// raster obs: the repeat-end pose of the 4 bodies (xyz, quat xyzw) for the render kernel
+CP_DEV void write_rposes(const Sim& S, float* dst) {
+#pragma unroll
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        float* o = dst + d * 7;
+        o[0] = S.b[d].x.x; o[1] = S.b[d].x.y; o[2] = S.b[d].x.z;
+        o[3] = S.b[d].q[0]; o[4] = S.b[d].q[1]; o[5] = S.b[d].q[2]; o[6] = S.b[d].q[3];
+    }
+}
 
 // per-wave stamp accumulation into b.stamps (lane 0 writes; CP_STAMPS builds only)
 CP_DEV void flush_stamps(const Stamps& ST, uint64_t* dst, uint64_t total) {
@@ -257,6 +271,8 @@ __global__ void CP_PHYS_ATTR cp_reset_kernel(cp_config cfg, Bufs b, float* obs_o
     float row[14];
     write_obs_row(S, row);
     const int R = cfg.action_repeats;
+    if (b.rposes)  // every repeat slot shows the reset pose (bullet_cartpole.py:342-345)
+        for (int r = 0; r < R; ++r) write_rposes(S, b.rposes + ((size_t)i * R + r) * CP_NUM_DYN * 7);
     float* o = obs_out + (size_t)i * R * 14;
     for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -281,6 +297,7 @@ __global__ void CP_PHYS_ATTR cp_step_kernel(cp_config cfg, Bufs b, const void* a
     float* pool = lds_pool + threadIdx.x;
     float* pool0 = lds_pool + (threadIdx.x & ~1u);
     bool want_reset = false;
+    bool render_me = false;  // simulated this step: its frames go to the render kernel
     Stamps ST;
     CP_STAMP(k0);
     if (inb) {
@@ -329,8 +346,10 @@ __global__ void CP_PHYS_ATTR cp_step_kernel(cp_config cfg, Bufs b, const void* a
                     write_obs_row(S, row);
 #pragma unroll
                     for (int f = 0; f < 14; ++f) obs[r * 14 + f] = row[f];
+                    if (b.rposes) write_rposes(S, b.rposes + ((size_t)i * R + r) * CP_NUM_DYN * 7);
                 }
             }
+            render_me = lead && b.rposes != nullptr;
             ov += (int)partner_u((uint32_t)ov);
             if (ov && lead) b.overflow[i] += ov;
             const int steps = ldi(G.st, CP_SF_STEPS, G.off) + 1;
@@ -371,6 +390,15 @@ __global__ void CP_PHYS_ATTR cp_step_kernel(cp_config cfg, Bufs b, const void* a
         base = __shfl(base, 0);
         if (want_reset) b.list[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
     }
+    if (b.rposes) {
+        const uint64_t bal = __ballot(render_me);
+        const int lane = threadIdx.x & (WAVE - 1);
+        const int n = __popcll(bal);
+        int base = 0;
+        if (lane == 0 && n) base = atomicAdd(b.rcount, n);
+        base = __shfl(base, 0);
+        if (render_me) b.rlist[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
+    }
 }
 
 __global__ void __launch_bounds__(256) cp_copy_kernel(const float* src, float* dst, size_t n) {
@@ -382,9 +410,11 @@ __global__ void __launch_bounds__(256) cp_copy_kernel(const float* src, float* d
 
 // ============================================================================ C-ABI
 struct cp_timing {
-    int cap = 0;                 // event pairs per kind
-    int nstep = 0, nreset = 0;   // pairs recorded
-    std::vector<hipEvent_t> ev;  // [0, 2cap): step pairs, [2cap, 4cap): reset pairs
+    int cap = 0;                             // event pairs per kind
+    int nstep = 0, nreset = 0, nrender = 0;  // pairs recorded
+    double render_ms = 0.0;                  // summed by cp_timing_end
+    int render_launches = 0;
+    std::vector<hipEvent_t> ev;  // [0, 2cap): step pairs, [2cap, 4cap): reset, [4cap, 6cap): render
 };
 
 struct cp_handle {
@@ -394,20 +424,22 @@ struct cp_handle {
     float* readback;
     int readback_bug;
     cp_timing timing;
+    cp_raster_config raster;
+    uint16_t* pixels;  // raster obs output (NULL: raster off)
     std::string err;
 };
 
 static void timing_free(cp_timing& t) {
     for (hipEvent_t e : t.ev) (void)hipEventDestroy(e);
     t.ev.clear();
-    t.cap = t.nstep = t.nreset = 0;
+    t.cap = t.nstep = t.nreset = t.nrender = 0;
 }
-// returns the event pair to record around a launch of `kind` (0 step, 1 reset), or nullptr
+// returns the event pair to record around a launch of `kind` (0 step, 1 reset, 2 render), or nullptr
 static hipEvent_t* timing_slot(cp_handle* h, int kind) {
     cp_timing& t = h->timing;
     if (t.cap == 0) return nullptr;
-    int& n = kind == 0 ? t.nstep : t.nreset;
-    if (n >= t.cap) return nullptr;
+    int& n = kind == 0 ? t.nstep : (kind == 1 ? t.nreset : t.nrender);
+    if (n >= (kind == 2 ? 2 * t.cap : t.cap)) return nullptr;  // up to 2 render launches per step
     hipEvent_t* p = &t.ev[(size_t)(kind * t.cap + n) * 2];
     ++n;
     return p;
@@ -512,6 +544,8 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     h->device = device;
     h->readback = nullptr;
     h->readback_bug = 1;
+    h->pixels = nullptr;
+    cp_default_raster_config(&h->raster);
     std::memset(&h->b, 0, sizeof(h->b));
     const size_t B = (size_t)cfg->num_envs;
     const int R = cfg->action_repeats;
@@ -567,16 +601,31 @@ void cp_destroy(cp_handle* h) {
     (void)hipFree(h->b.count);
     (void)hipFree(h->b.scratch);
     (void)hipFree(h->b.stamps);
+    (void)hipFree(h->b.rposes);
+    (void)hipFree(h->b.rlist);
+    (void)hipFree(h->b.rcount);
     delete h;
 }
 
-static int launch_reset_from_list(cp_handle* h, float* obs_out, hipStream_t st) {
+// raster obs of the envs in list[0 .. *count) (a device count: the grid covers B)
+static int launch_render(cp_handle* h, const int32_t* list, const int32_t* count, hipStream_t st) {
+    hipEvent_t* ev = timing_slot(h, 2);
+    if (ev) CP_TRY(h, hipEventRecord(ev[0], st));
+    hipLaunchKernelGGL(cp::cp_render_kernel, dim3((unsigned)h->cfg.num_envs), dim3(cp::RT), 0, st, h->raster,
+                       h->cfg.phys, h->cfg.action_repeats, list, count, h->b.rposes, h->pixels);
+    if (check(h, hipGetLastError(), "cp_render_kernel")) return -1;
+    if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
+    return 0;
+}
+
+static int launch_reset_from_list(cp_handle* h, float* obs_out, hipStream_t st, bool render) {
     const int B = h->cfg.num_envs;
     hipEvent_t* ev = timing_slot(h, 1);
     if (ev) CP_TRY(h, hipEventRecord(ev[0], st));
     hipLaunchKernelGGL(cp::cp_reset_kernel, dim3(grid_for(2 * B, cp::WAVE)), dim3(cp::WAVE), 0, st, h->cfg, h->b, obs_out);
     if (check(h, hipGetLastError(), "cp_reset_kernel")) return -1;
     if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
+    if (render && h->pixels) return launch_render(h, h->b.list, h->b.count, st);
     return 0;
 }
 
@@ -589,7 +638,7 @@ int cp_reset(cp_handle* h, const uint8_t* env_mask, float* obs_out, void* stream
     hipLaunchKernelGGL(cp::cp_mask_to_list_kernel, dim3(grid_for(B, 256)), dim3(256), 0, st, B, env_mask, h->b.list,
                        h->b.count);
     CP_TRY(h, hipGetLastError());
-    return launch_reset_from_list(h, obs_out, st);
+    return launch_reset_from_list(h, obs_out, st, true);
 }
 
 int cp_step(cp_handle* h, const void* actions, int action_kind, float* obs_out, float* reward_out,
@@ -601,6 +650,7 @@ int cp_step(cp_handle* h, const void* actions, int action_kind, float* obs_out, 
     const int B = h->cfg.num_envs;
     CP_TRY(h, hipSetDevice(h->device));
     if (h->cfg.autoreset) CP_TRY(h, hipMemsetAsync(h->b.count, 0, sizeof(int32_t), st));
+    if (h->pixels) CP_TRY(h, hipMemsetAsync(h->b.rcount, 0, sizeof(int32_t), st));
     dim3 grid(grid_for(2 * B, cp::WAVE)), block(cp::WAVE);  // two lanes per env
     hipEvent_t* ev = timing_slot(h, 0);
     if (ev) CP_TRY(h, hipEventRecord(ev[0], st));
@@ -612,7 +662,10 @@ int cp_step(cp_handle* h, const void* actions, int action_kind, float* obs_out, 
                            obs_out, reward_out, done_out, terminal_obs_out, h->readback, h->readback_bug);
     CP_TRY(h, hipGetLastError());
     if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
-    if (h->cfg.autoreset) return launch_reset_from_list(h, obs_out, st);
+    // autoreset envs were simulated this step, so they are in the render list; the reset
+    // kernel rewrites their poses first, and the one render launch draws the new episode
+    if (h->cfg.autoreset && launch_reset_from_list(h, obs_out, st, false)) return -1;
+    if (h->pixels) return launch_render(h, h->b.rlist, h->b.rcount, st);
     return 0;
 }
 
@@ -683,7 +736,7 @@ int cp_timing_begin(cp_handle* h, int max_launches) {
     if (!h || max_launches <= 0) return fail(h, "cp_timing_begin: bad argument");
     CP_TRY(h, hipSetDevice(h->device));
     timing_free(h->timing);
-    h->timing.ev.resize((size_t)max_launches * 4);
+    h->timing.ev.resize((size_t)max_launches * 8);
     for (auto& e : h->timing.ev) CP_TRY(h, hipEventCreate(&e));
     h->timing.cap = max_launches;
     return 0;
@@ -693,9 +746,9 @@ int cp_timing_end(cp_handle* h, double* step_ms, int32_t* step_launches, double*
                   int32_t* reset_launches) {
     if (!h) return fail(h, "cp_timing_end: null handle");
     cp_timing& t = h->timing;
-    double sums[2] = {0.0, 0.0};
-    int counts[2] = {t.nstep, t.nreset};
-    for (int kind = 0; kind < 2; ++kind) {
+    double sums[3] = {0.0, 0.0, 0.0};
+    int counts[3] = {t.nstep, t.nreset, t.nrender};
+    for (int kind = 0; kind < 3; ++kind) {
         for (int n = 0; n < counts[kind]; ++n) {
             hipEvent_t a = t.ev[(size_t)(kind * t.cap + n) * 2], b = t.ev[(size_t)(kind * t.cap + n) * 2 + 1];
             CP_TRY(h, hipEventSynchronize(b));
@@ -709,6 +762,80 @@ int cp_timing_end(cp_handle* h, double* step_ms, int32_t* step_launches, double*
     if (reset_ms) *reset_ms = sums[1];
     if (reset_launches) *reset_launches = counts[1];
     timing_free(t);
+    t.render_ms = sums[2];
+    t.render_launches = counts[2];
+    return 0;
+}
+
+int cp_timing_render(cp_handle* h, double* render_ms, int32_t* render_launches) {
+    if (!h) return fail(h, "cp_timing_render: null handle");
+    if (render_ms) *render_ms = h->timing.render_ms;
+    if (render_launches) *render_launches = h->timing.render_launches;
+    return 0;
+}
+
+void cp_default_raster_config(cp_raster_config* rc) {
+    std::memset(rc, 0, sizeof(*rc));
+    rc->width = 50;        // --render-width, bullet_cartpole.py:35
+    rc->height = 50;       // --render-height, :37
+    rc->num_cameras = 1;   // --num-cameras, :27
+    const float temp = 0.75f;  // :278-279
+    rc->eye[0][0] = 0.0f; rc->eye[0][1] = temp; rc->eye[0][2] = temp;
+    rc->eye[1][0] = temp; rc->eye[1][1] = 0.0f; rc->eye[1][2] = temp;
+    rc->target[0] = 0.0f; rc->target[1] = 0.0f; rc->target[2] = 0.3f;  // :280
+    rc->up[0] = 0.0f; rc->up[1] = 0.0f; rc->up[2] = 1.0f;              // :281
+    rc->tan_half_fov = (float)std::tan(0.5 * 30.0 * 3.141592653589793 / 180.0);  // fov 30, :283
+    rc->far_plane = 20.0f;                                             // :282
+    // light from above and in front of camera 0 (unpinned: TinyRenderer's is not available)
+    const double l[3] = {0.3, 0.5, 1.0};
+    const double ln = std::sqrt(l[0] * l[0] + l[1] * l[1] + l[2] * l[2]);
+    for (int k = 0; k < 3; ++k) rc->light[k] = (float)(l[k] / ln);
+    rc->ambient = 0.6f;
+    rc->diffuse = 0.4f;
+    rc->background[0] = 1.0f; rc->background[1] = 1.0f; rc->background[2] = 1.0f;
+    static const float col[5][3] = {{0.3f, 0.3f, 0.0f},   // ground.urdf:15
+                                    {0.9f, 0.2f, 0.1f},   // cart.urdf:25
+                                    {0.2f, 0.7f, 0.1f},   // pole.urdf:30
+                                    {0.2f, 0.9f, 0.1f},   // cart2.urdf:25
+                                    {0.7f, 0.2f, 0.7f}};  // pole2.urdf:24
+    std::memcpy(rc->color, col, sizeof(col));
+}
+
+int cp_set_raster(cp_handle* h, const cp_raster_config* rc, uint16_t* pixels_out) {
+    if (!h) return fail(h, "cp_set_raster: null handle");
+    CP_TRY(h, hipSetDevice(h->device));
+    if (!pixels_out) {
+        h->pixels = nullptr;
+        (void)hipFree(h->b.rposes);
+        (void)hipFree(h->b.rlist);
+        (void)hipFree(h->b.rcount);
+        h->b.rposes = nullptr;
+        h->b.rlist = h->b.rcount = nullptr;
+        return 0;
+    }
+    if (!rc) return fail(h, "cp_set_raster: null config");
+    const int R = h->cfg.action_repeats;
+    if (rc->width <= 0 || rc->height <= 0 || rc->width > 4096 || rc->height > 4096)
+        return fail(h, "cp_set_raster: width and height must be in 1..4096");
+    if (rc->num_cameras != 1 && rc->num_cameras != 2) return fail(h, "--num-cameras must be 1 or 2");
+    if (rc->num_cameras * R > cp::RMAX_FRAMES)
+        return fail(h, "cp_set_raster: num_cameras * action_repeats must be <= 16");
+    h->raster = *rc;
+    h->pixels = pixels_out;
+    if (!h->b.rposes) {
+        const size_t B = (size_t)h->cfg.num_envs;
+        hipError_t e = hipMalloc((void**)&h->b.rposes, B * R * CP_NUM_DYN * 7 * sizeof(float));
+        if (e == hipSuccess) e = hipMalloc((void**)&h->b.rlist, B * sizeof(int32_t));
+        if (e == hipSuccess) e = hipMalloc((void**)&h->b.rcount, sizeof(int32_t));
+        if (e != hipSuccess) {
+            (void)hipFree(h->b.rposes);
+            (void)hipFree(h->b.rlist);
+            h->b.rposes = nullptr;
+            h->b.rlist = nullptr;
+            h->pixels = nullptr;
+            return check(h, e, "cp_set_raster: hipMalloc");
+        }
+    }
     return 0;
 }
 

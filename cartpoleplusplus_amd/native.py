@@ -17,7 +17,7 @@ EXPORTS = (
     "cp_default_config", "cp_create", "cp_destroy", "cp_last_error", "cp_abi_version",
     "cp_reset", "cp_step", "cp_set_readback", "cp_set_bump_forces", "cp_get_state",
     "cp_set_state", "cp_episode_returns", "cp_overflow_counts", "cp_timing_begin", "cp_timing_end",
-    "cp_debug_stamps",
+    "cp_debug_stamps", "cp_default_raster_config", "cp_set_raster", "cp_timing_render",
 )
 
 _lib = None
@@ -56,6 +56,9 @@ def load():
         "cp_timing_begin": (I, [VP, I]),
         "cp_debug_stamps": (I, [VP, P(C.c_uint64), I]),
         "cp_timing_end": (I, [VP, P(C.c_double), P(C.c_int32), P(C.c_double), P(C.c_int32)]),
+        "cp_default_raster_config": (None, [P(abi.cp_raster_config)]),
+        "cp_set_raster": (I, [VP, P(abi.cp_raster_config), VP]),
+        "cp_timing_render": (I, [VP, P(C.c_double), P(C.c_int32)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -64,6 +67,17 @@ def load():
         raise CartpoleError("libcartpole_hip.so ABI version mismatch; rebuild it")
     _lib = lib
     return lib
+
+
+def default_raster_config(**overrides):
+    """cp_raster_config with the reference defaults (bullet_cartpole.py:27-37, :277-284)."""
+    rc = abi.cp_raster_config()
+    load().cp_default_raster_config(C.byref(rc))
+    for k, v in overrides.items():
+        if not hasattr(rc, k):
+            raise AttributeError(f"cp_raster_config has no field {k!r}")
+        setattr(rc, k, v)
+    return rc
 
 
 def default_config(**overrides):

@@ -25,6 +25,8 @@
  *   reward        float32 [B]            (1.0 per step, bullet_cartpole.py:260)
  *   done          uint8   [B]
  *   state (get/set) float32 [CP_STATE_FIELDS][B]  (SoA; see CP_SF_* below)
+ *   pixels        float16 [B][H][W][3][C][R]  raster obs (--use-raw-pixels,
+ *                 bullet_cartpole.py:277-306; cp_set_raster)
  */
 #ifndef CARTPOLE_AMD_H
 #define CARTPOLE_AMD_H
@@ -187,7 +189,7 @@ int cp_set_state(cp_handle* h, const float* state_in, void* stream);
  * either pointer may be NULL.  Feeds the RCCL return histogram. */
 int cp_episode_returns(cp_handle* h, float* returns_out, int32_t* lengths_out, void* stream);
 
-/* Diagnostics: per-env count of contact rows dropped by the CP_MAX_* caps since
+/* Diagnostics: per-env count of contact rows dropped by the CP_ISLAND_* caps since
  * creation (int32 [B], device).  0 everywhere in normal operation. */
 int cp_overflow_counts(cp_handle* h, int32_t* out, void* stream);
 
@@ -206,6 +208,43 @@ int cp_timing_end(cp_handle* h, double* step_ms, int32_t* step_launches, double*
  * substep count, total kernel cycles, waves.  Synchronises the device.  Returns 1
  * in a stamp build, 0 otherwise (counters then stay 0). */
 int cp_debug_stamps(cp_handle* h, uint64_t* out8, int reset);
+
+/* ---- Raster observation (--use-raw-pixels) ----------
+ * Replaces render_rgb + set_state_element_for_repeat (bullet_cartpole.py:277-306):
+ * per env, per repeat r and camera c, an RGB image of the scene from the
+ * reference's cameras, converted as the reference converts TinyRenderer's
+ * uint8 RGBA: float16(uint8) / 255 in float16 (:289-294).  The image is ray cast
+ * (DESIGN.md §Raster): flat-shaded boxes with the URDF colours; pixel parity with
+ * pybullet's TinyRenderer is unpinned (no pybullet here), the oracle's
+ * restatement of this renderer is pinned bit for bit. */
+typedef struct cp_raster_config {
+    int32_t width, height;     /* --render-width / --render-height (50, 50)          */
+    int32_t num_cameras;       /* --num-cameras, 1 or 2 (:111-114)                   */
+    float eye[2][3];           /* camera positions, (0,.75,.75) and (.75,0,.75) :279 */
+    float target[3];           /* (0, 0, 0.3) :280                                    */
+    float up[3];               /* (0, 0, 1) :281                                      */
+    float tan_half_fov;        /* tan(fov/2), fov = 30 deg vertical (:283)            */
+    float far_plane;           /* 20 (:282); rays stop there (near plane: DESIGN.md)  */
+    float light[3];            /* unit direction towards the light                   */
+    float ambient, diffuse;    /* shade = ambient + diffuse * max(0, n . light)       */
+    float background[3];       /* colour of a ray that hits nothing                  */
+    float color[CP_NUM_BODIES][3]; /* visual RGB of ground, cart, pole, cart2, pole2  */
+} cp_raster_config;
+
+/* Reference defaults (bullet_cartpole.py:15-40, :277-284, the models/ URDF colours). */
+void cp_default_raster_config(cp_raster_config* rc);
+
+/* Enable (pixels_out != NULL) or disable the raster obs.  When enabled, every
+ * later cp_step renders the R repeat-end frames of each simulated env into
+ * pixels_out float16 [B][H][W][3][C][R] (device), and cp_reset renders the reset
+ * envs' first frame into all R slots.  Envs that are done before a step keep
+ * their pixels (the last obs, :179-181).  With autoreset, a finishing env's
+ * pixels hold the new episode's first frame (its terminal frame is not kept). */
+int cp_set_raster(cp_handle* h, const cp_raster_config* rc, uint16_t* pixels_out);
+
+/* Timing of the render kernel launches (one per cp_step / cp_reset with raster on)
+ * of the last cp_timing_begin .. cp_timing_end window: summed ms and launch count. */
+int cp_timing_render(cp_handle* h, double* render_ms, int32_t* render_launches);
 
 #ifdef __cplusplus
 }

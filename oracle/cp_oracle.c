@@ -170,6 +170,94 @@ static void quat_euler(const real q[4], real rpy[3]) {
 }
 
 /* ------------------------------------------------------------------ Philox */
+
+/* --------------------------------------------------------------- raster obs */
+/* Restatement of the kernel's ray caster (cartpoleplusplus_amd/csrc/cp_raster.h),
+ * which stands in for bullet_cartpole.py:277-296 (render_rgb: TinyRenderer through
+ * p.renderImage, not available here).  Same fp32 operations in the same order. */
+static int raster_u8(real x) {
+    x = x > RC(1) ? RC(1) : (x < RC(0) ? RC(0) : x);
+    return (int)(x * RC(255) + RC(0.5));
+}
+static int ray_box(v3 eye, v3 d, v3 cc, const v3 ax[3], const real h[3], real* t, int* axis, real* sgn) {
+    v3 oc = sub(eye, cc);
+    real lo[3], hi[3], dd[3];
+    for (int i = 0; i < 3; ++i) {
+        real o = dot(oc, ax[i]);
+        dd[i] = dot(d, ax[i]);
+        real inv = RC(1) / dd[i];
+        real t1 = (-h[i] - o) * inv, t2 = (h[i] - o) * inv;
+        int lt = t1 < t2;
+        lo[i] = lt ? t1 : t2;
+        hi[i] = lt ? t2 : t1;
+    }
+    real tmin = lo[0];
+    int a = 0;
+    if (lo[1] > tmin) { tmin = lo[1]; a = 1; }
+    if (lo[2] > tmin) { tmin = lo[2]; a = 2; }
+    real tmax = hi[0] < hi[1] ? hi[0] : hi[1];
+    tmax = tmax < hi[2] ? tmax : hi[2];
+    *t = tmin;
+    *axis = a;
+    *sgn = dd[a] > RC(0) ? RC(-1) : RC(1);
+    return tmin <= tmax && tmin > RC(0);
+}
+/* One frame of camera `cam` for the body poses pose[d] = (xyz, quat xyzw) of
+ * cart, pole, cart2, pole2: rgb uint8 [H][W][3]. */
+void orc_render_frame(const cp_raster_config* rc, const cp_physics* P, const float pose[4][7], int cam,
+                      uint8_t* rgb) {
+    const int W = rc->width, H = rc->height;
+    v3 eye = mk((real)rc->eye[cam][0], (real)rc->eye[cam][1], (real)rc->eye[cam][2]);
+    v3 F = sub(mk((real)rc->target[0], (real)rc->target[1], (real)rc->target[2]), eye);
+    real lf = SQRT(dot(F, F));
+    v3 f = mk(F.x / lf, F.y / lf, F.z / lf);
+    v3 rr = cross(f, mk((real)rc->up[0], (real)rc->up[1], (real)rc->up[2]));
+    real lr = SQRT(dot(rr, rr));
+    v3 r = mk(rr.x / lr, rr.y / lr, rr.z / lr);
+    v3 u = cross(r, f);
+    const real syk = (real)rc->tan_half_fov;
+    const real sxk = (real)rc->tan_half_fov * ((real)W / (real)H);
+    v3 bc[CP_NUM_BODIES], bax[CP_NUM_BODIES][3];
+    real bh[CP_NUM_BODIES][3];
+    bc[0] = mk(RC(0), RC(0), RC(0));
+    bax[0][0] = mk(RC(1), RC(0), RC(0)); bax[0][1] = mk(RC(0), RC(1), RC(0)); bax[0][2] = mk(RC(0), RC(0), RC(1));
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        real q[4] = {pose[d][3], pose[d][4], pose[d][5], pose[d][6]};
+        bc[d + 1] = mk(pose[d][0], pose[d][1], pose[d][2]);
+        quat_axes(q, bax[d + 1]);
+    }
+    for (int b = 0; b < CP_NUM_BODIES; ++b)
+        for (int k = 0; k < 3; ++k) bh[b][k] = (real)P->half_extents[b][k];
+    v3 light = mk((real)rc->light[0], (real)rc->light[1], (real)rc->light[2]);
+    for (int py = 0; py < H; ++py) {
+        for (int px = 0; px < W; ++px) {
+            real sx = ((RC(2) * ((real)px + RC(0.5))) / (real)W - RC(1)) * sxk;
+            real sy = (RC(1) - (RC(2) * ((real)py + RC(0.5))) / (real)H) * syk;
+            v3 d = mk(FMA(sy, u.x, FMA(sx, r.x, f.x)), FMA(sy, u.y, FMA(sx, r.y, f.y)), FMA(sy, u.z, FMA(sx, r.z, f.z)));
+            real best = (real)rc->far_plane;
+            int hit = -1;
+            v3 n = mk(RC(0), RC(0), RC(1));
+            for (int b = 0; b < CP_NUM_BODIES; ++b) {
+                real t, sg;
+                int ax;
+                if (ray_box(eye, d, bc[b], bax[b], bh[b], &t, &ax, &sg) && t < best) {
+                    best = t;
+                    hit = b;
+                    n = scl(bax[b][ax], sg);
+                }
+            }
+            uint8_t* o = rgb + ((size_t)py * W + px) * 3;
+            if (hit < 0) {
+                for (int c = 0; c < 3; ++c) o[c] = (uint8_t)raster_u8((real)rc->background[c]);
+                continue;
+            }
+            real ndl = dot(n, light);
+            real sh = FMA((real)rc->diffuse, ndl > RC(0) ? ndl : RC(0), (real)rc->ambient);
+            for (int c = 0; c < 3; ++c) o[c] = (uint8_t)raster_u8((real)rc->color[hit][c] * sh);
+        }
+    }
+}
+
 void orc_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
     uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
     uint32_t k0 = key_in[0], k1 = key_in[1];

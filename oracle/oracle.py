@@ -74,6 +74,7 @@ def load(precision="f32"):
         "orc_envs_step_omp": (C.c_int, [VP, VP, C.c_int, VP, VP, VP, C.c_int]),
         "orc_envs_episode_returns": (None, [VP, VP, VP]),
         "orc_envs_sweeps": (None, [VP, VP]),
+        "orc_render_frame": (None, [VP, VP, VP, C.c_int, VP]),
         "orc_philox4x32_10": (None, [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]),
         "orc_sincos_turns": (None, [C.c_float, P(C.c_float), P(C.c_float)]),
         "orc_sizeof_real": (C.c_int, []),
@@ -217,6 +218,24 @@ class Envs:
         out = np.zeros((self.B, 2), np.int32)
         self.lib.orc_envs_sweeps(self.h, _ptr(out))
         return out
+
+
+def render_frame(raster_cfg, phys, poses, cam, precision="f32"):
+    """One frame (H, W, 3) uint8 of camera `cam` for poses (4, 7) = (xyz, quat xyzw) of
+    cart, pole, cart2, pole2 (the kernel's ray caster, restated)."""
+    lib = load(precision)
+    p = np.ascontiguousarray(poses, dtype=np.float32).reshape(4, 7)
+    out = np.zeros((raster_cfg.height, raster_cfg.width, 3), np.uint8)
+    lib.orc_render_frame(C.byref(raster_cfg), C.byref(phys), _ptr(p), int(cam), _ptr(out))
+    return out
+
+
+def u8_to_f16(u8):
+    """The reference's conversion of TinyRenderer bytes (bullet_cartpole.py:289-294):
+    float16(uint8), then /= 255 in float16 (numpy: float32 divide, round to half)."""
+    a = np.asarray(u8, dtype=np.float16)
+    a /= 255
+    return a
 
 
 def philox4x32_10(ctr, key):

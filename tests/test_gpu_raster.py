@@ -1,0 +1,127 @@
+"""Raster obs on the MI355X: the render kernel's float16 pixels vs the
+oracle's ray caster on the same poses, bit for bit, through the C-ABI.
+
+The poses come from the GPU env itself (get_state after the call: the last repeat's
+frame; after a reset every repeat slot holds the reset frame).  The conversion to
+float16 is the reference's (bullet_cartpole.py:289-294), restated in oracle.u8_to_f16."""
+import numpy as np
+import pytest
+import torch
+
+from cartpoleplusplus_amd import abi, native
+from cartpoleplusplus_amd.batched import BatchedCartpole
+
+pytestmark = pytest.mark.gpu
+
+
+def _poses(state, e):
+    out = np.zeros((4, 7), np.float32)
+    for d in range(4):
+        out[d] = state[abi.CP_SF_BODY(d, 0):abi.CP_SF_BODY(d, 0) + 7, e]
+    return out
+
+
+def _expect(O, rc, phys, state, e, cam):
+    return O.u8_to_f16(O.render_frame(rc, phys, _poses(state, e), cam)).view(np.uint16)
+
+
+def _check_env(O, env, pix, state, e, r):
+    rc = env.raster_cfg
+    for cam in range(rc.num_cameras):
+        got = pix[e, :, :, :, cam, r].view(np.uint16)
+        exp = _expect(O, rc, env.cfg.phys, state, e, cam)
+        if not np.array_equal(got, exp):
+            bad = np.argwhere(got != exp)
+            raise AssertionError(f"env {e} cam {cam} repeat {r}: {len(bad)} channel values differ, first {bad[:3]}")
+
+
+def test_reset_frames_bitexact(oracle_mod):
+    env = BatchedCartpole(40, 0, action_repeats=3, initial_force=55.0, seed=3)
+    env.enable_raster(True, num_cameras=2)
+    env.reset()
+    pix = env.pixels.cpu().numpy()
+    st = env.get_state().cpu().numpy()
+    assert pix.shape == (40, 50, 50, 3, 2, 3) and pix.dtype == np.float16
+    for e in range(0, 40, 7):
+        for r in range(3):
+            _check_env(oracle_mod, env, pix, st, e, r)
+
+
+@pytest.mark.parametrize("R,C", [(3, 1), (1, 2)])
+def test_step_frames_bitexact(oracle_mod, R, C):
+    B = 48
+    env = BatchedCartpole(B, 0, action_repeats=R, initial_force=55.0, seed=11)
+    env.enable_raster(True, num_cameras=C)
+    env.reset()
+    rng = np.random.default_rng(1)
+    for t in range(25):
+        a = torch.from_numpy(rng.uniform(-1, 1, (B, 2, 2)).astype(np.float32)).cuda()
+        env.step(a)
+        if t % 8 == 7:
+            pix = env.pixels.cpu().numpy()
+            st = env.get_state().cpu().numpy()
+            for e in range(0, B, 5):
+                _check_env(oracle_mod, env, pix, st, e, R - 1)
+
+
+def test_other_sizes_and_done_envs_keep_pixels(oracle_mod):
+    """A 37 x 23 image (odd pixel count: the 2-byte copy path), and an env that is done
+    before the step keeps its pixels (bullet_cartpole.py:179-181)."""
+    B = 10
+    env = BatchedCartpole(B, 0, action_repeats=1, initial_force=55.0, seed=5, max_episode_len=3)
+    env.enable_raster(True, width=37, height=23)
+    env.reset()
+    act = torch.zeros((B, 2, 2), device="cuda")
+    for _ in range(3):
+        env.step(act)
+    assert env.done.all()
+    before = env.pixels.clone()
+    st = env.get_state().cpu().numpy()
+    _check_env(oracle_mod, env, env.pixels.cpu().numpy(), st, 4, 0)
+    env.step(act)
+    assert torch.equal(before, env.pixels)
+
+
+def test_wide_image_row_major_path(oracle_mod):
+    """100 x 20 x 2 cameras x 3 repeats does not fit the 8-row band staging: the
+    kernel's row-major chunk path."""
+    env = BatchedCartpole(6, 0, action_repeats=3, initial_force=55.0, seed=9)
+    env.enable_raster(True, width=100, height=20, num_cameras=2)
+    env.reset()
+    env.step(torch.zeros((6, 2, 2), device="cuda"))
+    pix = env.pixels.cpu().numpy()
+    st = env.get_state().cpu().numpy()
+    for e in range(6):
+        _check_env(oracle_mod, env, pix, st, e, 2)
+
+
+def test_autoreset_frames_show_the_new_episode(oracle_mod):
+    B = 32
+    env = BatchedCartpole(B, 0, action_repeats=2, initial_force=55.0, seed=8, autoreset=True, max_episode_len=4)
+    env.enable_raster(True)
+    env.reset()
+    a = torch.zeros((B, 2), dtype=torch.int8, device="cuda")
+    for t in range(4):
+        env.step(a)
+    assert env.done.all()
+    pix = env.pixels.cpu().numpy()
+    st = env.get_state().cpu().numpy()
+    for e in range(0, B, 6):
+        for r in range(2):
+            _check_env(oracle_mod, env, pix, st, e, r)
+
+
+def test_gym_mirror_raw_pixels():
+    import argparse
+    from cartpoleplusplus_amd import bullet_cartpole as bc
+    p = argparse.ArgumentParser()
+    bc.add_opts(p)
+    opts = p.parse_args(["--use-raw-pixels", "--num-cameras", "2", "--action-repeats", "3"])
+    env = bc.BulletCartpole(opts, discrete_actions=True)
+    s = env.reset()
+    assert s.shape == (50, 50, 3, 2, 3) and s.dtype == np.float32
+    assert env.observation_space.shape == (50, 50, 3, 2, 3)
+    assert np.array_equal(s[..., 0], s[..., 2])           # every repeat slot: the reset frame
+    assert 0.0 <= s.min() and s.max() <= 1.0
+    s2, r, d, _ = env.step([1, 2])
+    assert s2.shape == s.shape and r == 1.0 and not d

@@ -11,7 +11,7 @@ STEPS=${STEPS:-200}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-B="python3 $R/bench.py --steps $STEPS --warmup 5 --no-cpu-baseline"
+B="python3 $R/bench.py --steps $STEPS --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-}"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- $B > "$OUT/trace.json" 2> "$OUT/trace.err"
 timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/sq" -o run \
     --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU \

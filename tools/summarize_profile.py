@@ -18,7 +18,7 @@ from collections import defaultdict
 def kernel_key(name):
     if "cp_step_kernel" in name:
         return "cp_step_kernel<discrete>" if "<1>" in name else "cp_step_kernel<continuous>"
-    for k in ("cp_reset_kernel", "cp_init_kernel", "cp_mask_to_list_kernel"):
+    for k in ("cp_reset_kernel", "cp_init_kernel", "cp_mask_to_list_kernel", "cp_render_kernel"):
         if k in name:
             return k
     return None
