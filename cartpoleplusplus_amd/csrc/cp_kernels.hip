@@ -50,6 +50,7 @@ struct Bufs {
     float* scratch;    // [4*CP_ISLAND_PAIRS][2B] manifold headers of the current substep, per lane
     uint64_t* stamps;  // [waves][8] diagnostic phase cycles (CP_STAMPS builds only)
     float* rposes;     // [B][R][4][7] repeat-end poses for the raster obs (NULL: raster off)
+    float4* rtable;    // [C][H*W][2] per-camera ray directions + ground hits (cp_raster_table_kernel)
     int32_t* rlist;    // [B] envs to render after the step kernel
     int32_t* rcount;   // [1]
 };
@@ -604,6 +605,7 @@ void cp_destroy(cp_handle* h) {
     (void)hipFree(h->b.rposes);
     (void)hipFree(h->b.rlist);
     (void)hipFree(h->b.rcount);
+    (void)hipFree(h->b.rtable);
     delete h;
 }
 
@@ -612,7 +614,7 @@ static int launch_render(cp_handle* h, const int32_t* list, const int32_t* count
     hipEvent_t* ev = timing_slot(h, 2);
     if (ev) CP_TRY(h, hipEventRecord(ev[0], st));
     hipLaunchKernelGGL(cp::cp_render_kernel, dim3((unsigned)h->cfg.num_envs), dim3(cp::RT), 0, st, h->raster,
-                       h->cfg.phys, h->cfg.action_repeats, list, count, h->b.rposes, h->pixels);
+                       h->cfg.phys, h->cfg.action_repeats, list, count, h->b.rposes, h->b.rtable, h->pixels);
     if (check(h, hipGetLastError(), "cp_render_kernel")) return -1;
     if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
     return 0;
@@ -809,8 +811,10 @@ int cp_set_raster(cp_handle* h, const cp_raster_config* rc, uint16_t* pixels_out
         (void)hipFree(h->b.rposes);
         (void)hipFree(h->b.rlist);
         (void)hipFree(h->b.rcount);
+        (void)hipFree(h->b.rtable);
         h->b.rposes = nullptr;
         h->b.rlist = h->b.rcount = nullptr;
+        h->b.rtable = nullptr;
         return 0;
     }
     if (!rc) return fail(h, "cp_set_raster: null config");
@@ -836,6 +840,15 @@ int cp_set_raster(cp_handle* h, const cp_raster_config* rc, uint16_t* pixels_out
             return check(h, e, "cp_set_raster: hipMalloc");
         }
     }
+    // per-camera ray table for this configuration (synchronous: a setup call)
+    (void)hipFree(h->b.rtable);
+    h->b.rtable = nullptr;
+    const int npx = rc->width * rc->height;
+    CP_TRY(h, hipMalloc((void**)&h->b.rtable, (size_t)rc->num_cameras * npx * 2 * sizeof(float4)));
+    hipLaunchKernelGGL(cp::cp_raster_table_kernel, dim3(grid_for(npx, cp::RT), rc->num_cameras), dim3(cp::RT), 0, 0,
+                       h->raster, h->cfg.phys, h->b.rtable);
+    CP_TRY(h, hipGetLastError());
+    CP_TRY(h, hipDeviceSynchronize());
     return 0;
 }
 

@@ -6,10 +6,12 @@
 //
 // One 256-thread block per env (taken from a compacted env list).  The block
 // stages the env's R poses and the cameras in LDS, projects every box to a
-// conservative screen rectangle per (camera, repeat), then each thread ray casts
-// its pixels for all C x R frames and writes the 3*C*R halves of a pixel
-// contiguously; a 256-pixel chunk is staged in LDS and stored with 4-byte stores,
-// so the image goes to HBM in full lines (the kernel is HBM-write bound).
+// conservative screen rectangle per (camera, repeat) and tabulates the shaded
+// colour of every face; the per-pixel ray directions and the static ground's hits
+// come from a per-camera table built once (cp_raster_table_kernel).  Each wave
+// renders an 8 x 8 pixel tile (a thin pole's rectangle diverges few waves) for all
+// C x R frames; an 8-row band is staged in LDS in the reference's pixel order and
+// stored with 4-byte stores.
 //
 // The per-pixel arithmetic is the oracle's (oracle/cp_oracle.c, raster section),
 // operation for operation; the rectangles only skip boxes a ray cannot hit.
@@ -122,16 +124,48 @@ CP_DEV bool ray_box_o(V3 d, const float o[3], const Axes& A, V3 h, float& t, int
     return tmin <= tmax && tmin > 0.0f;
 }
 
+// Per camera and pixel, the ray direction and the static ground's hit: the same for
+// every env, computed once per raster configuration (cp_set_raster) with the render
+// kernel's own arithmetic.  table [C][H*W][2] float4: (d.xyz, t_ground), (hit, face).
+__global__ void __launch_bounds__(RT) cp_raster_table_kernel(cp_raster_config rc, cp_physics P, float4* table) {
+    const int W = rc.width, H = rc.height, npx = W * H;
+    const int p = blockIdx.x * RT + threadIdx.x, cam = blockIdx.y;
+    if (p >= npx) return;
+    const Cam k = make_cam(rc, cam);
+    const float syk = rc.tan_half_fov;
+    const float sxk = rc.tan_half_fov * ((float)W / (float)H);
+    const int py = p / W, px = p - py * W;
+    const float sx = ((2.0f * ((float)px + 0.5f)) / (float)W - 1.0f) * sxk;
+    const float sy = (1.0f - (2.0f * ((float)py + 0.5f)) / (float)H) * syk;
+    const V3 d = mk(fmaf_(sy, k.u.x, fmaf_(sx, k.r.x, k.f.x)), fmaf_(sy, k.u.y, fmaf_(sx, k.r.y, k.f.y)),
+                    fmaf_(sy, k.u.z, fmaf_(sx, k.r.z, k.f.z)));
+    const Axes I3 = {mk(1.0f, 0.0f, 0.0f), mk(0.0f, 1.0f, 0.0f), mk(0.0f, 0.0f, 1.0f)};
+    const V3 oc = sub(k.eye, mk(0.0f, 0.0f, 0.0f));
+    const float o[3] = {dot(oc, I3.a0), dot(oc, I3.a1), dot(oc, I3.a2)};
+    float best = rc.far_plane;
+    int hit = -1, face = 0;
+    float t, sg;
+    int ax;
+    if (ray_box_o(d, o, I3, mk(P.half_extents[0][0], P.half_extents[0][1], P.half_extents[0][2]), t, ax, sg) &&
+        t < best) {
+        best = t;
+        hit = 0;
+        face = ax * 2 + (sg > 0.0f ? 1 : 0);
+    }
+    table[((size_t)cam * npx + p) * 2 + 0] = make_float4(d.x, d.y, d.z, best);
+    table[((size_t)cam * npx + p) * 2 + 1] = make_float4(__int_as_float(hit), __int_as_float(face), 0.0f, 0.0f);
+}
+
 // poses [B][R][4][7] (xyz, quat xyzw) -> pixels float16 [B][H][W][3][C][R] for the envs
 // in list[0 .. *count).  Per pixel and camera the ground (static) is tested once and
 // reused for every repeat; per (camera, repeat, body) the ray-independent terms are
 // precomputed in LDS.  The oracle evaluates the same expressions per frame, so the
 // images agree bit for bit.
 __global__ void __launch_bounds__(RT) cp_render_kernel(cp_raster_config rc, cp_physics P, int R, const int32_t* list,
-                                                        const int32_t* count, const float* poses, uint16_t* pixels) {
+                                                        const int32_t* count, const float* poses, const float4* table,
+                                                        uint16_t* pixels) {
     __shared__ Scene sc;
     __shared__ float oloc[2][RMAX_FRAMES][CP_NUM_DYN][3];  // (eye - c) . a_i per camera, repeat, body
-    __shared__ float gorig[2][3];                          // the same for the ground (identity axes)
     __shared__ uint16_t lut[256];                          // u8 -> float16 bits (:289-294)
     // shaded colour of every face: [repeat][box][axis * 2 + (sign > 0)][channel] as float16
     // bits (flat shading depends on the face only; same arithmetic as per pixel)
@@ -175,12 +209,6 @@ __global__ void __launch_bounds__(RT) cp_render_kernel(cp_raster_config rc, cp_p
             oloc[cam][r][b - 1][1] = dot(oc, A.a1);
             oloc[cam][r][b - 1][2] = dot(oc, A.a2);
         }
-        if (b == 0 && r == 0) {
-            const V3 oc = sub(k.eye, cc);
-            gorig[cam][0] = dot(oc, A.a0);
-            gorig[cam][1] = dot(oc, A.a1);
-            gorig[cam][2] = dot(oc, A.a2);
-        }
         box_rect(k, cc, A, mk(P.half_extents[b][0], P.half_extents[b][1], P.half_extents[b][2]), sxk, syk, W, H,
                  sc.rect[cam][r][b]);
     }
@@ -205,8 +233,6 @@ __global__ void __launch_bounds__(RT) cp_render_kernel(cp_raster_config rc, cp_p
     __syncthreads();
     const uint16_t bgh0 = lut[to_u8(rc.background[0])], bgh1 = lut[to_u8(rc.background[1])],
                    bgh2 = lut[to_u8(rc.background[2])];
-    const Axes I3 = {mk(1.0f, 0.0f, 0.0f), mk(0.0f, 1.0f, 0.0f), mk(0.0f, 0.0f, 1.0f)};
-    const V3 hg = mk(P.half_extents[0][0], P.half_extents[0][1], P.half_extents[0][2]);
     const int npx = W * H;
     uint16_t* out = pixels + (size_t)env * npx * per_px;
     const bool words = (npx * per_px) % 2 == 0 && ((size_t)env * npx * per_px) % 2 == 0;
@@ -214,26 +240,13 @@ __global__ void __launch_bounds__(RT) cp_render_kernel(cp_raster_config rc, cp_p
     // all C x R frames of pixel (px, py) -> dst[(ch * C + cam) * R + r] (the reference's
     // (3, C, R) order within a pixel)
     auto render_px = [&](int px, int py, uint64_t near, uint16_t* dst) {
-        const float sx = ((2.0f * ((float)px + 0.5f)) / (float)W - 1.0f) * sxk;
-        const float sy = (1.0f - (2.0f * ((float)py + 0.5f)) / (float)H) * syk;
         for (int cam = 0; cam < C; ++cam) {
-            const Cam k = sc.cam[cam];
-            const V3 d = mk(fmaf_(sy, k.u.x, fmaf_(sx, k.r.x, k.f.x)), fmaf_(sy, k.u.y, fmaf_(sx, k.r.y, k.f.y)),
-                            fmaf_(sy, k.u.z, fmaf_(sx, k.r.z, k.f.z)));
-            // the static ground, once for all repeats (inside its rectangle)
-            float best0 = rc.far_plane;
-            int hit0 = -1, face0 = 0;
-            {
-                const int16_t* rect = sc.rect[cam][0][0];
-                float t, sg;
-                int ax;
-                if (!(px < rect[0] || px > rect[1] || py < rect[2] || py > rect[3]) &&
-                    ray_box_o(d, gorig[cam], I3, hg, t, ax, sg) && t < best0) {
-                    best0 = t;
-                    hit0 = 0;
-                    face0 = ax * 2 + (sg > 0.0f ? 1 : 0);
-                }
-            }
+            // ray direction and the static ground's hit, from the per-camera table
+            const float4 t0 = table[((size_t)cam * npx + py * W + px) * 2 + 0];
+            const float4 t1 = table[((size_t)cam * npx + py * W + px) * 2 + 1];
+            const V3 d = mk(t0.x, t0.y, t0.z);
+            const float best0 = t0.w;
+            const int hit0 = __float_as_int(t1.x), face0 = __float_as_int(t1.y);
             for (int r = 0; r < R; ++r) {
                 float best = best0;
                 int hit = hit0, fc = face0;
