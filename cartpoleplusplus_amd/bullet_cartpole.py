@@ -77,8 +77,11 @@ class BulletCartpole(Env):
         self.random_theta = not opts.no_random_theta
         self.discrete_actions = discrete_actions
         self.action_space = Discrete(5) if discrete_actions else Box(-1.0, 1.0, shape=(1, 2))
-        if opts.event_log_out:
-            raise NotImplementedError("--event-log-out: the protobuf event log is not ported yet (DESIGN.md §Scope)")
+        if opts.event_log_out:  # :97-100 (protobuf wire format, cartpoleplusplus_amd/event_log.py)
+            from . import event_log
+            self.event_log = event_log.EventLog(opts.event_log_out, opts.use_raw_pixels)
+        else:
+            self.event_log = None
         self.repeats = opts.action_repeats
         self.steps_per_repeat = opts.steps_per_repeat
         if opts.num_cameras not in (1, 2):
@@ -131,6 +134,9 @@ class BulletCartpole(Env):
             draw_bump_forces(self.initial_force, self.random_theta, self.initial_force_steps)[None])
         obs = self._env.reset()
         self._capture(obs)
+        if self.event_log:  # :342-344
+            self.event_log.reset()
+            self.event_log.add_just_state(self.state)
         return np.copy(self.state)
 
     def step(self, action):
@@ -159,4 +165,6 @@ class BulletCartpole(Env):
             info['done_reason'] = 'episode length'
             self.done = True
         reward = 1.0
+        if self.event_log:  # :272-273; a 2-cart action is logged flattened (the fork's assert on
+            self.event_log.add(self.state, action, reward)  # action.shape[0] == 1 cannot hold)
         return np.copy(self.state), reward, self.done, info

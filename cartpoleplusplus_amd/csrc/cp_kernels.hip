@@ -53,6 +53,7 @@ struct Bufs {
     float4* rtable;    // [C][H*W][2] per-camera ray directions + ground hits (cp_raster_table_kernel)
     int32_t* rlist;    // [B] envs to render after the step kernel
     int32_t* rcount;   // [1]
+    uint8_t* stepped;  // [B] 1 = simulated by the last cp_step (event log: done-before envs are not logged)
 };
 
 // raster obs: the repeat-end pose of the 4 bodies (xyz, quat xyzw) for the render kernel
@@ -306,7 +307,9 @@ __global__ void CP_PHYS_ATTR cp_step_kernel(cp_config cfg, Bufs b, const void* a
         const Lane L = Lane::make(isl, cfg.phys);
         const Soa term = Soa::make(b.term_obs, B, R * 14);
         float* obs = obs_out + (size_t)i * R * 14;
-        if (ldi(G.st, CP_SF_DONE, G.off)) {  // step after done (bullet_cartpole.py:179-181)
+        const bool was_done = ldi(G.st, CP_SF_DONE, G.off) != 0;
+        if (lead) b.stepped[i] = was_done ? 0 : 1;
+        if (was_done) {  // step after done (bullet_cartpole.py:179-181)
             if (lead) {
                 for (int f = 0; f < R * 14; ++f) obs[f] = term.ld(f, G.off);
                 reward_out[i] = 0.0f;
@@ -400,6 +403,79 @@ __global__ void CP_PHYS_ATTR cp_step_kernel(cp_config cfg, Bufs b, const void* a
         base = __shfl(base, 0);
         if (render_me) b.rlist[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
     }
+}
+
+// ---------------------------------------------------------------------------
+// Event log records (protobuf wire format of event.proto; see cp_encode_events).
+CP_DEV void put_u8(uint8_t*& p, uint32_t v) { *p++ = (uint8_t)v; }
+CP_DEV void put_varint(uint8_t*& p, uint32_t v) {
+    while (v >= 0x80u) { put_u8(p, (v & 0x7Fu) | 0x80u); v >>= 7; }
+    put_u8(p, v);
+}
+CP_DEV void put_f32(uint8_t*& p, uint32_t key, float x) {  // fixed32 field, little endian
+    put_u8(p, key);
+    const uint32_t u = __float_as_uint(x);
+    put_u8(p, u); put_u8(p, u >> 8); put_u8(p, u >> 16); put_u8(p, u >> 24);
+}
+__host__ __device__ inline int varint_len(uint32_t v) { int n = 1; while (v >= 0x80u) { v >>= 7; ++n; } return n; }
+__host__ __device__ inline int event_len(int kind, int R, int with_action) {
+    // State: 7 cart_pose + 7 pole_pose fixed32 fields = 70 B, wrapped (tag, len 70) = 72 B
+    return (with_action ? (kind == CP_ACTION_CONTINUOUS ? 4 : 2) * 5 + 5 : 0) + R * 72;
+}
+__host__ __device__ inline int record_len(int kind, int R, int with_action) {
+    const int n = event_len(kind, R, with_action);
+    return 1 + varint_len((uint32_t)n) + n;
+}
+// one Episode.event entry: tag 1 (length-delimited), Event { action*, state*, reward }
+CP_DEV void put_record(uint8_t* p, int kind, int R, bool with_action, const void* actions, int i, const float* obs,
+                       float reward) {
+    put_u8(p, 0x0A);
+    put_varint(p, (uint32_t)event_len(kind, R, with_action ? 1 : 0));
+    if (with_action) {
+        if (kind == CP_ACTION_CONTINUOUS) {
+            const float* a = reinterpret_cast<const float*>(actions) + (size_t)i * 4;
+            for (int k = 0; k < 4; ++k) put_f32(p, 0x0D, a[k]);
+        } else {
+            const int8_t* a = reinterpret_cast<const int8_t*>(actions) + (size_t)i * 2;
+            put_f32(p, 0x0D, (float)a[0]);
+            put_f32(p, 0x0D, (float)a[1]);
+        }
+    }
+    for (int r = 0; r < R; ++r) {
+        put_u8(p, 0x12);
+        put_u8(p, 70);
+        const float* o = obs + ((size_t)i * R + r) * 14;
+        for (int k = 0; k < 7; ++k) put_f32(p, 0x0D, o[k]);       // cart_pose = 1
+        for (int k = 0; k < 7; ++k) put_f32(p, 0x15, o[7 + k]);   // pole_pose = 2
+    }
+    if (with_action) put_f32(p, 0x1D, reward);                    // reward = 3
+}
+
+__global__ void __launch_bounds__(256) cp_event_kernel(int B, int R, int mode, int kind, int autoreset,
+                                                        const void* actions, const float* obs, const float* term,
+                                                        const float* reward, const uint8_t* done,
+                                                        const uint8_t* mask, const uint8_t* stepped,
+                                                        uint8_t* step_rec, uint8_t* reset_rec, uint8_t* flags) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    const int sb = record_len(kind, R, 1), rb = record_len(kind, R, 0);
+    uint8_t fl = 0;
+    if (mode == 0) {
+        if (stepped[i]) {
+            fl = 1;
+            const bool fresh = autoreset && done[i];   // finished and auto-reset in that cp_step
+            put_record(step_rec + (size_t)i * sb, kind, R, true, actions, i, fresh && term ? term : obs,
+                       reward[i]);
+            if (fresh && reset_rec) {
+                fl |= 2;
+                put_record(reset_rec + (size_t)i * rb, kind, R, false, nullptr, i, obs, 0.0f);
+            }
+        }
+    } else if (!mask || mask[i]) {
+        fl = 2;
+        put_record(reset_rec + (size_t)i * rb, kind, R, false, nullptr, i, obs, 0.0f);
+    }
+    flags[i] = fl;
 }
 
 __global__ void __launch_bounds__(256) cp_copy_kernel(const float* src, float* dst, size_t n) {
@@ -571,7 +647,10 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     CP_ALLOC(h->b.count, sizeof(int32_t));
     CP_ALLOC(h->b.scratch, (size_t)4 * CP_ISLAND_PAIRS * 2 * B * sizeof(float));
     CP_ALLOC(h->b.stamps, 8 * sizeof(uint64_t));
+    CP_ALLOC(h->b.stepped, B * sizeof(uint8_t));
 #undef CP_ALLOC
+    e = hipMemset(h->b.stepped, 0, B * sizeof(uint8_t));
+    if (e != hipSuccess) return fail_free(e, "hipMemset");
     e = hipMemset(h->b.stamps, 0, 8 * sizeof(uint64_t));
     if (e != hipSuccess) return fail_free(e, "hipMemset");
     e = hipMemset(h->b.term_obs, 0, (size_t)R * 14 * B * sizeof(float));
@@ -602,6 +681,7 @@ void cp_destroy(cp_handle* h) {
     (void)hipFree(h->b.count);
     (void)hipFree(h->b.scratch);
     (void)hipFree(h->b.stamps);
+    (void)hipFree(h->b.stepped);
     (void)hipFree(h->b.rposes);
     (void)hipFree(h->b.rlist);
     (void)hipFree(h->b.rcount);
@@ -769,6 +849,31 @@ int cp_timing_end(cp_handle* h, double* step_ms, int32_t* step_launches, double*
     return 0;
 }
 
+int cp_event_record_bytes(int action_kind, int repeats, int with_action) {
+    if ((action_kind != CP_ACTION_CONTINUOUS && action_kind != CP_ACTION_DISCRETE) || repeats <= 0)
+        return fail(nullptr, "cp_event_record_bytes: bad action kind or repeats");
+    return cp::record_len(action_kind, repeats, with_action ? 1 : 0);
+}
+
+int cp_encode_events(cp_handle* h, int mode, const void* actions, int action_kind, const float* obs,
+                     const float* terminal_obs, const float* reward, const uint8_t* done, const uint8_t* env_mask,
+                     uint8_t* step_records, uint8_t* reset_records, uint8_t* flags, void* stream) {
+    if (!h || !obs || !flags) return fail(h, "cp_encode_events: null argument");
+    if (action_kind != CP_ACTION_CONTINUOUS && action_kind != CP_ACTION_DISCRETE)
+        return fail(h, "cp_encode_events: bad action kind");
+    if (mode == 0 && (!actions || !reward || !done || !step_records))
+        return fail(h, "cp_encode_events: mode 0 needs actions, reward, done and step_records");
+    if (mode == 1 && !reset_records) return fail(h, "cp_encode_events: mode 1 needs reset_records");
+    if (mode != 0 && mode != 1) return fail(h, "cp_encode_events: mode must be 0 (step) or 1 (reset)");
+    CP_TRY(h, hipSetDevice(h->device));
+    const int B = h->cfg.num_envs;
+    hipLaunchKernelGGL(cp::cp_event_kernel, dim3(grid_for(B, 256)), dim3(256), 0, (hipStream_t)stream, B,
+                       h->cfg.action_repeats, mode, action_kind, h->cfg.autoreset, actions, obs, terminal_obs, reward,
+                       done, env_mask, h->b.stepped, step_records, reset_records, flags);
+    CP_TRY(h, hipGetLastError());
+    return 0;
+}
+
 int cp_timing_render(cp_handle* h, double* render_ms, int32_t* render_launches) {
     if (!h) return fail(h, "cp_timing_render: null handle");
     if (render_ms) *render_ms = h->timing.render_ms;
@@ -850,6 +955,68 @@ int cp_set_raster(cp_handle* h, const cp_raster_config* rc, uint16_t* pixels_out
     CP_TRY(h, hipGetLastError());
     CP_TRY(h, hipDeviceSynchronize());
     return 0;
+}
+
+// ---------------------------------------------------------------- event log writer
+}  // extern "C"
+
+struct cp_eventlog {
+    FILE* f = nullptr;
+    std::vector<std::vector<uint8_t>> ep;  // open episode per env (encoded Episode body)
+};
+
+static int eventlog_flush(cp_eventlog* log, std::vector<uint8_t>& ep) {
+    if (ep.empty()) return 0;
+    const int32_t n = (int32_t)ep.size();  // struct.pack('=l', len(buff)), event_log.py:54
+    if (std::fwrite(&n, sizeof(n), 1, log->f) != 1 || std::fwrite(ep.data(), 1, ep.size(), log->f) != ep.size())
+        return fail(nullptr, "cp_eventlog: write failed");
+    ep.clear();
+    return 0;
+}
+
+extern "C" {
+
+int cp_eventlog_open(const char* path, int num_envs, cp_eventlog** out) {
+    if (!path || !out || num_envs <= 0) return fail(nullptr, "cp_eventlog_open: bad argument");
+    cp_eventlog* log = new (std::nothrow) cp_eventlog();
+    if (!log) return fail(nullptr, "cp_eventlog_open: out of memory");
+    log->f = std::fopen(path, "ab");  // appends, as event_log.py:45
+    if (!log->f) {
+        delete log;
+        return fail(nullptr, std::string("cp_eventlog_open: cannot open ") + path);
+    }
+    log->ep.resize((size_t)num_envs);
+    *out = log;
+    return 0;
+}
+
+int cp_eventlog_write(cp_eventlog* log, const uint8_t* flags, const uint8_t* step_records, int step_bytes,
+                      const uint8_t* reset_records, int reset_bytes) {
+    if (!log || !flags) return fail(nullptr, "cp_eventlog_write: null argument");
+    for (size_t i = 0; i < log->ep.size(); ++i) {
+        const uint8_t fl = flags[i];
+        if ((fl & 1) && step_records) {
+            const uint8_t* r = step_records + i * (size_t)step_bytes;
+            log->ep[i].insert(log->ep[i].end(), r, r + step_bytes);
+        }
+        if ((fl & 2) && reset_records) {  // EventLog.reset + add_just_state (bullet_cartpole.py:342-344)
+            if (eventlog_flush(log, log->ep[i])) return -1;
+            const uint8_t* r = reset_records + i * (size_t)reset_bytes;
+            log->ep[i].assign(r, r + reset_bytes);
+        }
+    }
+    std::fflush(log->f);
+    return 0;
+}
+
+int cp_eventlog_close(cp_eventlog* log) {
+    if (!log) return fail(nullptr, "cp_eventlog_close: null handle");
+    int rc = 0;
+    for (auto& ep : log->ep)
+        if (eventlog_flush(log, ep)) rc = -1;
+    if (std::fclose(log->f) != 0) rc = fail(nullptr, "cp_eventlog_close: close failed");
+    delete log;
+    return rc;
 }
 
 }  // extern "C"

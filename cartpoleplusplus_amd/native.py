@@ -18,6 +18,7 @@ EXPORTS = (
     "cp_reset", "cp_step", "cp_set_readback", "cp_set_bump_forces", "cp_get_state",
     "cp_set_state", "cp_episode_returns", "cp_overflow_counts", "cp_timing_begin", "cp_timing_end",
     "cp_debug_stamps", "cp_default_raster_config", "cp_set_raster", "cp_timing_render",
+    "cp_event_record_bytes", "cp_encode_events", "cp_eventlog_open", "cp_eventlog_write", "cp_eventlog_close",
 )
 
 _lib = None
@@ -59,6 +60,11 @@ def load():
         "cp_default_raster_config": (None, [P(abi.cp_raster_config)]),
         "cp_set_raster": (I, [VP, P(abi.cp_raster_config), VP]),
         "cp_timing_render": (I, [VP, P(C.c_double), P(C.c_int32)]),
+        "cp_event_record_bytes": (I, [I, I, I]),
+        "cp_encode_events": (I, [VP, I, VP, I, VP, VP, VP, VP, VP, VP, VP, VP, VP]),
+        "cp_eventlog_open": (I, [C.c_char_p, I, P(VP)]),
+        "cp_eventlog_write": (I, [VP, VP, VP, I, VP, I]),
+        "cp_eventlog_close": (I, [VP]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

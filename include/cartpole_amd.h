@@ -246,6 +246,41 @@ int cp_set_raster(cp_handle* h, const cp_raster_config* rc, uint16_t* pixels_out
  * of the last cp_timing_begin .. cp_timing_end window: summed ms and launch count. */
 int cp_timing_render(cp_handle* h, double* render_ms, int32_t* render_launches);
 
+/* ---- Event log (--event-log-out) ---------------------
+ * Replaces event_log.EventLog (event_log.py:42-99) for B envs: episodes of events
+ * in the protobuf wire format of event.proto:1-35, each episode framed by a
+ * native int32 length ('=l', event_log.py:53-57), appended to one file.
+ *
+ * Record = one `event` field of an Episode (tag, length, Event), fixed size per
+ * (action kind, R): a step record holds the action (continuous: 4 floats
+ * a00 a01 a10 a11; discrete: the 2 indices as floats), R States (cart_pose[7],
+ * pole_pose[7]) and the reward; a reset record holds the R States only
+ * (event_log.py:95-97, bullet_cartpole.py:342-344). */
+int cp_event_record_bytes(int action_kind, int repeats, int with_action);
+
+/* GPU encoder (device pointers).  mode 0, after cp_step: for every env simulated by
+ * the last cp_step (not the done-before ones, which the reference does not log,
+ * :179-181) a step record from obs (or terminal_obs for an env that finished and
+ * was auto-reset) and flags |= 1; an auto-reset env also gets a reset record from
+ * obs and flags |= 2.  mode 1, after cp_reset: a reset record and flags = 2 for
+ * every env with env_mask != 0 (NULL = all).  step_records [B][step bytes],
+ * reset_records [B][reset bytes], flags uint8 [B]; unused pointers may be NULL. */
+int cp_encode_events(cp_handle* h, int mode, const void* actions, int action_kind, const float* obs,
+                     const float* terminal_obs, const float* reward, const uint8_t* done,
+                     const uint8_t* env_mask, uint8_t* step_records, uint8_t* reset_records,
+                     uint8_t* flags, void* stream);
+
+/* Host writer (host pointers; no GPU).  cp_eventlog_write, per env i: flags & 1
+ * appends step_records[i] to the env's open episode; flags & 2 writes the open
+ * episode (if not empty) and starts a new one with reset_records[i].  Close
+ * writes every non-empty open episode, then closes the file (the reference
+ * drops the last episode; writing it is the one extension). */
+typedef struct cp_eventlog cp_eventlog;
+int cp_eventlog_open(const char* path, int num_envs, cp_eventlog** out);
+int cp_eventlog_write(cp_eventlog* log, const uint8_t* flags, const uint8_t* step_records, int step_bytes,
+                      const uint8_t* reset_records, int reset_bytes);
+int cp_eventlog_close(cp_eventlog* log);
+
 #ifdef __cplusplus
 }
 #endif
