@@ -133,3 +133,33 @@ def obs_shape(B, R):
 
 def readback_shape(B, R, S):
     return (B, 2, R, S, 4, 3)
+
+
+# ---- replay memory (include/cartpole_amd.h: cp_replay)
+CP_RM_INSERT, CP_RM_FULL, CP_RM_HEAD, CP_RM_TAIL, CP_RM_ERROR, CP_RM_ADDS, CP_RM_EVICTED_S2 = range(7)
+CP_RM_CTRL = 8
+CP_STATES_F32 = 0
+CP_STATES_F16 = 1
+
+
+class cp_replay(C.Structure):
+    _fields_ = [
+        ("buffer_size", C.c_int32),
+        ("state_buffer_size", C.c_int32),
+        ("state_dim", C.c_int32),
+        ("action_dim", C.c_int32),
+        ("state", C.c_void_p),
+        ("state_1_idx", C.c_void_p),
+        ("action", C.c_void_p),
+        ("reward", C.c_void_p),
+        ("terminal_mask", C.c_void_p),
+        ("state_2_idx", C.c_void_p),
+        ("free_slots", C.c_void_p),
+        ("ctrl", C.c_void_p),
+        ("plan", C.c_void_p),
+    ]
+
+
+class cp_replay_batch(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("idx", "state_1", "action", "reward", "terminal_mask", "state_2",
+                                          "state_1_idx", "state_2_idx")]

@@ -13,7 +13,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "cp_kernels.hip")
-DEPS = [os.path.join(HERE, "csrc", f) for f in ("cp_kernels.hip", "cp_physics.h", "cp_math.h", "cp_raster.h")] + [
+DEPS = [os.path.join(HERE, "csrc", f) for f in ("cp_kernels.hip", "cp_physics.h", "cp_math.h", "cp_raster.h", "cp_replay.h")] + [
     os.path.join(HERE, "..", "include", "cartpole_amd.h")]
 LIB = os.path.join(HERE, "libcartpole_hip.so")
 STAMPS_LIB = os.path.join(HERE, "libcartpole_hip_stamps.so")

@@ -16,6 +16,7 @@
 // 20 KiB-per-wave LDS pool (8 waves per CU = 160 KiB).  DESIGN.md §Kernels.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -26,6 +27,7 @@
 #include "../../include/cartpole_amd.h"
 #include "cp_physics.h"
 #include "cp_raster.h"
+#include "cp_replay.h"
 
 namespace cp {
 
@@ -1017,6 +1019,86 @@ int cp_eventlog_close(cp_eventlog* log) {
     if (std::fclose(log->f) != 0) rc = fail(nullptr, "cp_eventlog_close: close failed");
     delete log;
     return rc;
+}
+
+int cp_get_stepped(cp_handle* h, uint8_t* out, void* stream) {
+    if (!h || !out) return fail(h, "cp_get_stepped: null argument");
+    CP_TRY(h, hipSetDevice(h->device));
+    CP_TRY(h, hipMemcpyAsync(out, h->b.stepped, h->cfg.num_envs, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return 0;
+}
+
+/* ---- replay memory (cp_replay.h) ---- */
+static int replay_ok(const cp_replay* rm, const char* what) {
+    if (!rm || !rm->state || !rm->state_1_idx || !rm->action || !rm->reward || !rm->terminal_mask ||
+        !rm->state_2_idx || !rm->free_slots || !rm->ctrl || !rm->plan)
+        return fail(nullptr, std::string(what) + ": null replay buffer");
+    if (rm->buffer_size < 1 || rm->state_dim < 1 || rm->action_dim < 1 ||
+        rm->state_buffer_size < rm->buffer_size + rm->buffer_size / 2)
+        return fail(nullptr, std::string(what) + ": bad sizes (state_buffer_size must be >= int(1.5 * buffer_size))");
+    return 0;
+}
+
+int cp_replay_init(const cp_replay* rm, int32_t* cur, int rows, void* stream) {
+    if (replay_ok(rm, "cp_replay_init")) return -1;
+    if (rows < 0 || (rows > 0 && !cur)) return fail(nullptr, "cp_replay_init: bad rows / cur");
+    const int64_t n = std::max<int64_t>(std::max<int64_t>(rm->state_buffer_size, rows), CP_RM_CTRL);
+    hipLaunchKernelGGL(cprm::init_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       *rm, cur, rows);
+    CP_TRY(nullptr, hipGetLastError());
+    return 0;
+}
+
+int cp_replay_add(const cp_replay* rm, int32_t* cur, int rows, const uint8_t* valid, const void* actions,
+                  int action_kind, const float* reward, const uint8_t* done, const uint8_t* restart,
+                  const void* next_states, const void* terminal_states, int state_kind, void* stream) {
+    if (replay_ok(rm, "cp_replay_add")) return -1;
+    if (rows < 0 || rows > rm->buffer_size) return fail(nullptr, "cp_replay_add: rows must be in [0, buffer_size]");
+    if (rows == 0) return 0;
+    if (!cur) return fail(nullptr, "cp_replay_add: null cur");
+    if (valid && (!actions || !reward || !done || !next_states))
+        return fail(nullptr, "cp_replay_add: events need actions, reward, done and next_states");
+    if (restart && !next_states) return fail(nullptr, "cp_replay_add: restarts need next_states");
+    if (action_kind != CP_ACTION_CONTINUOUS && action_kind != CP_ACTION_DISCRETE)
+        return fail(nullptr, "cp_replay_add: bad action kind");
+    if (state_kind != CP_STATES_F32 && state_kind != CP_STATES_F16)
+        return fail(nullptr, "cp_replay_add: bad state kind");
+    if (!valid && !restart) return 0;
+    const hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(cprm::plan_kernel, dim3(1), dim3(cprm::PLAN_THREADS), 0, st, *rm, rows, valid, restart);
+    switch (cprm::vec_for(rm->state_dim, state_kind)) {
+        case 8: cprm::launch_write<8>(rm, rows, cur, actions, action_kind, reward, done, restart, next_states,
+                                       terminal_states, state_kind, st); break;
+        case 4: cprm::launch_write<4>(rm, rows, cur, actions, action_kind, reward, done, restart, next_states,
+                                       terminal_states, state_kind, st); break;
+        case 2: cprm::launch_write<2>(rm, rows, cur, actions, action_kind, reward, done, restart, next_states,
+                                       terminal_states, state_kind, st); break;
+        default: cprm::launch_write<1>(rm, rows, cur, actions, action_kind, reward, done, restart, next_states,
+                                        terminal_states, state_kind, st);
+    }
+    CP_TRY(nullptr, hipGetLastError());
+    return 0;
+}
+
+int cp_replay_sample(const cp_replay* rm, int n, const int32_t* idxs, uint64_t seed, uint64_t counter,
+                     const cp_replay_batch* out, void* stream) {
+    if (replay_ok(rm, "cp_replay_sample")) return -1;
+    if (n < 0 || !out) return fail(nullptr, "cp_replay_sample: bad n / null out");
+    if (n == 0) return 0;
+    const int vec = cprm::vec_for(rm->state_dim, CP_STATES_F16);
+    const int64_t threads = (int64_t)n * (rm->state_dim / vec);
+    const dim3 grid((unsigned)((threads + 255) / 256));
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32), c1 = (uint32_t)counter,
+                   c2 = (uint32_t)(counter >> 32);
+    const hipStream_t st = (hipStream_t)stream;
+    switch (vec) {
+        case 8: hipLaunchKernelGGL(cprm::sample_kernel<8>, grid, dim3(256), 0, st, *rm, n, idxs, k0, k1, c1, c2, *out); break;
+        case 4: hipLaunchKernelGGL(cprm::sample_kernel<4>, grid, dim3(256), 0, st, *rm, n, idxs, k0, k1, c1, c2, *out); break;
+        case 2: hipLaunchKernelGGL(cprm::sample_kernel<2>, grid, dim3(256), 0, st, *rm, n, idxs, k0, k1, c1, c2, *out); break;
+        default: hipLaunchKernelGGL(cprm::sample_kernel<1>, grid, dim3(256), 0, st, *rm, n, idxs, k0, k1, c1, c2, *out);
+    }
+    CP_TRY(nullptr, hipGetLastError());
+    return 0;
 }
 
 }  // extern "C"

@@ -281,6 +281,82 @@ int cp_eventlog_write(cp_eventlog* log, const uint8_t* flags, const uint8_t* ste
                       const uint8_t* reset_records, int reset_bytes);
 int cp_eventlog_close(cp_eventlog* log);
 
+/* Envs simulated by the last cp_step (uint8 [B], 1 = its transition is real; the
+ * done-before envs of a non-autoreset handle are 0).  Device copy on `stream`. */
+int cp_get_stepped(cp_handle* h, uint8_t* out, void* stream);
+
+/* ---- Replay memory in HBM ------------------------------
+ * Replaces replay_memory.ReplayMemory (replay_memory.py:11-163): a ring of
+ * buffer_size events (state_1_idx, action, reward, terminal_mask, state_2_idx) and
+ * a float16 state buffer of state_buffer_size = int(buffer_size * load_factor)
+ * rows shared by consecutive events, free state slots in a FIFO ring (the
+ * reference's state_free_slots list, pop(0) / append).  All storage is caller
+ * owned device memory (the struct holds device pointers); the functions below
+ * launch kernels on `stream` and never synchronise.
+ *
+ * Transitions arrive in "rows" (one per env; cur[row] holds the row's current
+ * state_1 slot, -1 before its first episode).  cp_replay_add applies, for row
+ * j = 0 .. rows-1 in order, exactly the reference's _add (:76-118) for every row
+ * with valid[j] (s1 = cur[j], terminal = done[j], s2 = terminal_states[j] when
+ * restart[j] and terminal_states != NULL, else next_states[j]) and then, for every
+ * row with restart[j], add_episode's slot pop for the new episode's first state
+ * next_states[j] (:65-67).  valid = NULL adds no events (episode starts only);
+ * restart = NULL restarts none.  rows <= buffer_size.
+ * A free-slot underflow (the reference's pop from an empty list), an event for a
+ * row with no episode, or a sample index out of range sets a sticky error bit in
+ * ctrl[CP_RM_ERROR] (read it back; the memory is unusable after one). */
+#define CP_RM_INSERT 0   /* ctrl[]: int64 insert pointer */
+#define CP_RM_FULL 1     /* 1 once the ring wrapped */
+#define CP_RM_HEAD 2     /* free-slot ring: pops so far */
+#define CP_RM_TAIL 3     /* free-slot ring: pushes so far (+ state_buffer_size initial) */
+#define CP_RM_ERROR 4    /* bit 0 slot underflow, bit 1 row without episode, bit 2 bad index */
+#define CP_RM_ADDS 5     /* events added ('>add' stat) */
+#define CP_RM_EVICTED_S2 6 /* 'cache_evicted_s2' stat */
+#define CP_RM_CTRL 8
+
+#define CP_STATES_F32 0  /* state inputs float32 (converted round-to-nearest-even) */
+#define CP_STATES_F16 1  /* state inputs float16 bits, stored as is */
+
+typedef struct cp_replay {
+    int32_t buffer_size;        /* N events */
+    int32_t state_buffer_size;  /* S state slots */
+    int32_t state_dim;          /* D: float16 elements per state */
+    int32_t action_dim;         /* A */
+    uint16_t* state;            /* [S][D] float16 */
+    int32_t* state_1_idx;       /* [N] */
+    float* action;              /* [N][A] */
+    float* reward;              /* [N] */
+    float* terminal_mask;       /* [N] 0 = terminal */
+    int32_t* state_2_idx;       /* [N] */
+    int32_t* free_slots;        /* [S] FIFO ring */
+    int64_t* ctrl;              /* [CP_RM_CTRL] */
+    int32_t* plan;              /* [2 * max rows] scratch */
+} cp_replay;
+
+/* Empty memory: free_slots = 0..S-1 in order (:35), ctrl zeroed, cur[0..rows) = -1. */
+int cp_replay_init(const cp_replay* rm, int32_t* cur, int rows, void* stream);
+int cp_replay_add(const cp_replay* rm, int32_t* cur, int rows, const uint8_t* valid, const void* actions,
+                  int action_kind, const float* reward, const uint8_t* done, const uint8_t* restart,
+                  const void* next_states, const void* terminal_states, int state_kind, void* stream);
+
+/* Gather n events (batch(), :128-135): idxs (int32 [n], device) or, when NULL, uniform
+ * random indexes in [0, size) from Philox4x32-10 (seed, counter) (random_indexes,
+ * :120-126).  Outputs (each may be NULL): idx_out [n], state_1 [n][D] float16,
+ * action [n][A], reward [n], terminal_mask [n], state_2 [n][D], state_1_idx [n],
+ * state_2_idx [n]. */
+typedef struct cp_replay_batch {
+    int32_t* idx;
+    uint16_t* state_1;
+    float* action;
+    float* reward;
+    float* terminal_mask;
+    uint16_t* state_2;
+    int32_t* state_1_idx;
+    int32_t* state_2_idx;
+} cp_replay_batch;
+int cp_replay_sample(const cp_replay* rm, int n, const int32_t* idxs, uint64_t seed, uint64_t counter,
+                     const cp_replay_batch* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -78,6 +78,8 @@ int main(void) {{
          offsetof(cp_config, seed), offsetof(cp_config, phys), offsetof(cp_physics, half_extents),
          offsetof(cp_physics, spawn_pos), offsetof(cp_physics, warmstart));
   printf("%d %d\\n", CP_STATE_FIELDS, CP_SF_WS_LAM(1, 4, 3));
+  printf("%zu %zu %zu %zu %zu\\n", sizeof(cp_replay), offsetof(cp_replay, state), offsetof(cp_replay, plan),
+         sizeof(cp_replay_batch), offsetof(cp_replay_batch, state_2_idx));
   return 0;
 }}""")
     exe = tmp_path / "layout"
@@ -89,6 +91,9 @@ int main(void) {{
            abi.cp_physics.warmstart.offset]
     assert got == exp
     assert list(map(int, out[1].split())) == [abi.CP_STATE_FIELDS, abi.CP_SF_WS_LAM(1, 4, 3)]
+    assert list(map(int, out[2].split())) == [C.sizeof(abi.cp_replay), abi.cp_replay.state.offset,
+                                              abi.cp_replay.plan.offset, C.sizeof(abi.cp_replay_batch),
+                                              abi.cp_replay_batch.state_2_idx.offset]
 
 
 def test_create_without_gpu_fails_loudly():
