@@ -122,6 +122,24 @@ class BatchedCartpole:
         native.check(self.h, self.lib.cp_set_raster(self.h, C.byref(rc), _ptr(self.pixels)), "cp_set_raster")
         return self.pixels
 
+    def enable_lqr(self, gains, per_env=False, state8=True, done_pos=0.0, done_angle=0.0):
+        """Closed-loop LQR policy (random_action_agent.py:60-135; see cp_set_lqr): every
+        substep pushes cart p with action_force * action_p + u_p, u_p = -K_p . s_p from pole
+        p's 8-state.  gains (2, 2, 8) shared or (B, 2, 2, 8) per env (A/B gain search
+        across envs); None turns it off.  state8: fill self.state8 (B, R, S, 2, 8).
+        done_pos > 0: end an episode when both pairs leave the agent's bounds
+        (random_action_agent.py:108-119, :908; the agent uses 3.0 m and pi/4)."""
+        if gains is None:
+            self.lqr_gains = self.state8 = None
+            native.check(self.h, self.lib.cp_set_lqr(self.h, None, 0, None, 0.0, 0.0), "cp_set_lqr")
+            return
+        g = torch.as_tensor(gains, dtype=torch.float32, device=self.device).contiguous()
+        assert g.shape == ((self.B,) if per_env else ()) + (2, 2, 8), g.shape
+        self.lqr_gains = g
+        self.state8 = torch.zeros((self.B, self.R, self.S, 2, 8), device=self.device) if state8 else None
+        native.check(self.h, self.lib.cp_set_lqr(self.h, _ptr(g), int(bool(per_env)), _ptr(self.state8),
+                                                 float(done_pos), float(done_angle)), "cp_set_lqr")
+
     def set_bump_forces(self, forces):
         """Parity mode (bump_mode='host'): LINK-frame bump forces (B, 30, 2, 2)."""
         f = torch.as_tensor(forces, dtype=torch.float32, device=self.device).contiguous()

@@ -147,6 +147,57 @@ CP_DEV void readback_pole(const Sim& S, float* dst) {
     dst[9] = vb.w.x; dst[10] = vb.w.y; dst[11] = vb.w.z;
 }
 
+// ---- closed-loop LQR policy (random_action_agent.py:60-135)
+struct Lqr {
+    const float* gains;  // [B or 1][2 pairs][2 (fx, fy)][8]
+    int per_env;
+    float* state8;       // [B][2][R][S][8] or null
+    float done_pos;      // _check_done thresholds (:108-119); <= 0: no bounds termination
+    float done_angle;
+};
+
+// pole 8-state of pair P (:121-135): x - x0, x', y, y', roll, roll', pitch, pitch'
+template <int P>
+CP_DEV void pole_state8(const Sim& S, float x0, float s[8]) {
+    const Body& p = S.b[2 * P + 1];
+    const V3 rpy = quat_euler(p.q[0], p.q[1], p.q[2], p.q[3]);
+    s[0] = p.x.x - x0; s[1] = p.v.x; s[2] = p.x.y; s[3] = p.v.y;
+    s[4] = rpy.x; s[5] = p.w.x; s[6] = rpy.y; s[7] = p.w.y;
+}
+
+// u = -K s (:92-95, lqr zero point 0), accumulated k = 0..7 with fma
+CP_DEV void lqr_u(const float* K, const float s[8], float& ux, float& uy) {
+    float ax = 0.0f, ay = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        ax = fmaf_(K[k], s[k], ax);
+        ay = fmaf_(K[8 + k], s[k], ay);
+    }
+    ux = -ax;
+    uy = -ay;
+}
+
+CP_DEV bool lqr_out_of_bounds(const float s[8], float pos, float ang) {
+    return fabsf(s[0]) > pos || fabsf(s[2]) > pos || fabsf(s[4]) > ang || fabsf(s[6]) > ang;
+}
+
+// 8-states of both pairs -> next forces; true if both pairs are out of bounds (:908)
+CP_DEV bool lqr_observe(const Sim& S, const cp_config& cfg, const Lqr& q, const float* K, float u[2][2],
+                        float* s8_out) {
+    float s[8];
+    pole_state8<0>(S, cfg.phys.spawn_pos[CP_BODY_POLE][0], s);
+    if (s8_out)
+        for (int k = 0; k < 8; ++k) s8_out[k] = s[k];
+    lqr_u(K, s, u[0][0], u[0][1]);
+    const bool out0 = lqr_out_of_bounds(s, q.done_pos, q.done_angle);
+    pole_state8<1>(S, cfg.phys.spawn_pos[CP_BODY_POLE2][0], s);
+    if (s8_out)
+        for (int k = 0; k < 8; ++k) s8_out[k + 8] = s[k];
+    lqr_u(K + 16, s, u[1][0], u[1][1]);
+    const bool out1 = lqr_out_of_bounds(s, q.done_pos, q.done_angle);
+    return q.done_pos > 0.0f && out0 && out1;
+}
+
 // commented-out bounds check of the reference (:243-253), on the pole pose
 CP_DEV bool bounds_exceeded(const Sim& S, const cp_config& cfg) {
     const Body& p = S.b[1];
@@ -287,10 +338,10 @@ __global__ void CP_PHYS_ATTR cp_reset_kernel(cp_config cfg, Bufs b, float* obs_o
     b.ret_acc[i] = 0.0f;
 }
 
-template <int KIND>
+template <int KIND, bool LQR>
 __global__ void CP_PHYS_ATTR cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out,
                                                         float* reward_out, uint8_t* done_out, float* term_out,
-                                                        float* readback, int rb_bug) {
+                                                        float* readback, int rb_bug, Lqr lq) {
     __shared__ float lds_pool[POOL_FLOATS * WAVE];
     const int B = cfg.num_envs;
     const int t = blockIdx.x * WAVE + threadIdx.x;
@@ -335,11 +386,25 @@ __global__ void CP_PHYS_ATTR cp_step_kernel(cp_config cfg, Bufs b, const void* a
             Sim S;
             load_sim(S, G.st, G.off);
             int ov = 0;
+            float u[2][2] = {{0.0f, 0.0f}, {0.0f, 0.0f}};  // LQR forces from the last observed state
+            bool lqr_done = false;
+            const float* K = nullptr;
+            if constexpr (LQR) {
+                K = lq.gains + (lq.per_env ? (size_t)i * 32 : 0);
+                lqr_observe(S, cfg, lq, K, u, nullptr);
+            }
             for (int r = 0; r < R; ++r) {
                 for (int s = 0; s < SR; ++s) {
                     substep(S, cfg.phys, L, pool, pool0, ov, G, ST);
-                    apply_force_link<0>(S, f00, f01);
-                    apply_force_link<1>(S, f10, f11);
+                    if constexpr (LQR) {  // disturbance + control (:897-901), control from the pre-step state
+                        apply_force_link<0>(S, f00 + u[0][0], f01 + u[0][1]);
+                        apply_force_link<1>(S, f10 + u[1][0], f11 + u[1][1]);
+                        float* s8 = (lq.state8 && lead) ? lq.state8 + (((size_t)i * R + r) * SR + s) * 16 : nullptr;
+                        lqr_done |= lqr_observe(S, cfg, lq, K, u, s8);
+                    } else {
+                        apply_force_link<0>(S, f00, f01);
+                        apply_force_link<1>(S, f10, f11);
+                    }
                     if (readback && lead) {
                         float* rb = readback + (size_t)i * 2 * R * SR * 12;
                         readback_pole<1, 1>(S, rb + ((size_t)(0 * R + r) * SR + s) * 12);
@@ -361,6 +426,7 @@ __global__ void CP_PHYS_ATTR cp_step_kernel(cp_config cfg, Bufs b, const void* a
             const int steps = ldi(G.st, CP_SF_STEPS, G.off) + 1;
             bool done = steps >= cfg.max_episode_len;
             if (cfg.done_on_bounds && bounds_exceeded(S, cfg)) done = true;
+            if (LQR && lqr_done) done = true;
             if (lead) {
                 store_sim(S, G.st, G.off);
                 sti(G.st, CP_SF_STEPS, G.off, steps);
@@ -502,6 +568,7 @@ struct cp_handle {
     cp::Bufs b;
     float* readback;
     int readback_bug;
+    cp::Lqr lqr;
     cp_timing timing;
     cp_raster_config raster;
     uint16_t* pixels;  // raster obs output (NULL: raster off)
@@ -623,6 +690,7 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     h->device = device;
     h->readback = nullptr;
     h->readback_bug = 1;
+    h->lqr = cp::Lqr{nullptr, 0, nullptr, 0.0f, 0.0f};
     h->pixels = nullptr;
     cp_default_raster_config(&h->raster);
     std::memset(&h->b, 0, sizeof(h->b));
@@ -738,12 +806,18 @@ int cp_step(cp_handle* h, const void* actions, int action_kind, float* obs_out, 
     dim3 grid(grid_for(2 * B, cp::WAVE)), block(cp::WAVE);  // two lanes per env
     hipEvent_t* ev = timing_slot(h, 0);
     if (ev) CP_TRY(h, hipEventRecord(ev[0], st));
-    if (action_kind == CP_ACTION_CONTINUOUS)
-        hipLaunchKernelGGL(cp::cp_step_kernel<CP_ACTION_CONTINUOUS>, grid, block, 0, st, h->cfg, h->b, actions,
-                           obs_out, reward_out, done_out, terminal_obs_out, h->readback, h->readback_bug);
-    else
-        hipLaunchKernelGGL(cp::cp_step_kernel<CP_ACTION_DISCRETE>, grid, block, 0, st, h->cfg, h->b, actions,
-                           obs_out, reward_out, done_out, terminal_obs_out, h->readback, h->readback_bug);
+    const bool lqr = h->lqr.gains != nullptr;
+#define CP_LAUNCH_STEP(K, Q)                                                                                   \
+    hipLaunchKernelGGL((cp::cp_step_kernel<K, Q>), grid, block, 0, st, h->cfg, h->b, actions, obs_out, reward_out, \
+                       done_out, terminal_obs_out, h->readback, h->readback_bug, h->lqr)
+    if (action_kind == CP_ACTION_CONTINUOUS) {
+        if (lqr) CP_LAUNCH_STEP(CP_ACTION_CONTINUOUS, true);
+        else CP_LAUNCH_STEP(CP_ACTION_CONTINUOUS, false);
+    } else {
+        if (lqr) CP_LAUNCH_STEP(CP_ACTION_DISCRETE, true);
+        else CP_LAUNCH_STEP(CP_ACTION_DISCRETE, false);
+    }
+#undef CP_LAUNCH_STEP
     CP_TRY(h, hipGetLastError());
     if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
     // autoreset envs were simulated this step, so they are in the render list; the reset
@@ -757,6 +831,18 @@ int cp_set_readback(cp_handle* h, float* readback_out, int reference_bug) {
     if (!h) return fail(h, "cp_set_readback: null handle");
     h->readback = readback_out;
     h->readback_bug = reference_bug ? 1 : 0;
+    return 0;
+}
+
+int cp_set_lqr(cp_handle* h, const float* gains, int per_env, float* state8_out, float done_pos,
+               float done_angle) {
+    if (!h) return fail(h, "cp_set_lqr: null handle");
+    if (!gains && state8_out) return fail(h, "cp_set_lqr: the 8-state readback needs the LQR policy on");
+    h->lqr.gains = gains;
+    h->lqr.per_env = per_env ? 1 : 0;
+    h->lqr.state8 = state8_out;
+    h->lqr.done_pos = done_pos;
+    h->lqr.done_angle = done_angle;
     return 0;
 }
 

@@ -19,7 +19,7 @@ EXPORTS = (
     "cp_set_state", "cp_episode_returns", "cp_overflow_counts", "cp_timing_begin", "cp_timing_end",
     "cp_debug_stamps", "cp_default_raster_config", "cp_set_raster", "cp_timing_render",
     "cp_event_record_bytes", "cp_encode_events", "cp_eventlog_open", "cp_eventlog_write", "cp_eventlog_close",
-    "cp_get_stepped", "cp_replay_init", "cp_replay_add", "cp_replay_sample",
+    "cp_set_lqr", "cp_get_stepped", "cp_replay_init", "cp_replay_add", "cp_replay_sample",
 )
 
 _lib = None
@@ -67,6 +67,7 @@ def load():
         "cp_eventlog_write": (I, [VP, VP, VP, I, VP, I]),
         "cp_eventlog_close": (I, [VP]),
         "cp_get_stepped": (I, [VP, VP, VP]),
+        "cp_set_lqr": (I, [VP, VP, I, VP, C.c_float, C.c_float]),
         "cp_replay_init": (I, [P(abi.cp_replay), VP, I, VP]),
         "cp_replay_add": (I, [P(abi.cp_replay), VP, I, VP, VP, I, VP, VP, VP, VP, VP, I, VP]),
         "cp_replay_sample": (I, [P(abi.cp_replay), I, VP, C.c_uint64, C.c_uint64, P(abi.cp_replay_batch), VP]),

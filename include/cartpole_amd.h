@@ -181,6 +181,19 @@ int cp_set_readback(cp_handle* h, float* readback_out, int reference_bug);
  * Device pointer; copied into the handle (used by every later reset). */
 int cp_set_bump_forces(cp_handle* h, const float* forces, void* stream);
 
+/* Closed-loop LQR policy (random_action_agent.py:60-135, gains :812-829; SURVEY.md
+ * §8f row f4).  With gains != NULL every substep applies, per cart p,
+ *     force_p = action_force * action_p + u_p,   u_p = -K_p . s_p   (:92-95, :897-901)
+ * in the cart's LINK frame, where s_p is pole p's 8-state observed after the
+ * previous substep: (x - x0, x', y, y', roll, roll', pitch, pitch') with x0 the pole's
+ * spawn x (:121-135).  gains: device float [per_env ? B : 1][2 pairs][2 (fx, fy)][8].
+ * state8_out (device, may be NULL): [B][R][S][2 pairs][8], the 8-states after every
+ * substep.  done_pos > 0 adds the agent's termination (:108-119, :908): the episode
+ * ends when both pairs have |x - x0| or |y| > done_pos or |roll| or |pitch| >
+ * done_angle after the same substep.  gains = NULL turns the policy off. */
+int cp_set_lqr(cp_handle* h, const float* gains, int per_env, float* state8_out, float done_pos,
+               float done_angle);
+
 /* Full env state, SoA float32 [CP_STATE_FIELDS][B] (device pointers). */
 int cp_get_state(cp_handle* h, float* state_out, void* stream);
 int cp_set_state(cp_handle* h, const float* state_in, void* stream);

@@ -1186,6 +1186,46 @@ static void readback_pole(const sim_t* S, int pole_dyn, int vel_dyn, float* dst 
     dst[9] = (float)S->w[vel_dyn].x; dst[10] = (float)S->w[vel_dyn].y; dst[11] = (float)S->w[vel_dyn].z;
 }
 
+/* ---- LQR policy (random_action_agent.py:60-135; cp_kernels.hip lqr_*) ---- */
+void orc_envs_set_lqr(orc_envs* e, const float* gains, int per_env, float* state8_out, float done_pos,
+                      float done_angle) {
+    e->lqr_gains = gains;
+    e->lqr_per_env = per_env ? 1 : 0;
+    e->lqr_state8 = state8_out;
+    e->lqr_done_pos = done_pos;
+    e->lqr_done_angle = done_angle;
+}
+
+/* pole 8-state (:121-135): x - x0, x', y, y', roll, roll', pitch, pitch' */
+static void pole_state8(const sim_t* S, int pole_dyn, real x0, real s[8]) {
+    real rpy[3];
+    quat_euler(S->q[pole_dyn], rpy);
+    s[0] = S->x[pole_dyn].x - x0; s[1] = S->v[pole_dyn].x; s[2] = S->x[pole_dyn].y; s[3] = S->v[pole_dyn].y;
+    s[4] = rpy[0]; s[5] = S->w[pole_dyn].x; s[6] = rpy[1]; s[7] = S->w[pole_dyn].y;
+}
+
+/* u = -K s (:92-95) for both pairs; returns 1 when both pairs are out of bounds (:108-119, :908) */
+static int lqr_observe(const orc_envs* e, const sim_t* S, const float* K, real u[2][2], float* s8_out) {
+    int out[2];
+    for (int p = 0; p < 2; ++p) {
+        real s[8];
+        const int pole = 2 * p + 1;
+        pole_state8(S, pole, (real)e->cfg.phys.spawn_pos[pole + 1][0], s);
+        if (s8_out)
+            for (int k = 0; k < 8; ++k) s8_out[8 * p + k] = (float)s[k];
+        real ax = RC(0), ay = RC(0);
+        for (int k = 0; k < 8; ++k) {
+            ax = FMA((real)K[16 * p + k], s[k], ax);
+            ay = FMA((real)K[16 * p + 8 + k], s[k], ay);
+        }
+        u[p][0] = -ax;
+        u[p][1] = -ay;
+        const real pos = (real)e->lqr_done_pos, ang = (real)e->lqr_done_angle;
+        out[p] = FABS(s[0]) > pos || FABS(s[2]) > pos || FABS(s[4]) > ang || FABS(s[6]) > ang;
+    }
+    return e->lqr_done_pos > 0.0f && out[0] && out[1];
+}
+
 static void step_one(orc_envs* e, int i, const void* actions, int kind, float* obs_out, float* reward_out,
                      uint8_t* done_out, float* term_out, float* readback, int rb_bug) {
     const cp_config* cfg = &e->cfg;
@@ -1216,11 +1256,22 @@ static void step_one(orc_envs* e, int i, const void* actions, int kind, float* o
     int32_t ov = 0;
     int32_t* sw = e->sweeps + (size_t)i * 2;
     sw[0] = sw[1] = 0;
+    real u[2][2] = {{RC(0), RC(0)}, {RC(0), RC(0)}};
+    int lqr_done = 0;
+    const float* K = e->lqr_gains ? e->lqr_gains + (e->lqr_per_env ? (size_t)i * 32 : 0) : NULL;
+    if (K) lqr_observe(e, &S, K, u, NULL);
     for (int r = 0; r < R; ++r) {
         for (int s = 0; s < Sn; ++s) {
             substep(&S, &cfg->phys, &ov, NULL, NULL, sw);
-            apply_force_link(&S, 0, a[0][0] * F, a[0][1] * F, RC(0));
-            apply_force_link(&S, 2, a[1][0] * F, a[1][1] * F, RC(0));
+            if (K) {   /* disturbance + control from the pre-step state (:897-901) */
+                apply_force_link(&S, 0, a[0][0] * F + u[0][0], a[0][1] * F + u[0][1], RC(0));
+                apply_force_link(&S, 2, a[1][0] * F + u[1][0], a[1][1] * F + u[1][1], RC(0));
+                float* s8 = e->lqr_state8 ? e->lqr_state8 + (((size_t)i * R + r) * Sn + s) * 16 : NULL;
+                lqr_done |= lqr_observe(e, &S, K, u, s8);
+            } else {
+                apply_force_link(&S, 0, a[0][0] * F, a[0][1] * F, RC(0));
+                apply_force_link(&S, 2, a[1][0] * F, a[1][1] * F, RC(0));
+            }
             if (readback) {
                 size_t base = (size_t)i * 2 * R * Sn * 12;
                 readback_pole(&S, 1, 1, readback + base + ((size_t)(0 * R + r) * Sn + s) * 12);
@@ -1233,6 +1284,7 @@ static void step_one(orc_envs* e, int i, const void* actions, int kind, float* o
     int steps = get_i(e, CP_SF_STEPS, i) + 1;
     int done = steps >= cfg->max_episode_len;
     if (cfg->done_on_bounds && bounds_exceeded(e, &S)) done = 1;
+    if (lqr_done) done = 1;
     env_store(e, i, &S);
     set_i(e, CP_SF_STEPS, i, steps);
     reward_out[i] = 1.0f;            /* bullet_cartpole.py:260 */

@@ -67,6 +67,7 @@ def load(precision="f32"):
         "orc_envs_create": (C.c_int, [cfgp, P(VP)]),
         "orc_envs_destroy": (None, [VP]),
         "orc_envs_set_bump_forces": (None, [VP, VP]),
+        "orc_envs_set_lqr": (None, [VP, VP, C.c_int, VP, C.c_float, C.c_float]),
         "orc_envs_get_state": (None, [VP, VP]),
         "orc_envs_set_state": (None, [VP, VP]),
         "orc_envs_reset": (None, [VP, VP, VP]),
@@ -169,6 +170,19 @@ class Envs:
         f = np.ascontiguousarray(forces, dtype=np.float32)
         assert f.shape == (self.B, self.cfg.initial_force_steps, 2, 2)
         self.lib.orc_envs_set_bump_forces(self.h, _ptr(f))
+
+    def set_lqr(self, gains, per_env=False, state8=False, done_pos=0.0, done_angle=0.0):
+        """cp_set_lqr restated (random_action_agent.py:60-135); gains None = off.
+        With state8, later steps fill self.state8 (B, R, S, 2, 8)."""
+        if gains is None:
+            self._gains = self.state8 = None
+            self.lib.orc_envs_set_lqr(self.h, None, 0, None, 0.0, 0.0)
+            return
+        self._gains = np.ascontiguousarray(gains, dtype=np.float32)
+        assert self._gains.shape == ((self.B,) if per_env else ()) + (2, 2, 8), self._gains.shape
+        self.state8 = np.zeros((self.B, self.R, self.S, 2, 8), np.float32) if state8 else None
+        self.lib.orc_envs_set_lqr(self.h, _ptr(self._gains), int(bool(per_env)), _ptr(self.state8),
+                                  float(done_pos), float(done_angle))
 
     def get_state(self):
         s = np.empty((abi.CP_STATE_FIELDS, self.B), np.float32)
