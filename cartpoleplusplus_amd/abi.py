@@ -157,6 +157,7 @@ class cp_replay(C.Structure):
         ("free_slots", C.c_void_p),
         ("ctrl", C.c_void_p),
         ("plan", C.c_void_p),
+        ("scan", C.c_void_p),
     ]
 
 

@@ -1117,7 +1117,7 @@ int cp_get_stepped(cp_handle* h, uint8_t* out, void* stream) {
 /* ---- replay memory (cp_replay.h) ---- */
 static int replay_ok(const cp_replay* rm, const char* what) {
     if (!rm || !rm->state || !rm->state_1_idx || !rm->action || !rm->reward || !rm->terminal_mask ||
-        !rm->state_2_idx || !rm->free_slots || !rm->ctrl || !rm->plan)
+        !rm->state_2_idx || !rm->free_slots || !rm->ctrl || !rm->plan || !rm->scan)
         return fail(nullptr, std::string(what) + ": null replay buffer");
     if (rm->buffer_size < 1 || rm->state_dim < 1 || rm->action_dim < 1 ||
         rm->state_buffer_size < rm->buffer_size + rm->buffer_size / 2)
@@ -1151,7 +1151,10 @@ int cp_replay_add(const cp_replay* rm, int32_t* cur, int rows, const uint8_t* va
         return fail(nullptr, "cp_replay_add: bad state kind");
     if (!valid && !restart) return 0;
     const hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(cprm::plan_kernel, dim3(1), dim3(cprm::PLAN_THREADS), 0, st, *rm, rows, valid, restart);
+    const dim3 nb((unsigned)((rows + cprm::PLAN_THREADS - 1) / cprm::PLAN_THREADS)), nt(cprm::PLAN_THREADS);
+    hipLaunchKernelGGL(cprm::count_kernel, nb, nt, 0, st, *rm, rows, valid);
+    hipLaunchKernelGGL(cprm::free_count_kernel, nb, nt, 0, st, *rm, rows, valid, restart);
+    hipLaunchKernelGGL(cprm::plan_kernel, nb, nt, 0, st, *rm, rows, valid, restart);
     switch (cprm::vec_for(rm->state_dim, state_kind)) {
         case 8: cprm::launch_write<8>(rm, rows, cur, actions, action_kind, reward, done, restart, next_states,
                                        terminal_states, state_kind, st); break;

@@ -5,9 +5,9 @@
 // state_2.  For a batch of rows the slot bookkeeping is a pure prefix-sum
 // problem: row j's event lands at insert + (valid rows before j), its frees are
 // appended at tail + (frees before j) and its pops read head + (pops before j).
-// So one small scan kernel (one workgroup, rows in chunks of 1024) fixes every
-// position and pushes the freed slots; a wide kernel then does the HBM work (state
-// rows, event fields) for all rows in parallel.  The result is identical to the
+// So three short scan passes over blocks of 1024 rows (count valid rows; count frees
+// and pops; fix every position and push the freed slots) plan the batch, and a wide
+// kernel then does the HBM work (state rows, event fields) for all rows in parallel.  The result is identical to the
 // sequential reference order, FIFO contents included.
 #pragma once
 
@@ -47,62 +47,109 @@ __device__ inline int64_t block_exclusive_scan(int64_t x, int64_t* total, int64_
     return r;
 }
 
-// plan[2j] = event position of row j (-1: no event); plan[2j+1] = its first pop's
-// free-ring position (-1: no pop).  Frees are pushed here, before any pop reads them.
+// sum of a[0..n) over the block (every thread gets it)
+__device__ inline int64_t block_sum(const int64_t* a, int n, int64_t* lds) {
+    int64_t x = 0;
+    for (int k = threadIdx.x; k < n; k += PLAN_THREADS) x += a[k];
+    int64_t tot;
+    block_exclusive_scan(x, &tot, lds);
+    return tot;
+}
+
+// Three passes over blocks of 1024 rows; scan[] = blockV[nb] | blockFP[nb] | ctrl snapshot.
+// Pass 1: valid rows per block, and the ctrl snapshot the later passes read (pass 3
+// rewrites ctrl).
+__global__ void __launch_bounds__(PLAN_THREADS) count_kernel(cp_replay rm, int rows, const uint8_t* valid) {
+    __shared__ int64_t lds[2 * PLAN_WAVES + 1];
+    const int nb = (rows + PLAN_THREADS - 1) / PLAN_THREADS;
+    const int j = blockIdx.x * PLAN_THREADS + threadIdx.x;
+    const int v = (j < rows && valid && valid[j]) ? 1 : 0;
+    int64_t tot;
+    block_exclusive_scan(v, &tot, lds);
+    if (threadIdx.x == 0) rm.scan[blockIdx.x] = tot;
+    if (blockIdx.x == 0 && threadIdx.x < CP_RM_CTRL) rm.scan[2 * nb + threadIdx.x] = rm.ctrl[threadIdx.x];
+}
+
+struct RowPlan {
+    int v, r, f, p;
+    int64_t pos;
+};
+
+// row j's event position and free / pop counts (needs the global valid prefix)
+__device__ inline RowPlan row_plan(const cp_replay& rm, int rows, const uint8_t* valid, const uint8_t* restart,
+                                   int64_t* lds) {
+    const int nb = (rows + PLAN_THREADS - 1) / PLAN_THREADS;
+    const int64_t* snap = rm.scan + 2 * nb;
+    const int64_t N = rm.buffer_size, insert = snap[CP_RM_INSERT];
+    const bool full = snap[CP_RM_FULL] != 0;
+    const int j = blockIdx.x * PLAN_THREADS + threadIdx.x;
+    RowPlan q;
+    q.v = (j < rows && valid && valid[j]) ? 1 : 0;
+    q.r = (j < rows && restart && restart[j]) ? 1 : 0;
+    const int64_t Kb = block_sum(rm.scan, blockIdx.x, lds);
+    int64_t kv;
+    const int64_t k = Kb + block_exclusive_scan(q.v, &kv, lds);
+    q.pos = -1;
+    q.f = 0;
+    if (q.v) {
+        const int64_t g = insert + k;  // < 2N: rows <= N
+        q.pos = g >= N ? g - N : g;
+        if (full || g >= N) q.f = rm.terminal_mask[q.pos] == 0.f ? 2 : 1;  // :80-91
+    }
+    q.p = q.v + q.r;
+    return q;
+}
+
+// Pass 2: frees and pops per block (packed f | p << 32).
+__global__ void __launch_bounds__(PLAN_THREADS) free_count_kernel(cp_replay rm, int rows, const uint8_t* valid,
+                                                                  const uint8_t* restart) {
+    __shared__ int64_t lds[2 * PLAN_WAVES + 1];
+    const int nb = (rows + PLAN_THREADS - 1) / PLAN_THREADS;
+    const RowPlan q = row_plan(rm, rows, valid, restart, lds);
+    int64_t tot;
+    block_exclusive_scan((int64_t)q.f | ((int64_t)q.p << 32), &tot, lds);
+    if (threadIdx.x == 0) rm.scan[nb + blockIdx.x] = tot;
+}
+
+// Pass 3: plan[2j] = event position of row j (-1: no event), plan[2j+1] = its first
+// pop's free-ring position (-1: no pop); the freed slots are pushed here, before any
+// pop reads them (write_kernel).  The last block publishes the new ctrl.
 __global__ void __launch_bounds__(PLAN_THREADS) plan_kernel(cp_replay rm, int rows, const uint8_t* valid,
                                                             const uint8_t* restart) {
     __shared__ int64_t lds[2 * PLAN_WAVES + 1];
-    __shared__ int err;
-    int64_t* ctrl = rm.ctrl;
-    const int64_t N = rm.buffer_size, S = rm.state_buffer_size;
-    const int64_t insert = ctrl[CP_RM_INSERT], head = ctrl[CP_RM_HEAD], tail = ctrl[CP_RM_TAIL];
-    const bool full = ctrl[CP_RM_FULL] != 0;
-    if (threadIdx.x == 0) err = 0;
-    int64_t K = 0, F = 0, P = 0, E2 = 0;  // events, frees, pops, s2 evictions so far
-    for (int base = 0; base < rows; base += PLAN_THREADS) {
-        const int j = base + threadIdx.x;
-        const int v = (j < rows && valid && valid[j]) ? 1 : 0;
-        const int r = (j < rows && restart && restart[j]) ? 1 : 0;
-        int64_t kv;
-        const int64_t k = block_exclusive_scan(v, &kv, lds);
-        int64_t pos = -1;
-        int f = 0;
-        if (v) {
-            const int64_t g = insert + K + k;  // < 2N: rows <= N
-            pos = g >= N ? g - N : g;
-            if (full || g >= N) f = rm.terminal_mask[pos] == 0.f ? 2 : 1;  // :80-91
-        }
-        const int p = v + r;
-        int64_t tot;
-        const int64_t ex = block_exclusive_scan((int64_t)f | ((int64_t)p << 32), &tot, lds);
-        const int64_t fj = ex & 0xffffffffll, pj = ex >> 32;
-        if (f) {
-            const int64_t a = tail + F + fj;
-            rm.free_slots[a % S] = rm.state_1_idx[pos];
-            if (f == 2) rm.free_slots[(a + 1) % S] = rm.state_2_idx[pos];
-        }
-        // sequential order: row j's pops come after its own frees
-        if (p && head + P + pj + p > tail + F + fj + f) err = 1;
-        if (j < rows) {
-            rm.plan[2 * j] = (int32_t)pos;
-            rm.plan[2 * j + 1] = p ? (int32_t)((head + P + pj) % S) : -1;
-        }
-        int64_t e2;
-        block_exclusive_scan(f == 2 ? 1 : 0, &e2, lds);
-        K += kv;
-        F += tot & 0xffffffffll;
-        P += tot >> 32;
-        E2 += e2;
+    const int nb = (rows + PLAN_THREADS - 1) / PLAN_THREADS;
+    const int64_t* snap = rm.scan + 2 * nb;
+    const int64_t S = rm.state_buffer_size, head = snap[CP_RM_HEAD], tail = snap[CP_RM_TAIL];
+    const RowPlan q = row_plan(rm, rows, valid, restart, lds);
+    const int j = blockIdx.x * PLAN_THREADS + threadIdx.x;
+    const int64_t FPb = block_sum(rm.scan + nb, blockIdx.x, lds);
+    int64_t tot;
+    const int64_t ex = FPb + block_exclusive_scan((int64_t)q.f | ((int64_t)q.p << 32), &tot, lds);
+    const int64_t fj = ex & 0xffffffffll, pj = ex >> 32;
+    if (q.f) {
+        const int64_t a = tail + fj;
+        rm.free_slots[a % S] = rm.state_1_idx[q.pos];
+        if (q.f == 2) rm.free_slots[(a + 1) % S] = rm.state_2_idx[q.pos];
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        ctrl[CP_RM_INSERT] = (insert + K) % N;
-        ctrl[CP_RM_FULL] = (full || insert + K >= N) ? 1 : 0;
-        ctrl[CP_RM_HEAD] = head + P;
-        ctrl[CP_RM_TAIL] = tail + F;
-        ctrl[CP_RM_ADDS] += K;
-        ctrl[CP_RM_EVICTED_S2] += E2;
-        if (err) ctrl[CP_RM_ERROR] |= 1;
+    // sequential order: row j's pops come after its own frees
+    if (q.p && head + pj + q.p > tail + fj + q.f) atomicOr((unsigned long long*)&rm.ctrl[CP_RM_ERROR], 1ull);
+    if (j < rows) {
+        rm.plan[2 * j] = (int32_t)q.pos;
+        rm.plan[2 * j + 1] = q.p ? (int32_t)((head + pj) % S) : -1;
+    }
+    int64_t e2;
+    block_exclusive_scan(q.f == 2 ? 1 : 0, &e2, lds);
+    if (threadIdx.x == 0 && e2) atomicAdd((unsigned long long*)&rm.ctrl[CP_RM_EVICTED_S2], (unsigned long long)e2);
+    if (blockIdx.x == nb - 1) {
+        const int64_t K = block_sum(rm.scan, nb, lds), FP = block_sum(rm.scan + nb, nb, lds);
+        if (threadIdx.x == 0) {
+            const int64_t N = rm.buffer_size, insert = snap[CP_RM_INSERT];
+            rm.ctrl[CP_RM_INSERT] = (insert + K) % N;
+            rm.ctrl[CP_RM_FULL] = (snap[CP_RM_FULL] || insert + K >= N) ? 1 : 0;
+            rm.ctrl[CP_RM_HEAD] = head + (FP >> 32);
+            rm.ctrl[CP_RM_TAIL] = tail + (FP & 0xffffffffll);
+            rm.ctrl[CP_RM_ADDS] = snap[CP_RM_ADDS] + K;
+        }
     }
 }
 

@@ -64,10 +64,11 @@ class ReplayMemory:
         # cur[j]: env j's current state_1 slot; the extra last row serves add_episode
         self.cur = torch.full((self.num_envs + 1,), -1, **i32)
         self.plan = torch.zeros(2 * (self.num_envs + 1), **i32)
+        self.scan = torch.zeros(2 * ((self.num_envs + 1024) // 1024) + abi.CP_RM_CTRL, dtype=torch.int64, device=dev)
         self._stepped = torch.zeros(max(self.num_envs, 1), dtype=torch.uint8, device=dev)
         self.rm = abi.cp_replay(N, S, self.state_dim, self.action_dim, *(
             t.data_ptr() for t in (self.state, self.state_1_idx, self.action, self.reward, self.terminal_mask,
-                                   self.state_2_idx, self.free_slot_ring, self.ctrl, self.plan)))
+                                   self.state_2_idx, self.free_slot_ring, self.ctrl, self.plan, self.scan)))
         self.seed, self._counter = int(seed), 0
         self.stats = collections.Counter()
         self._check(self.lib.cp_replay_init(C.byref(self.rm), _p(self.cur), self.num_envs + 1, self._stream()),

@@ -344,6 +344,7 @@ typedef struct cp_replay {
     int32_t* free_slots;        /* [S] FIFO ring */
     int64_t* ctrl;              /* [CP_RM_CTRL] */
     int32_t* plan;              /* [2 * max rows] scratch */
+    int64_t* scan;              /* [2 * ceil(max rows / 1024) + CP_RM_CTRL] scratch */
 } cp_replay;
 
 /* Empty memory: free_slots = 0..S-1 in order (:35), ctrl zeroed, cur[0..rows) = -1. */

@@ -218,3 +218,30 @@ def test_large_ring_invariants():
         exp, dn = keep[s_]
         assert torch.equal(b.state_2[m], exp[env[m]])
         assert torch.equal(b.terminal_mask[m, 0], 1.0 - dn[env[m]].float())
+
+
+def test_reset_from_event_log(tmp_path):
+    """replay_memory.py:40-61 over a log written by the GPU event-log path (f2)."""
+    from cartpoleplusplus_amd import event_log as EL
+    B, R = 8, 2
+    env = BatchedCartpole(B, 0, action_repeats=R, autoreset=True, max_episode_len=7, seed=4)
+    path = str(tmp_path / "roll.log")
+    log = EL.BatchedEventLog(env, path)
+    env.reset()
+    log.after_reset()
+    g = torch.Generator(device="cuda").manual_seed(1)
+    for _ in range(20):
+        a = torch.rand((B, 2, 2), device="cuda", generator=g) * 2 - 1
+        env.step(a)
+        log.after_step(a)
+    log.close()
+    rm = ReplayMemory(100, (R, 2, 7), 4, 1.5)
+    o = ReplayOracle(100, (R, 2, 7), 4, 1.5)
+    rm.reset_from_event_log(path)
+    for ep in EL.EventLogReader(path).entries():
+        init = EL.read_state_from_event(ep.event[0])
+        o.add_episode(init, [(e.action, e.reward, EL.read_state_from_event(e)) for e in ep.event[1:]])
+        if o.full:
+            break
+    assert rm.size() > 0
+    same_as_oracle(rm, o)

@@ -134,7 +134,7 @@ def test_replay_abi_rejects_bad_sizes():
     import ctypes as C
     from cartpoleplusplus_amd import abi, native
     lib = native.load()
-    rm = abi.cp_replay(10, 12, 4, 1, *([8] * 9))   # S < 1.5 N; non-null fake pointers, no launch
+    rm = abi.cp_replay(10, 12, 4, 1, *([8] * 10))   # S < 1.5 N; non-null fake pointers, no launch
     assert lib.cp_replay_init(C.byref(rm), None, 0, None) != 0
     assert b"1.5" in lib.cp_last_error(None)
     assert lib.cp_replay_add(None, None, 0, None, None, 0, None, None, None, None, None, 0, None) != 0
