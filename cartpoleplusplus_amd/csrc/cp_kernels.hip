@@ -52,7 +52,7 @@ struct Bufs {
     float* scratch;    // [4*CP_ISLAND_PAIRS][2B] manifold headers of the current substep, per lane
     uint64_t* stamps;  // [waves][8] diagnostic phase cycles (CP_STAMPS builds only)
     float* rposes;     // [B][R][4][7] repeat-end poses for the raster obs (NULL: raster off)
-    float4* rtable;    // [C][H*W][2] per-camera ray directions + ground hits (cp_raster_table_kernel)
+    float4* rtable;    // [C][H*W] (d, t_ground) then [C][H*W] uint8 ground class (cp_raster_table_kernel)
     int32_t* rlist;    // [B] envs to render after the step kernel
     int32_t* rcount;   // [1]
     uint8_t* stepped;  // [B] 1 = simulated by the last cp_step (event log: done-before envs are not logged)
@@ -763,8 +763,19 @@ void cp_destroy(cp_handle* h) {
 static int launch_render(cp_handle* h, const int32_t* list, const int32_t* count, hipStream_t st) {
     hipEvent_t* ev = timing_slot(h, 2);
     if (ev) CP_TRY(h, hipEventRecord(ev[0], st));
-    hipLaunchKernelGGL(cp::cp_render_kernel, dim3((unsigned)h->cfg.num_envs), dim3(cp::RT), 0, st, h->raster,
-                       h->cfg.phys, h->cfg.action_repeats, list, count, h->b.rposes, h->b.rtable, h->pixels);
+    const int C = h->raster.num_cameras, R = h->cfg.action_repeats, npx = h->raster.width * h->raster.height;
+    const uint8_t* cls = reinterpret_cast<const uint8_t*>(h->b.rtable + (size_t)C * npx);
+    const size_t small = (size_t)cp::render_small_lds(C, R, npx).total;
+    if (small <= (size_t)cp::SMALL_LDS_MAX) {  // one block per env, dense ray tests
+        hipLaunchKernelGGL(cp::cp_render_small_kernel, dim3((unsigned)h->cfg.num_envs),
+                           dim3(cp::RENDER_WAVES * cp::WAVE_R), small, st, h->raster, h->cfg.phys, R, list, count,
+                           h->b.rposes, h->b.rtable, cls, h->pixels);
+    } else {  // large frames: one wave per env
+        const size_t lds = (size_t)cp::RENDER_WAVES * cp::render_lds(C, R).total;
+        const unsigned grid = (unsigned)((h->cfg.num_envs + cp::RENDER_WAVES - 1) / cp::RENDER_WAVES);
+        hipLaunchKernelGGL(cp::cp_render_kernel, dim3(grid), dim3(cp::RENDER_WAVES * cp::WAVE_R), lds, st, h->raster,
+                           h->cfg.phys, R, list, count, h->b.rposes, h->b.rtable, cls, h->pixels);
+    }
     if (check(h, hipGetLastError(), "cp_render_kernel")) return -1;
     if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
     return 0;
@@ -1039,7 +1050,8 @@ int cp_set_raster(cp_handle* h, const cp_raster_config* rc, uint16_t* pixels_out
     const int npx = rc->width * rc->height;
     CP_TRY(h, hipMalloc((void**)&h->b.rtable, (size_t)rc->num_cameras * npx * 2 * sizeof(float4)));
     hipLaunchKernelGGL(cp::cp_raster_table_kernel, dim3(grid_for(npx, cp::RT), rc->num_cameras), dim3(cp::RT), 0, 0,
-                       h->raster, h->cfg.phys, h->b.rtable);
+                       h->raster, h->cfg.phys, h->b.rtable,
+                       reinterpret_cast<uint8_t*>(h->b.rtable + (size_t)rc->num_cameras * npx));
     CP_TRY(h, hipGetLastError());
     CP_TRY(h, hipDeviceSynchronize());
     return 0;

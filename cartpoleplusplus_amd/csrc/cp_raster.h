@@ -4,14 +4,13 @@
 // for every env, repeat r and camera c, an H x W RGB image of the 5 boxes, written
 // as float16 [H][W][3][C][R] per env, the reference's state layout (:299-306).
 //
-// One 256-thread block per env (taken from a compacted env list).  The block
-// stages the env's R poses and the cameras in LDS, projects every box to a
-// conservative screen rectangle per (camera, repeat) and tabulates the shaded
-// colour of every face; the per-pixel ray directions and the static ground's hits
-// come from a per-camera table built once (cp_raster_table_kernel).  Each wave
-// renders an 8 x 8 pixel tile (a thin pole's rectangle diverges few waves) for all
-// C x R frames; an 8-row band is staged in LDS in the reference's pixel order and
-// stored with 4-byte stores.
+// One wave per env (taken from a compacted env list).  The wave stages the env's R
+// poses in LDS, projects every box to a conservative screen rectangle per (camera,
+// repeat) and tabulates the shaded colour of every face; the per-pixel ray
+// directions and the static ground's hits come from a per-camera table built once
+// (cp_raster_table_kernel).  Strips of 64 consecutive pixels are contiguous in the
+// output: most pixels meet no box rectangle and take a static colour, so the kernel
+// is a stream of 16-byte stores with the ray tests confined to the boxes' rectangles.
 //
 // The per-pixel arithmetic is the oracle's (oracle/cp_oracle.c, raster section),
 // operation for operation; the rectangles only skip boxes a ray cannot hit.
@@ -23,7 +22,7 @@
 
 namespace cp {
 
-constexpr int RT = 256;           // threads per render block
+constexpr int RT = 256;           // threads per table block
 constexpr int WAVE_R = 64;        // lanes per wave
 constexpr int RMAX_FRAMES = 16;   // C * R frames per env staged in LDS (checked at cp_set_raster)
 
@@ -53,14 +52,6 @@ CP_DEV int to_u8(float x) {
     x = x > 1.0f ? 1.0f : (x < 0.0f ? 0.0f : x);
     return (int)(x * 255.0f + 0.5f);
 }
-
-// LDS layout of one env's scene
-struct Scene {
-    Cam cam[2];                             // camera bases
-    float ax[RMAX_FRAMES][CP_NUM_DYN][9];   // per repeat r (index < R) the body axes (columns)
-    float c[RMAX_FRAMES][CP_NUM_DYN][3];    // and centres
-    int16_t rect[2][RMAX_FRAMES][CP_NUM_BODIES][4];  // per camera, repeat, box: x0 x1 y0 y1 (pixels)
-};
 
 // conservative pixel rectangle of box (centre cc, axes A, half h) seen by camera k
 CP_DEV void box_rect(const Cam& k, V3 cc, const Axes& A, V3 h, float sxk, float syk, int W, int H, int16_t* out) {
@@ -126,8 +117,11 @@ CP_DEV bool ray_box_o(V3 d, const float o[3], const Axes& A, V3 h, float& t, int
 
 // Per camera and pixel, the ray direction and the static ground's hit: the same for
 // every env, computed once per raster configuration (cp_set_raster) with the render
-// kernel's own arithmetic.  table [C][H*W][2] float4: (d.xyz, t_ground), (hit, face).
-__global__ void __launch_bounds__(RT) cp_raster_table_kernel(cp_raster_config rc, cp_physics P, float4* table) {
+// kernel's own arithmetic.  tabd [C][H*W] float4 (d.xyz, t of the ground hit or
+// far_plane); cls [C][H*W] uint8: the ground face hit (axis * 2 + (sign > 0)), or 6 =
+// background.  A pixel no dynamic box can reach shows its class's colour.
+__global__ void __launch_bounds__(RT) cp_raster_table_kernel(cp_raster_config rc, cp_physics P, float4* tabd,
+                                                              uint8_t* cls) {
     const int W = rc.width, H = rc.height, npx = W * H;
     const int p = blockIdx.x * RT + threadIdx.x, cam = blockIdx.y;
     if (p >= npx) return;
@@ -143,77 +137,102 @@ __global__ void __launch_bounds__(RT) cp_raster_table_kernel(cp_raster_config rc
     const V3 oc = sub(k.eye, mk(0.0f, 0.0f, 0.0f));
     const float o[3] = {dot(oc, I3.a0), dot(oc, I3.a1), dot(oc, I3.a2)};
     float best = rc.far_plane;
-    int hit = -1, face = 0;
+    int face = 6;
     float t, sg;
     int ax;
     if (ray_box_o(d, o, I3, mk(P.half_extents[0][0], P.half_extents[0][1], P.half_extents[0][2]), t, ax, sg) &&
         t < best) {
         best = t;
-        hit = 0;
         face = ax * 2 + (sg > 0.0f ? 1 : 0);
     }
-    table[((size_t)cam * npx + p) * 2 + 0] = make_float4(d.x, d.y, d.z, best);
-    table[((size_t)cam * npx + p) * 2 + 1] = make_float4(__int_as_float(hit), __int_as_float(face), 0.0f, 0.0f);
+    tabd[(size_t)cam * npx + p] = make_float4(d.x, d.y, d.z, best);
+    cls[(size_t)cam * npx + p] = (uint8_t)face;
 }
 
+// Per-wave LDS carve-up of the render kernel (byte offsets, 16-byte aligned), for C
+// cameras and R repeats.
+struct RenderLds {
+    int ax, c, oloc, rect, face, stage, total;
+};
+__host__ __device__ inline RenderLds render_lds(int C, int R) {
+    RenderLds w;
+    int o = 0;
+    auto al = [](int x) { return (x + 15) & ~15; };
+    w.ax = o;    o = al(o + R * CP_NUM_DYN * 9 * 4);          // body axes (columns) per repeat
+    w.c = o;     o = al(o + R * CP_NUM_DYN * 3 * 4);          // body centres per repeat
+    w.oloc = o;  o = al(o + C * R * CP_NUM_DYN * 3 * 4);      // (eye - c) . a_i per camera, repeat, body
+    w.rect = o;  o = al(o + C * R * CP_NUM_DYN * 4 * 2);      // screen rectangle x0 x1 y0 y1
+    w.face = o;  o = al(o + R * CP_NUM_BODIES * 6 * 3 * 2);   // shaded face colours, float16 bits
+    w.stage = o; o = al(o + (WAVE_R * 3 * C * R + 8) * 2);    // one strip of 64 pixels (+ alignment slack)
+    w.total = o;
+    return w;
+}
+
+CP_DEV void wave_sync() {  // LDS written by some lanes, then read by others of the same wave
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+constexpr int RENDER_WAVES = 4;  // envs (one per wave) per render block
+
 // poses [B][R][4][7] (xyz, quat xyzw) -> pixels float16 [B][H][W][3][C][R] for the envs
-// in list[0 .. *count).  Per pixel and camera the ground (static) is tested once and
-// reused for every repeat; per (camera, repeat, body) the ray-independent terms are
-// precomputed in LDS.  The oracle evaluates the same expressions per frame, so the
-// images agree bit for bit.
-__global__ void __launch_bounds__(RT) cp_render_kernel(cp_raster_config rc, cp_physics P, int R, const int32_t* list,
-                                                        const int32_t* count, const float* poses, const float4* table,
-                                                        uint16_t* pixels) {
-    __shared__ Scene sc;
-    __shared__ float oloc[2][RMAX_FRAMES][CP_NUM_DYN][3];  // (eye - c) . a_i per camera, repeat, body
-    __shared__ uint16_t lut[256];                          // u8 -> float16 bits (:289-294)
-    // shaded colour of every face: [repeat][box][axis * 2 + (sign > 0)][channel] as float16
-    // bits (flat shading depends on the face only; same arithmetic as per pixel)
-    __shared__ uint16_t face[RMAX_FRAMES][CP_NUM_BODIES][6][3];
-    __shared__ uint16_t chunk[RT * 3 * RMAX_FRAMES];
-    if ((int)blockIdx.x >= *count) return;  // block-uniform
-    const int env = list[blockIdx.x];
-    const int W = rc.width, H = rc.height, C = rc.num_cameras;
-    const int per_px = 3 * C * R;           // halves per pixel
+// in list[0 .. *count), one env per wave.  Per (camera, repeat, body) the ray-independent
+// terms and a conservative screen rectangle go to the wave's LDS; the image is rendered
+// in strips of 64 consecutive pixels (one per lane), which are contiguous in the output:
+// a pixel outside every rectangle takes its static class colour, the others test the
+// boxes whose rectangle holds them in body order against the ground's t (the oracle
+// evaluates the same expressions per frame, so the images agree bit for bit).  Each
+// strip is staged in LDS in the reference's (3, C, R) pixel order at the output's
+// alignment and stored with 16-byte writes.
+__global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_kernel(
+    cp_raster_config rc, cp_physics P, int R, const int32_t* list, const int32_t* count, const float* poses,
+    const float4* tabd, const uint8_t* cls, uint16_t* pixels) {
+    extern __shared__ __align__(16) unsigned char render_lds_raw[];
+    const int wave = threadIdx.x / WAVE_R, lane = threadIdx.x % WAVE_R;
+    const int slot = blockIdx.x * RENDER_WAVES + wave;
+    if (slot >= *count) return;  // wave-uniform; the kernel has no block barriers
+    const int env = list[slot];
+    const int W = rc.width, H = rc.height, C = rc.num_cameras, npx = W * H;
+    const int per_px = 3 * C * R, F = C * R;
+    const RenderLds L = render_lds(C, R);
+    unsigned char* base = render_lds_raw + wave * L.total;
+    float* sax = reinterpret_cast<float*>(base + L.ax);
+    float* sc = reinterpret_cast<float*>(base + L.c);
+    float* soloc = reinterpret_cast<float*>(base + L.oloc);
+    int16_t* srect = reinterpret_cast<int16_t*>(base + L.rect);
+    uint16_t* sface = reinterpret_cast<uint16_t*>(base + L.face);
+    uint16_t* stage = reinterpret_cast<uint16_t*>(base + L.stage);
+
     const float* pe = poses + (size_t)env * R * CP_NUM_DYN * 7;
-    const int tid = threadIdx.x;
-    lut[tid] = u8_to_half(tid);
-    if (tid < R * CP_NUM_DYN) {
-        const int r = tid / CP_NUM_DYN, b = tid % CP_NUM_DYN;
-        const float* q = pe + (r * CP_NUM_DYN + b) * 7;
+    if (lane < R * CP_NUM_DYN) {
+        const float* q = pe + lane * 7;
         const Axes A = quat_axes(q[3], q[4], q[5], q[6]);
-        float* a9 = sc.ax[r][b];
+        float* a9 = sax + lane * 9;
         a9[0] = A.a0.x; a9[1] = A.a0.y; a9[2] = A.a0.z;
         a9[3] = A.a1.x; a9[4] = A.a1.y; a9[5] = A.a1.z;
         a9[6] = A.a2.x; a9[7] = A.a2.y; a9[8] = A.a2.z;
-        sc.c[r][b][0] = q[0]; sc.c[r][b][1] = q[1]; sc.c[r][b][2] = q[2];
+        sc[lane * 3 + 0] = q[0]; sc[lane * 3 + 1] = q[1]; sc[lane * 3 + 2] = q[2];
     }
-    if (tid < C) sc.cam[tid] = make_cam(rc, tid);
-    __syncthreads();
+    wave_sync();
     const float syk = rc.tan_half_fov;
     const float sxk = rc.tan_half_fov * ((float)W / (float)H);
-    if (tid < C * R * CP_NUM_BODIES) {
-        const int cam = tid / (R * CP_NUM_BODIES), r = (tid / CP_NUM_BODIES) % R, b = tid % CP_NUM_BODIES;
-        const Cam k = sc.cam[cam];
-        V3 cc;
+    if (lane < F * CP_NUM_DYN) {  // item (cam, r, dyn body)
+        const int cam = lane / (R * CP_NUM_DYN), rb = lane % (R * CP_NUM_DYN), b = rb % CP_NUM_DYN;
+        const Cam k = make_cam(rc, cam);
+        const float* a9 = sax + rb * 9;
         Axes A;
-        if (b == 0) {
-            cc = mk(0.0f, 0.0f, 0.0f);
-            A.a0 = mk(1.0f, 0.0f, 0.0f); A.a1 = mk(0.0f, 1.0f, 0.0f); A.a2 = mk(0.0f, 0.0f, 1.0f);
-        } else {
-            const float* a9 = sc.ax[r][b - 1];
-            cc = mk(sc.c[r][b - 1][0], sc.c[r][b - 1][1], sc.c[r][b - 1][2]);
-            A.a0 = mk(a9[0], a9[1], a9[2]); A.a1 = mk(a9[3], a9[4], a9[5]); A.a2 = mk(a9[6], a9[7], a9[8]);
-            const V3 oc = sub(k.eye, cc);
-            oloc[cam][r][b - 1][0] = dot(oc, A.a0);  // (the oracle's ray_box computes these per ray)
-            oloc[cam][r][b - 1][1] = dot(oc, A.a1);
-            oloc[cam][r][b - 1][2] = dot(oc, A.a2);
-        }
-        box_rect(k, cc, A, mk(P.half_extents[b][0], P.half_extents[b][1], P.half_extents[b][2]), sxk, syk, W, H,
-                 sc.rect[cam][r][b]);
+        A.a0 = mk(a9[0], a9[1], a9[2]); A.a1 = mk(a9[3], a9[4], a9[5]); A.a2 = mk(a9[6], a9[7], a9[8]);
+        const V3 c = mk(sc[rb * 3 + 0], sc[rb * 3 + 1], sc[rb * 3 + 2]);
+        const V3 oc = sub(k.eye, c);
+        soloc[lane * 3 + 0] = dot(oc, A.a0);  // (the oracle's ray_box computes these per ray)
+        soloc[lane * 3 + 1] = dot(oc, A.a1);
+        soloc[lane * 3 + 2] = dot(oc, A.a2);
+        box_rect(k, c, A, mk(P.half_extents[b + 1][0], P.half_extents[b + 1][1], P.half_extents[b + 1][2]), sxk,
+                 syk, W, H, srect + lane * 4);
     }
     const V3 light = mk(rc.light[0], rc.light[1], rc.light[2]);
-    for (int it = tid; it < R * CP_NUM_BODIES * 6; it += RT) {
+    for (int it = lane; it < R * CP_NUM_BODIES * 6; it += WAVE_R) {  // [r][body][face]
         const int r = it / (CP_NUM_BODIES * 6), b = (it / 6) % CP_NUM_BODIES, fc = it % 6;
         const int ax = fc >> 1;
         const float sg = (fc & 1) ? 1.0f : -1.0f;
@@ -221,113 +240,293 @@ __global__ void __launch_bounds__(RT) cp_render_kernel(cp_raster_config rc, cp_p
         if (b == 0) {
             an = ax == 0 ? mk(1.0f, 0.0f, 0.0f) : (ax == 1 ? mk(0.0f, 1.0f, 0.0f) : mk(0.0f, 0.0f, 1.0f));
         } else {
-            const float* a9 = sc.ax[r][b - 1] + 3 * ax;
+            const float* a9 = sax + (r * CP_NUM_DYN + b - 1) * 9 + 3 * ax;
             an = mk(a9[0], a9[1], a9[2]);
         }
         const float ndl = dot(scl(an, sg), light);
         const float sh = fmaf_(rc.diffuse, ndl > 0.0f ? ndl : 0.0f, rc.ambient);
-        face[r][b][fc][0] = u8_to_half(to_u8(rc.color[b][0] * sh));
-        face[r][b][fc][1] = u8_to_half(to_u8(rc.color[b][1] * sh));
-        face[r][b][fc][2] = u8_to_half(to_u8(rc.color[b][2] * sh));
+        sface[it * 3 + 0] = u8_to_half(to_u8(rc.color[b][0] * sh));
+        sface[it * 3 + 1] = u8_to_half(to_u8(rc.color[b][1] * sh));
+        sface[it * 3 + 2] = u8_to_half(to_u8(rc.color[b][2] * sh));
     }
-    __syncthreads();
-    const uint16_t bgh0 = lut[to_u8(rc.background[0])], bgh1 = lut[to_u8(rc.background[1])],
-                   bgh2 = lut[to_u8(rc.background[2])];
-    const int npx = W * H;
-    uint16_t* out = pixels + (size_t)env * npx * per_px;
-    const bool words = (npx * per_px) % 2 == 0 && ((size_t)env * npx * per_px) % 2 == 0;
+    const uint16_t bg0 = u8_to_half(to_u8(rc.background[0])), bg1 = u8_to_half(to_u8(rc.background[1])),
+                   bg2 = u8_to_half(to_u8(rc.background[2]));
+    wave_sync();
 
-    // all C x R frames of pixel (px, py) -> dst[(ch * C + cam) * R + r] (the reference's
-    // (3, C, R) order within a pixel)
-    auto render_px = [&](int px, int py, uint64_t near, uint16_t* dst) {
+    uint16_t* out = pixels + (size_t)env * npx * per_px;
+    const int RB = R * CP_NUM_DYN;  // near bits per camera
+    const uint64_t cam_mask = RB >= 64 ? ~0ull : ((1ull << RB) - 1ull);
+    for (int p0 = 0; p0 < npx; p0 += WAVE_R) {
+        const int p = p0 + lane;
+        const bool valid = p < npx;
+        const int pl = valid ? p : npx - 1;
+        const int py = pl / W, px = pl - py * W;
+        const int last = (p0 + WAVE_R - 1 < npx ? p0 + WAVE_R - 1 : npx - 1);
+        const int yA = p0 / W, yB = last / W;
+        const int xA = yA == yB ? p0 - yA * W : 0, xB = yA == yB ? last - yB * W : W - 1;
+        // (camera, repeat, body) items whose rectangle meets the strip: one bit each
+        bool ov = false;
+        if (lane < F * CP_NUM_DYN) {
+            const int16_t* q = srect + lane * 4;
+            ov = q[0] <= xB && q[1] >= xA && q[2] <= yB && q[3] >= yA;
+        }
+        const uint64_t near = __ballot(ov);
+        uint16_t* dst = out + (size_t)p0 * per_px;
+        const int sh = (int)((reinterpret_cast<uintptr_t>(dst) & 15) >> 1);  // halves before dst in its 16 B
+        uint16_t* sp = stage + sh + lane * per_px;
         for (int cam = 0; cam < C; ++cam) {
-            // ray direction and the static ground's hit, from the per-camera table
-            const float4 t0 = table[((size_t)cam * npx + py * W + px) * 2 + 0];
-            const float4 t1 = table[((size_t)cam * npx + py * W + px) * 2 + 1];
-            const V3 d = mk(t0.x, t0.y, t0.z);
-            const float best0 = t0.w;
-            const int hit0 = __float_as_int(t1.x), face0 = __float_as_int(t1.y);
+            const int cl = cls[(size_t)cam * npx + pl];
+            const uint64_t nc = (near >> (cam * RB)) & cam_mask;
+            bool need = false;
+            if (nc) {  // wave-uniform
+                for (int k = 0; k < RB; ++k) {
+                    if (!((nc >> k) & 1ull)) continue;
+                    const int16_t* q = srect + (cam * RB + k) * 4;
+                    need = need || (px >= q[0] && px <= q[1] && py >= q[2] && py <= q[3]);
+                }
+            }
+            float4 t0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (need) t0 = tabd[(size_t)cam * npx + pl];
             for (int r = 0; r < R; ++r) {
-                float best = best0;
-                int hit = hit0, fc = face0;
+                int hit = cl < 6 ? 0 : -1, fc = cl;
+                const uint32_t nr = (uint32_t)(nc >> (r * CP_NUM_DYN)) & 15u;
+                if (nr && need) {
+                    const V3 d = mk(t0.x, t0.y, t0.z);
+                    float best = t0.w;
 #pragma unroll
-                for (int b = 1; b < CP_NUM_BODIES; ++b) {
-                    if (!((near >> ((cam * R + r) * 4 + b - 1)) & 1ull)) continue;  // wave-uniform
-                    const int16_t* rect = sc.rect[cam][r][b];
-                    if (px < rect[0] || px > rect[1] || py < rect[2] || py > rect[3]) continue;
-                    const float* a9 = sc.ax[r][b - 1];
-                    Axes A;
-                    A.a0 = mk(a9[0], a9[1], a9[2]); A.a1 = mk(a9[3], a9[4], a9[5]); A.a2 = mk(a9[6], a9[7], a9[8]);
-                    const V3 h = mk(P.half_extents[b][0], P.half_extents[b][1], P.half_extents[b][2]);
-                    float t, sg;
-                    int ax;
-                    if (ray_box_o(d, oloc[cam][r][b - 1], A, h, t, ax, sg) && t < best) {
-                        best = t;
-                        hit = b;
-                        fc = ax * 2 + (sg > 0.0f ? 1 : 0);
+                    for (int b = 1; b < CP_NUM_BODIES; ++b) {
+                        if (!((nr >> (b - 1)) & 1u)) continue;
+                        const int item = (cam * R + r) * CP_NUM_DYN + b - 1;
+                        const int16_t* q = srect + item * 4;
+                        if (px < q[0] || px > q[1] || py < q[2] || py > q[3]) continue;
+                        const float* a9 = sax + (r * CP_NUM_DYN + b - 1) * 9;
+                        Axes A;
+                        A.a0 = mk(a9[0], a9[1], a9[2]); A.a1 = mk(a9[3], a9[4], a9[5]);
+                        A.a2 = mk(a9[6], a9[7], a9[8]);
+                        const V3 h = mk(P.half_extents[b][0], P.half_extents[b][1], P.half_extents[b][2]);
+                        float t, sg;
+                        int ax;
+                        if (ray_box_o(d, soloc + item * 3, A, h, t, ax, sg) && t < best) {
+                            best = t;
+                            hit = b;
+                            fc = ax * 2 + (sg > 0.0f ? 1 : 0);
+                        }
                     }
                 }
-                uint16_t h0 = bgh0, h1 = bgh1, h2 = bgh2;
+                uint16_t h0 = bg0, h1 = bg1, h2 = bg2;
                 if (hit >= 0) {
-                    const uint16_t* fh = face[r][hit][fc];
+                    const uint16_t* fh = sface + ((r * CP_NUM_BODIES + hit) * 6 + fc) * 3;
                     h0 = fh[0];
                     h1 = fh[1];
                     h2 = fh[2];
                 }
-                uint16_t* o = dst + cam * R + r;
-                o[0] = h0;
-                o[C * R] = h1;
-                o[2 * C * R] = h2;
-            }
-        }
-    };
-    // copy `n` staged halves to out[first ...] (a contiguous span of the image)
-    auto flush = [&](size_t first, int n) {
-        if (words) {
-            const uint32_t* src = reinterpret_cast<const uint32_t*>(chunk);
-            uint32_t* dst = reinterpret_cast<uint32_t*>(out + first);
-            for (int w = tid; w < n / 2; w += RT) dst[w] = src[w];
-        } else {
-            for (int w = tid; w < n; w += RT) out[first + w] = chunk[w];
-        }
-    };
-    constexpr int TW = 8, TH = 8;  // one wave = an 8 x 8 pixel tile: a thin pole's rectangle
-                                   // then diverges few waves, where a row strip hits them all
-    constexpr int CHUNK = RT * 3 * RMAX_FRAMES;
-    if (TH * W * per_px <= CHUNK) {
-        // 8-row bands; per pass the 4 waves take 4 tiles side by side
-        const int wv = tid / WAVE_R, ln = tid % WAVE_R;
-        for (int y0 = 0; y0 < H; y0 += TH) {
-            const int rows = H - y0 < TH ? H - y0 : TH;
-            for (int x0 = 0; x0 < W; x0 += (RT / WAVE_R) * TW) {
-                const int tx = x0 + wv * TW;
-                const int px = tx + ln % TW, py = y0 + ln / TW;
-                // bodies whose rectangle meets this wave's tile, one bit per (camera, repeat,
-                // body): lane l tests item l, a ballot gathers them
-                bool ov = false;
-                if (ln < C * R * 4) {
-                    const int16_t* rect = sc.rect[ln / (R * 4)][(ln / 4) % R][ln % 4 + 1];
-                    ov = rect[0] <= tx + TW - 1 && rect[1] >= tx && rect[2] <= y0 + TH - 1 && rect[3] >= y0;
+                if (valid) {
+                    sp[cam * R + r] = h0;
+                    sp[F + cam * R + r] = h1;
+                    sp[2 * F + cam * R + r] = h2;
                 }
-                const uint64_t near = __ballot(ov);
-                if (px < W && py < H) render_px(px, py, near, chunk + ((py - y0) * W + px) * per_px);
             }
-            __syncthreads();
-            flush((size_t)y0 * W * per_px, rows * W * per_px);
-            __syncthreads();
         }
-    } else {
-        // wide images: row-major chunks of RT pixels
-        for (int base = 0; base < npx; base += RT) {
-            const int p = base + tid;
-            if (p < npx) {
-                const int py = p / W;
-                render_px(p - py * W, py, ~0ull, chunk + tid * per_px);
+        wave_sync();
+        // copy the strip: 16-byte blocks of the aligned span, partial blocks by halves
+        const int nh = ((npx - p0) < WAVE_R ? (npx - p0) : WAVE_R) * per_px;
+        const int tot = sh + nh;
+        uint4* d4 = reinterpret_cast<uint4*>(dst - sh);
+        const uint4* s4 = reinterpret_cast<const uint4*>(stage);
+        for (int k = lane; k * 8 < tot; k += WAVE_R) {
+            const int h0 = k * 8;
+            if (h0 >= sh && h0 + 8 <= tot) {
+                d4[k] = s4[k];
+            } else {
+                for (int e = (h0 > sh ? h0 : sh); e < (h0 + 8 < tot ? h0 + 8 : tot); ++e) dst[e - sh] = stage[e];
             }
-            __syncthreads();
-            flush((size_t)base * per_px, (npx - base < RT ? npx - base : RT) * per_px);
-            __syncthreads();
         }
+        wave_sync();
+    }
+}
+
+// ---- small frames (the reference's 50 x 50): one block per env, dense ray tests ----
+// Every box is tested only over its own screen rectangle, densely (thread k of the
+// block takes the rectangle's k-th pixel), one body after another in body order, per
+// frame; the nearest hit so far lives in an LDS depth / id buffer of the frame (id
+// 0xFF = no box yet, so the comparison is against the ground's t from the table).
+// That is the sequential "t < best" scan of the oracle with the pixels of one body
+// in parallel.  A second pass turns ids (or the static ground class) into colours and
+// streams strips of 64 pixels out as in cp_render_kernel.
+struct SmallLds {
+    int scene, best, id, stage, total;
+    RenderLds w;  // the scene part (its own stage field unused)
+};
+__host__ __device__ inline SmallLds render_small_lds(int C, int R, int npx) {
+    SmallLds s;
+    s.w = render_lds(C, R);
+    s.scene = 0;
+    int o = s.w.stage;  // scene arrays end where the per-wave stage began
+    s.best = o;  o = (o + npx * 4 + 15) & ~15;
+    s.id = o;    o = (o + C * R * npx + 15) & ~15;
+    s.stage = o; o = (o + RENDER_WAVES * (WAVE_R * 3 * C * R + 8) * 2 + 15) & ~15;
+    s.total = o;
+    return s;
+}
+constexpr int SMALL_LDS_MAX = 48 * 1024;  // keeps >= 3 blocks (12 waves) per CU
+
+__global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small_kernel(
+    cp_raster_config rc, cp_physics P, int R, const int32_t* list, const int32_t* count, const float* poses,
+    const float4* tabd, const uint8_t* cls, uint16_t* pixels) {
+    extern __shared__ __align__(16) unsigned char render_lds_raw[];
+    if ((int)blockIdx.x >= *count) return;  // block-uniform
+    const int env = list[blockIdx.x];
+    const int tid = threadIdx.x, wave = tid / WAVE_R, lane = tid % WAVE_R;
+    constexpr int NT = RENDER_WAVES * WAVE_R;
+    const int W = rc.width, H = rc.height, C = rc.num_cameras, npx = W * H;
+    const int per_px = 3 * C * R, F = C * R;
+    const SmallLds L = render_small_lds(C, R, npx);
+    unsigned char* base = render_lds_raw;
+    float* sax = reinterpret_cast<float*>(base + L.w.ax);
+    float* sc = reinterpret_cast<float*>(base + L.w.c);
+    float* soloc = reinterpret_cast<float*>(base + L.w.oloc);
+    int16_t* srect = reinterpret_cast<int16_t*>(base + L.w.rect);
+    uint16_t* sface = reinterpret_cast<uint16_t*>(base + L.w.face);
+    float* sbest = reinterpret_cast<float*>(base + L.best);
+    uint8_t* sid = reinterpret_cast<uint8_t*>(base + L.id);
+    uint16_t* stage = reinterpret_cast<uint16_t*>(base + L.stage) + wave * (WAVE_R * per_px + 8);
+
+    const float* pe = poses + (size_t)env * R * CP_NUM_DYN * 7;
+    if (tid < R * CP_NUM_DYN) {
+        const float* q = pe + tid * 7;
+        const Axes A = quat_axes(q[3], q[4], q[5], q[6]);
+        float* a9 = sax + tid * 9;
+        a9[0] = A.a0.x; a9[1] = A.a0.y; a9[2] = A.a0.z;
+        a9[3] = A.a1.x; a9[4] = A.a1.y; a9[5] = A.a1.z;
+        a9[6] = A.a2.x; a9[7] = A.a2.y; a9[8] = A.a2.z;
+        sc[tid * 3 + 0] = q[0]; sc[tid * 3 + 1] = q[1]; sc[tid * 3 + 2] = q[2];
+    }
+    {  // no box hit yet in any frame
+        uint32_t* id4 = reinterpret_cast<uint32_t*>(sid);
+        for (int k = tid; k < (F * npx + 3) / 4; k += NT) id4[k] = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    const float syk = rc.tan_half_fov;
+    const float sxk = rc.tan_half_fov * ((float)W / (float)H);
+    if (tid < F * CP_NUM_DYN) {
+        const int cam = tid / (R * CP_NUM_DYN), rb = tid % (R * CP_NUM_DYN), b = rb % CP_NUM_DYN;
+        const Cam k = make_cam(rc, cam);
+        const float* a9 = sax + rb * 9;
+        Axes A;
+        A.a0 = mk(a9[0], a9[1], a9[2]); A.a1 = mk(a9[3], a9[4], a9[5]); A.a2 = mk(a9[6], a9[7], a9[8]);
+        const V3 c = mk(sc[rb * 3 + 0], sc[rb * 3 + 1], sc[rb * 3 + 2]);
+        const V3 oc = sub(k.eye, c);
+        soloc[tid * 3 + 0] = dot(oc, A.a0);
+        soloc[tid * 3 + 1] = dot(oc, A.a1);
+        soloc[tid * 3 + 2] = dot(oc, A.a2);
+        int16_t q[4];
+        box_rect(k, c, A, mk(P.half_extents[b + 1][0], P.half_extents[b + 1][1], P.half_extents[b + 1][2]), sxk,
+                 syk, W, H, q);
+        // clipped to the image (empty: x0 > x1)
+        srect[tid * 4 + 0] = q[0] < 0 ? 0 : q[0];
+        srect[tid * 4 + 1] = q[1] > W - 1 ? (int16_t)(W - 1) : q[1];
+        srect[tid * 4 + 2] = q[2] < 0 ? 0 : q[2];
+        srect[tid * 4 + 3] = q[3] > H - 1 ? (int16_t)(H - 1) : q[3];
+    }
+    const V3 light = mk(rc.light[0], rc.light[1], rc.light[2]);
+    for (int it = tid; it < R * CP_NUM_BODIES * 6; it += NT) {
+        const int r = it / (CP_NUM_BODIES * 6), b = (it / 6) % CP_NUM_BODIES, fc = it % 6;
+        const int ax = fc >> 1;
+        const float sg = (fc & 1) ? 1.0f : -1.0f;
+        V3 an;
+        if (b == 0) {
+            an = ax == 0 ? mk(1.0f, 0.0f, 0.0f) : (ax == 1 ? mk(0.0f, 1.0f, 0.0f) : mk(0.0f, 0.0f, 1.0f));
+        } else {
+            const float* a9 = sax + (r * CP_NUM_DYN + b - 1) * 9 + 3 * ax;
+            an = mk(a9[0], a9[1], a9[2]);
+        }
+        const float ndl = dot(scl(an, sg), light);
+        const float sh = fmaf_(rc.diffuse, ndl > 0.0f ? ndl : 0.0f, rc.ambient);
+        sface[it * 3 + 0] = u8_to_half(to_u8(rc.color[b][0] * sh));
+        sface[it * 3 + 1] = u8_to_half(to_u8(rc.color[b][1] * sh));
+        sface[it * 3 + 2] = u8_to_half(to_u8(rc.color[b][2] * sh));
+    }
+    __syncthreads();
+
+    // dense ray tests: frame by frame, body by body
+    for (int f = 0; f < F; ++f) {
+        const int cam = f / R, r = f % R;
+        uint8_t* idf = sid + f * npx;
+        for (int b = 1; b < CP_NUM_BODIES; ++b) {
+            const int item = f * CP_NUM_DYN + b - 1;
+            const int x0 = srect[item * 4 + 0], x1 = srect[item * 4 + 1];
+            const int y0 = srect[item * 4 + 2], y1 = srect[item * 4 + 3];
+            if (x0 > x1 || y0 > y1) continue;  // block-uniform
+            const int rw = x1 - x0 + 1, area = rw * (y1 - y0 + 1);
+            const float* a9 = sax + (r * CP_NUM_DYN + b - 1) * 9;
+            Axes A;
+            A.a0 = mk(a9[0], a9[1], a9[2]); A.a1 = mk(a9[3], a9[4], a9[5]); A.a2 = mk(a9[6], a9[7], a9[8]);
+            const V3 h = mk(P.half_extents[b][0], P.half_extents[b][1], P.half_extents[b][2]);
+            const float* ol = soloc + item * 3;
+            for (int k = tid; k < area; k += NT) {
+                const int yy = k / rw, px = x0 + (k - yy * rw), py = y0 + yy;
+                const int p = py * W + px;
+                const float4 t0 = tabd[(size_t)cam * npx + p];
+                float t, sg;
+                int ax;
+                if (ray_box_o(mk(t0.x, t0.y, t0.z), ol, A, h, t, ax, sg)) {
+                    const uint8_t cur = idf[p];
+                    const float best = cur == 0xFF ? t0.w : sbest[p];
+                    if (t < best) {
+                        sbest[p] = t;
+                        idf[p] = (uint8_t)((b << 3) | (ax * 2 + (sg > 0.0f ? 1 : 0)));
+                    }
+                }
+            }
+            __syncthreads();  // the next body compares against this one's hits
+        }
+    }
+
+    // colours, strips of 64 pixels per wave
+    const uint16_t bg0 = u8_to_half(to_u8(rc.background[0])), bg1 = u8_to_half(to_u8(rc.background[1])),
+                   bg2 = u8_to_half(to_u8(rc.background[2]));
+    uint16_t* out = pixels + (size_t)env * npx * per_px;
+    for (int p0 = wave * WAVE_R; p0 < npx; p0 += RENDER_WAVES * WAVE_R) {
+        const int p = p0 + lane;
+        const bool valid = p < npx;
+        const int pl = valid ? p : npx - 1;
+        uint16_t* dst = out + (size_t)p0 * per_px;
+        const int sh = (int)((reinterpret_cast<uintptr_t>(dst) & 15) >> 1);
+        uint16_t* sp = stage + sh + lane * per_px;
+        for (int cam = 0; cam < C; ++cam) {
+            const int cl = cls[(size_t)cam * npx + pl];
+            for (int r = 0; r < R; ++r) {
+                const int v = sid[(cam * R + r) * npx + pl];
+                uint16_t h0 = bg0, h1 = bg1, h2 = bg2;
+                const int hit = v != 0xFF ? (v >> 3) : (cl < 6 ? 0 : -1);
+                const int fc = v != 0xFF ? (v & 7) : cl;
+                if (hit >= 0) {
+                    const uint16_t* fh = sface + ((r * CP_NUM_BODIES + hit) * 6 + fc) * 3;
+                    h0 = fh[0];
+                    h1 = fh[1];
+                    h2 = fh[2];
+                }
+                if (valid) {
+                    sp[cam * R + r] = h0;
+                    sp[F + cam * R + r] = h1;
+                    sp[2 * F + cam * R + r] = h2;
+                }
+            }
+        }
+        wave_sync();
+        const int nh = ((npx - p0) < WAVE_R ? (npx - p0) : WAVE_R) * per_px;
+        const int tot = sh + nh;
+        uint4* d4 = reinterpret_cast<uint4*>(dst - sh);
+        const uint4* s4 = reinterpret_cast<const uint4*>(stage);
+        for (int k = lane; k * 8 < tot; k += WAVE_R) {
+            const int h0 = k * 8;
+            if (h0 >= sh && h0 + 8 <= tot) {
+                d4[k] = s4[k];
+            } else {
+                for (int e = (h0 > sh ? h0 : sh); e < (h0 + 8 < tot ? h0 + 8 : tot); ++e) dst[e - sh] = stage[e];
+            }
+        }
+        wave_sync();
     }
 }
 

@@ -82,17 +82,18 @@ def test_other_sizes_and_done_envs_keep_pixels(oracle_mod):
     assert torch.equal(before, env.pixels)
 
 
-def test_wide_image_row_major_path(oracle_mod):
-    """100 x 20 x 2 cameras x 3 repeats does not fit the 8-row band staging: the
-    kernel's row-major chunk path."""
-    env = BatchedCartpole(6, 0, action_repeats=3, initial_force=55.0, seed=9)
-    env.enable_raster(True, width=100, height=20, num_cameras=2)
+@pytest.mark.parametrize("W,H,C,R", [(100, 20, 2, 3), (160, 120, 1, 2), (90, 70, 2, 2)])
+def test_large_frames_wave_path(oracle_mod, W, H, C, R):
+    """Frames whose depth / id buffers exceed the small-frame kernel's LDS budget go to
+    the one-wave-per-env kernel (160 x 120, 90 x 70 x 2 cameras); 100 x 20 stays small."""
+    env = BatchedCartpole(6, 0, action_repeats=R, initial_force=55.0, seed=9)
+    env.enable_raster(True, width=W, height=H, num_cameras=C)
     env.reset()
     env.step(torch.zeros((6, 2, 2), device="cuda"))
     pix = env.pixels.cpu().numpy()
     st = env.get_state().cpu().numpy()
     for e in range(6):
-        _check_env(oracle_mod, env, pix, st, e, 2)
+        _check_env(oracle_mod, env, pix, st, e, R - 1)
 
 
 def test_autoreset_frames_show_the_new_episode(oracle_mod):
