@@ -185,7 +185,7 @@ def main():
         per_launch_s = tm["render_ms"] / max(1, tm["render_launches"]) / 1e3  # one launch per step
         bytes_launch = B * render_kernel_bytes(rc.height, rc.width, rc.num_cameras, R)
         achieved = bytes_launch / per_launch_s / 1e9
-        kernel = "cp_render_kernel"
+        kernel = "cp_render_small_kernel"
         traffic, traffic_src = pmc_traffic(kernel, B, R)
     out = {
         "metric": METRIC,

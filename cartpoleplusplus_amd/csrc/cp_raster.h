@@ -80,10 +80,12 @@ CP_DEV void box_rect(const Cam& k, V3 cc, const Axes& A, V3 h, float sxk, float 
         return;
     }
     const float lim = 30000.0f;
-    out[0] = (int16_t)fmaxf(-lim, floorf(x0) - 2.0f);
-    out[1] = (int16_t)fminf(lim, ceilf(x1) + 2.0f);
-    out[2] = (int16_t)fmaxf(-lim, floorf(y0) - 2.0f);
-    out[3] = (int16_t)fminf(lim, ceilf(y1) + 2.0f);
+    // a pixel centre k is hit only if k lies in [x0, x1] up to rounding (~1e-4 px):
+    // floor / ceil plus one pixel covers it
+    out[0] = (int16_t)fmaxf(-lim, floorf(x0) - 1.0f);
+    out[1] = (int16_t)fminf(lim, ceilf(x1) + 1.0f);
+    out[2] = (int16_t)fmaxf(-lim, floorf(y0) - 1.0f);
+    out[3] = (int16_t)fminf(lim, ceilf(y1) + 1.0f);
 }
 
 // Ray (eye + t d) against a box with axes A and half extents h, given the origin-side
@@ -346,24 +348,27 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_kernel(
 }
 
 // ---- small frames (the reference's 50 x 50): one block per env, dense ray tests ----
-// Every box is tested only over its own screen rectangle, densely (thread k of the
-// block takes the rectangle's k-th pixel), one body after another in body order, per
-// frame; the nearest hit so far lives in an LDS depth / id buffer of the frame (id
-// 0xFF = no box yet, so the comparison is against the ground's t from the table).
-// That is the sequential "t < best" scan of the oracle with the pixels of one body
-// in parallel.  A second pass turns ids (or the static ground class) into colours and
-// streams strips of 64 pixels out as in cp_render_kernel.
+// Per frame an LDS code buffer holds, per pixel, what it shows: the static ground
+// class (face 0..5, or 30 = background) to start with, then body b's face f as
+// b * 6 + f once a box is nearer, with its depth in a depth buffer.  Every box is
+// tested only over its own screen rectangle, densely (thread k of the block takes the
+// rectangle's k-th pixel), one body after another in body order: the sequential
+// "t < best" scan of the oracle with the pixels of one body in parallel (a pixel still
+// showing the ground compares against the ground's t from the table).  The output
+// pass maps codes to colours through a per-repeat LUT and streams strips of 64
+// pixels out as cp_render_kernel does.
+constexpr int CODE_BG = 30;  // background; codes 0..29 = body * 6 + face (body 0 = ground)
 struct SmallLds {
-    int scene, best, id, stage, total;
-    RenderLds w;  // the scene part (its own stage field unused)
+    int lut, best, code, stage, total;
+    RenderLds w;  // the scene part (its own face / stage fields unused)
 };
 __host__ __device__ inline SmallLds render_small_lds(int C, int R, int npx) {
     SmallLds s;
     s.w = render_lds(C, R);
-    s.scene = 0;
-    int o = s.w.stage;  // scene arrays end where the per-wave stage began
+    int o = s.w.face;  // the scene arrays before the face table are shared with RenderLds
+    s.lut = o;   o = (o + R * 32 * 8 + 15) & ~15;  // [R][32] x 4 float16 (3 used)
     s.best = o;  o = (o + npx * 4 + 15) & ~15;
-    s.id = o;    o = (o + C * R * npx + 15) & ~15;
+    s.code = o;  o = (o + C * R * npx + 15) & ~15;
     s.stage = o; o = (o + RENDER_WAVES * (WAVE_R * 3 * C * R + 8) * 2 + 15) & ~15;
     s.total = o;
     return s;
@@ -386,9 +391,9 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small_kernel(
     float* sc = reinterpret_cast<float*>(base + L.w.c);
     float* soloc = reinterpret_cast<float*>(base + L.w.oloc);
     int16_t* srect = reinterpret_cast<int16_t*>(base + L.w.rect);
-    uint16_t* sface = reinterpret_cast<uint16_t*>(base + L.w.face);
+    uint2* slut = reinterpret_cast<uint2*>(base + L.lut);
     float* sbest = reinterpret_cast<float*>(base + L.best);
-    uint8_t* sid = reinterpret_cast<uint8_t*>(base + L.id);
+    uint8_t* scode = reinterpret_cast<uint8_t*>(base + L.code);
     uint16_t* stage = reinterpret_cast<uint16_t*>(base + L.stage) + wave * (WAVE_R * per_px + 8);
 
     const float* pe = poses + (size_t)env * R * CP_NUM_DYN * 7;
@@ -401,9 +406,12 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small_kernel(
         a9[6] = A.a2.x; a9[7] = A.a2.y; a9[8] = A.a2.z;
         sc[tid * 3 + 0] = q[0]; sc[tid * 3 + 1] = q[1]; sc[tid * 3 + 2] = q[2];
     }
-    {  // no box hit yet in any frame
-        uint32_t* id4 = reinterpret_cast<uint32_t*>(sid);
-        for (int k = tid; k < (F * npx + 3) / 4; k += NT) id4[k] = 0xFFFFFFFFu;
+    // every frame starts as the static ground / background (class 6 -> CODE_BG)
+    for (int k = tid; k < C * npx; k += NT) {
+        const int cl = cls[k];
+        const uint8_t code = (uint8_t)(cl < 6 ? cl : CODE_BG);
+        const int cam = k / npx, p = k - cam * npx;
+        for (int r = 0; r < R; ++r) scode[(cam * R + r) * npx + p] = code;
     }
     __syncthreads();
     const float syk = rc.tan_half_fov;
@@ -429,52 +437,59 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small_kernel(
         srect[tid * 4 + 3] = q[3] > H - 1 ? (int16_t)(H - 1) : q[3];
     }
     const V3 light = mk(rc.light[0], rc.light[1], rc.light[2]);
-    for (int it = tid; it < R * CP_NUM_BODIES * 6; it += NT) {
-        const int r = it / (CP_NUM_BODIES * 6), b = (it / 6) % CP_NUM_BODIES, fc = it % 6;
-        const int ax = fc >> 1;
-        const float sg = (fc & 1) ? 1.0f : -1.0f;
-        V3 an;
-        if (b == 0) {
-            an = ax == 0 ? mk(1.0f, 0.0f, 0.0f) : (ax == 1 ? mk(0.0f, 1.0f, 0.0f) : mk(0.0f, 0.0f, 1.0f));
+    for (int it = tid; it < R * 32; it += NT) {  // colour LUT [r][code]
+        const int r = it / 32, code = it % 32;
+        uint16_t h[3];
+        if (code < CP_NUM_BODIES * 6) {
+            const int b = code / 6, fc = code % 6, ax = fc >> 1;
+            const float sg = (fc & 1) ? 1.0f : -1.0f;
+            V3 an;
+            if (b == 0) {
+                an = ax == 0 ? mk(1.0f, 0.0f, 0.0f) : (ax == 1 ? mk(0.0f, 1.0f, 0.0f) : mk(0.0f, 0.0f, 1.0f));
+            } else {
+                const float* a9 = sax + (r * CP_NUM_DYN + b - 1) * 9 + 3 * ax;
+                an = mk(a9[0], a9[1], a9[2]);
+            }
+            const float ndl = dot(scl(an, sg), light);
+            const float sh = fmaf_(rc.diffuse, ndl > 0.0f ? ndl : 0.0f, rc.ambient);
+            for (int ch = 0; ch < 3; ++ch) h[ch] = u8_to_half(to_u8(rc.color[b][ch] * sh));
         } else {
-            const float* a9 = sax + (r * CP_NUM_DYN + b - 1) * 9 + 3 * ax;
-            an = mk(a9[0], a9[1], a9[2]);
+            for (int ch = 0; ch < 3; ++ch) h[ch] = u8_to_half(to_u8(rc.background[ch]));
         }
-        const float ndl = dot(scl(an, sg), light);
-        const float sh = fmaf_(rc.diffuse, ndl > 0.0f ? ndl : 0.0f, rc.ambient);
-        sface[it * 3 + 0] = u8_to_half(to_u8(rc.color[b][0] * sh));
-        sface[it * 3 + 1] = u8_to_half(to_u8(rc.color[b][1] * sh));
-        sface[it * 3 + 2] = u8_to_half(to_u8(rc.color[b][2] * sh));
+        slut[it] = make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2]);
     }
     __syncthreads();
 
     // dense ray tests: frame by frame, body by body
     for (int f = 0; f < F; ++f) {
         const int cam = f / R, r = f % R;
-        uint8_t* idf = sid + f * npx;
+        uint8_t* cf = scode + f * npx;
         for (int b = 1; b < CP_NUM_BODIES; ++b) {
             const int item = f * CP_NUM_DYN + b - 1;
             const int x0 = srect[item * 4 + 0], x1 = srect[item * 4 + 1];
             const int y0 = srect[item * 4 + 2], y1 = srect[item * 4 + 3];
             if (x0 > x1 || y0 > y1) continue;  // block-uniform
             const int rw = x1 - x0 + 1, area = rw * (y1 - y0 + 1);
+            const float inv_rw = 1.0f / (float)rw;
             const float* a9 = sax + (r * CP_NUM_DYN + b - 1) * 9;
             Axes A;
             A.a0 = mk(a9[0], a9[1], a9[2]); A.a1 = mk(a9[3], a9[4], a9[5]); A.a2 = mk(a9[6], a9[7], a9[8]);
             const V3 h = mk(P.half_extents[b][0], P.half_extents[b][1], P.half_extents[b][2]);
             const float* ol = soloc + item * 3;
             for (int k = tid; k < area; k += NT) {
-                const int yy = k / rw, px = x0 + (k - yy * rw), py = y0 + yy;
-                const int p = py * W + px;
+                int yy = (int)((float)k * inv_rw), xx = k - yy * rw;  // k / rw, corrected
+                if (xx < 0) { --yy; xx += rw; }
+                if (xx >= rw) { ++yy; xx -= rw; }
+                const int p = (y0 + yy) * W + x0 + xx;
                 const float4 t0 = tabd[(size_t)cam * npx + p];
                 float t, sg;
                 int ax;
                 if (ray_box_o(mk(t0.x, t0.y, t0.z), ol, A, h, t, ax, sg)) {
-                    const uint8_t cur = idf[p];
-                    const float best = cur == 0xFF ? t0.w : sbest[p];
+                    const int cur = cf[p];
+                    const float best = (cur < 6 || cur == CODE_BG) ? t0.w : sbest[p];
                     if (t < best) {
                         sbest[p] = t;
-                        idf[p] = (uint8_t)((b << 3) | (ax * 2 + (sg > 0.0f ? 1 : 0)));
+                        cf[p] = (uint8_t)(b * 6 + ax * 2 + (sg > 0.0f ? 1 : 0));
                     }
                 }
             }
@@ -483,8 +498,6 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small_kernel(
     }
 
     // colours, strips of 64 pixels per wave
-    const uint16_t bg0 = u8_to_half(to_u8(rc.background[0])), bg1 = u8_to_half(to_u8(rc.background[1])),
-                   bg2 = u8_to_half(to_u8(rc.background[2]));
     uint16_t* out = pixels + (size_t)env * npx * per_px;
     for (int p0 = wave * WAVE_R; p0 < npx; p0 += RENDER_WAVES * WAVE_R) {
         const int p = p0 + lane;
@@ -493,24 +506,12 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small_kernel(
         uint16_t* dst = out + (size_t)p0 * per_px;
         const int sh = (int)((reinterpret_cast<uintptr_t>(dst) & 15) >> 1);
         uint16_t* sp = stage + sh + lane * per_px;
-        for (int cam = 0; cam < C; ++cam) {
-            const int cl = cls[(size_t)cam * npx + pl];
-            for (int r = 0; r < R; ++r) {
-                const int v = sid[(cam * R + r) * npx + pl];
-                uint16_t h0 = bg0, h1 = bg1, h2 = bg2;
-                const int hit = v != 0xFF ? (v >> 3) : (cl < 6 ? 0 : -1);
-                const int fc = v != 0xFF ? (v & 7) : cl;
-                if (hit >= 0) {
-                    const uint16_t* fh = sface + ((r * CP_NUM_BODIES + hit) * 6 + fc) * 3;
-                    h0 = fh[0];
-                    h1 = fh[1];
-                    h2 = fh[2];
-                }
-                if (valid) {
-                    sp[cam * R + r] = h0;
-                    sp[F + cam * R + r] = h1;
-                    sp[2 * F + cam * R + r] = h2;
-                }
+        for (int f = 0; f < F; ++f) {
+            const uint2 c = slut[(f % R) * 32 + scode[f * npx + pl]];
+            if (valid) {
+                sp[f] = (uint16_t)c.x;
+                sp[F + f] = (uint16_t)(c.x >> 16);
+                sp[2 * F + f] = (uint16_t)c.y;
             }
         }
         wave_sync();

@@ -17,10 +17,15 @@ from collections import defaultdict
 
 def kernel_key(name):
     if "cp_step_kernel" in name:
-        return "cp_step_kernel<discrete>" if "<1>" in name else "cp_step_kernel<continuous>"
-    for k in ("cp_reset_kernel", "cp_init_kernel", "cp_mask_to_list_kernel", "cp_render_kernel"):
+        kind = "discrete" if ("<1>" in name or "<1," in name) else "continuous"
+        return f"cp_step_kernel<{kind}{',lqr' if 'true>' in name else ''}>"
+    for k in ("cp_reset_kernel", "cp_init_kernel", "cp_mask_to_list_kernel", "cp_render_small_kernel",
+              "cp_render_kernel", "cp_raster_table_kernel", "cp_event_kernel"):
         if k in name:
             return k
+    for k in ("count_kernel", "free_count_kernel", "plan_kernel", "write_kernel", "sample_kernel"):
+        if "cprm::" + k in name:
+            return "cp_replay_" + k
     return None
 
 
