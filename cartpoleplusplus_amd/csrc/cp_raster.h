@@ -170,6 +170,14 @@ __host__ __device__ inline RenderLds render_lds(int C, int R) {
     return w;
 }
 
+// 16-byte streaming (non-temporal) store: the frames are written once and read by the
+// consumer much later
+CP_DEV void store_stream(uint4* dst, uint4 q) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    v4u v = {q.x, q.y, q.z, q.w};
+    __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(dst));
+}
+
 CP_DEV void wave_sync() {  // LDS written by some lanes, then read by others of the same wave
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -338,7 +346,7 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_kernel(
         for (int k = lane; k * 8 < tot; k += WAVE_R) {
             const int h0 = k * 8;
             if (h0 >= sh && h0 + 8 <= tot) {
-                d4[k] = s4[k];
+                store_stream(&d4[k], s4[k]);
             } else {
                 for (int e = (h0 > sh ? h0 : sh); e < (h0 + 8 < tot ? h0 + 8 : tot); ++e) dst[e - sh] = stage[e];
             }
@@ -348,6 +356,8 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_kernel(
 }
 
 // ---- small frames (the reference's 50 x 50): one block per env, dense ray tests ----
+// (diagnostic builds: -DCP_RV_NO_DENSE / -DCP_RV_NO_OUTPUT / -DCP_RV_NO_STORE drop a
+// phase to time the others; tools/variant_raster.sh)
 // Per frame an LDS code buffer holds, per pixel, what it shows: the static ground
 // class (face 0..5, or 30 = background) to start with, then body b's face f as
 // b * 6 + f once a box is nearer, with its depth in a depth buffer.  Every box is
@@ -471,6 +481,7 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small_kernel(
     __syncthreads();
 
     // dense ray tests: frame by frame, body by body
+#ifndef CP_RV_NO_DENSE
     for (int f = 0; f < F; ++f) {
         const int cam = f / R, r = f % R;
         uint8_t* cf = scode + f * npx;
@@ -506,9 +517,13 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small_kernel(
             __syncthreads();  // the next body compares against this one's hits
         }
     }
+#endif
 
     // colours, strips of 64 pixels per wave
     uint16_t* out = pixels + (size_t)env * npx * per_px;
+#ifdef CP_RV_NO_OUTPUT
+    if (npx > 0) return;
+#endif
     for (int p0 = wave * WAVE_R; p0 < npx; p0 += RENDER_WAVES * WAVE_R) {
         const int p = p0 + lane;
         const bool valid = p < npx;
@@ -525,6 +540,7 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small_kernel(
             }
         }
         wave_sync();
+#ifndef CP_RV_NO_STORE
         const int nh = ((npx - p0) < WAVE_R ? (npx - p0) : WAVE_R) * per_px;
         const int tot = sh + nh;
         uint4* d4 = reinterpret_cast<uint4*>(dst - sh);
@@ -532,11 +548,12 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small_kernel(
         for (int k = lane; k * 8 < tot; k += WAVE_R) {
             const int h0 = k * 8;
             if (h0 >= sh && h0 + 8 <= tot) {
-                d4[k] = s4[k];
+                store_stream(&d4[k], s4[k]);
             } else {
                 for (int e = (h0 > sh ? h0 : sh); e < (h0 + 8 < tot ? h0 + 8 : tot); ++e) dst[e - sh] = stage[e];
             }
         }
+#endif
         wave_sync();
     }
 }
