@@ -928,6 +928,381 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, float* pool, float* pool
     }
 }
 
+// ---- fast-form island rows.  Bullet's sequential-impulse solver
+// precomputes, per solver row, the lever-arm cross product r x t and the angular
+// component M (r x t) once per step (btSequentialImpulseConstraintSolver::
+// setupContactConstraint), so its sweeps only touch velocities.  fast_build does the
+// same for the lane's island rows: the values are the ones isl_row computes inside
+// the sweep loop (pure functions of loop-invariant operands: rb, n, the tangents,
+// the positions and the world inverse inertias), so every sweep result is
+// bit-identical to the slow form.  Rows live in registers, statically indexed by
+// (local pair, point); used when no lane of the wave has friction rows on local
+// pairs 0 or 2 (the default friction table: a cart's friction is 0).
+struct GRow {
+    V3 rbt, ib;
+    float ie, tg, lam;
+};
+struct CRow {
+    V3 rbt, ib, rat, ia;
+    float ie, tg, lam;
+};
+struct FRow {
+    V3 rbt1, ib1, rbt2, ib2;
+    float ie1, ie2, l1, l2;
+};
+struct FastIsl {
+    GRow g0[4], g1[4];  // local pair 0 (ground, cart), 1 (ground, pole)
+    CRow c2[4];         // local pair 2 (cart, pole)
+    FRow f1[4];         // friction points of local pair 1
+    V3 t1, t2;          // their tangents (plane_space of pair 1's normal)
+};
+
+CP_DEV bool fast_ok(const Ctx& c) { return pk_fcnt(c.T.pk[0]) == 0 && pk_fcnt(c.T.pk[2]) == 0; }
+
+template <int J>
+CP_DEV void fast_ground_rows(GRow* R, const Ctx& c, float* pool) {
+    const uint32_t pk = c.T.pk[J];
+    const int cnt = pk_cnt(pk), base = pk_base(pk);
+    const Sym& M = J == 0 ? c.I.d1.M : c.I.d2.M;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (k < cnt) {
+            const int s = base + k;
+            const V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
+            R[k].rbt = cross(rb, c.T.n[J]);
+            R[k].ib = symv(M, R[k].rbt);
+            R[k].ie = pool_n(pool, F_IE, s);
+            R[k].tg = pool_n(pool, F_TG, s);
+            R[k].lam = pool_n(pool, F_LAM, s);
+        }
+    }
+}
+
+CP_DEV void fast_build(FastIsl& F, const Ctx& c, float* pool) {
+    fast_ground_rows<0>(F.g0, c, pool);
+    fast_ground_rows<1>(F.g1, c, pool);
+    {
+        const uint32_t pk = c.T.pk[2];
+        const int cnt = pk_cnt(pk), base = pk_base(pk);
+        const V3 n = c.T.n[2];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k < cnt) {
+                const int s = base + k;
+                const V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
+                CRow& R = F.c2[k];
+                R.rbt = cross(rb, n);
+                R.ib = symv(c.I.d2.M, R.rbt);
+                const V3 ra = add(rb, sub(c.I.d2.x, c.I.d1.x));
+                R.rat = cross(ra, n);
+                R.ia = symv(c.I.d1.M, R.rat);
+                R.ie = pool_n(pool, F_IE, s);
+                R.tg = pool_n(pool, F_TG, s);
+                R.lam = pool_n(pool, F_LAM, s);
+            }
+        }
+    }
+    {
+        const uint32_t pk = c.T.pk[1];
+        const int fcnt = pk_fcnt(pk), base = pk_base(pk), fbase = pk_fbase(pk);
+        plane_space(c.T.n[1], F.t1, F.t2);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k < fcnt) {
+                const int s = base + k, fs = fbase + k;
+                const V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
+                FRow& R = F.f1[k];
+                R.rbt1 = cross(rb, F.t1);
+                R.ib1 = symv(c.I.d2.M, R.rbt1);
+                R.rbt2 = cross(rb, F.t2);
+                R.ib2 = symv(c.I.d2.M, R.rbt2);
+                R.ie1 = pool_f(pool, FF_IE1, fs);
+                R.ie2 = pool_f(pool, FF_IE2, fs);
+                R.l1 = pool_f(pool, FF_L1, fs);
+                R.l2 = pool_f(pool, FF_L2, fs);
+            }
+        }
+    }
+}
+
+// one ground row (A = static ground) on body b: isl_row<0, B, FRICTION> with r x t
+// and M (r x t) precomputed
+template <bool FRICTION>
+CP_DEV float fast_grow(Dyn& b, float imb, V3 t, V3 rbt, V3 ib, float inv_eff, float target, float& lam,
+                       float bound) {
+    const float vn = dot(t, b.v) + dot(b.w, rbt);
+    const float e = target - vn;
+    float dl = e * inv_eff;
+    const float l0 = lam + dl;
+    float ln;
+    if constexpr (!FRICTION) ln = l0 > 0.0f ? l0 : 0.0f;
+    else ln = l0 > bound ? bound : (l0 < -bound ? -bound : l0);
+    dl = ln - lam;
+    lam = ln;
+    const float sb = dl * imb;
+    b.v = madd(b.v, t, sb);
+    b.w = madd(b.w, ib, dl);
+    return fabsf(e * dl);
+}
+
+// one cart-pole normal row: isl_row<1, 2, false> with both bodies' terms precomputed
+CP_DEV float fast_crow(Isl& I, V3 t, const CRow& R, float& lam) {
+    const float vn = (dot(t, sub(I.d2.v, I.d1.v)) + dot(I.d2.w, R.rbt)) - dot(I.d1.w, R.rat);
+    const float e = R.tg - vn;
+    float dl = e * R.ie;
+    const float l0 = lam + dl;
+    const float ln = l0 > 0.0f ? l0 : 0.0f;
+    dl = ln - lam;
+    lam = ln;
+    const float sb = dl * I.im2;
+    I.d2.v = madd(I.d2.v, t, sb);
+    I.d2.w = madd(I.d2.w, R.ib, dl);
+    const float sa = dl * I.im1;
+    I.d1.v = madd(I.d1.v, neg(t), sa);
+    I.d1.w = madd(I.d1.w, neg(R.ia), dl);
+    return fabsf(e * dl);
+}
+
+// sweeps() with the island rows in fast form (same row order, same residual sums)
+CP_DEV void sweeps_fast(Ctx& c, FastIsl& F, Sim& S, const cp_physics& P, float* pool, float* pool0, bool second,
+                        int it0, int it1, Stamps& ST) {
+    const float thr = P.residual_threshold;
+    const int cnt0 = pk_cnt(c.T.pk[0]), cnt1 = pk_cnt(c.T.pk[1]), cnt2 = pk_cnt(c.T.pk[2]);
+    const int fc1 = pk_fcnt(c.T.pk[1]);
+    const V3 n0 = c.T.n[0], n1 = c.T.n[1], n2 = c.T.n[2];
+    for (int it = it0; it < it1; ++it) {
+        if (__ballot(c.active) == 0ull) break;
+#ifdef CP_STAMPS
+        ST.sweeps += 1;
+#endif
+        float r = 0.0f, rc = 0.0f;
+        if (c.active) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < cnt0) r = r + fast_grow<false>(c.I.d1, c.I.im1, n0, F.g0[k].rbt, F.g0[k].ib, F.g0[k].ie,
+                                                       F.g0[k].tg, F.g0[k].lam, 0.0f);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < cnt1) r = r + fast_grow<false>(c.I.d2, c.I.im2, n1, F.g1[k].rbt, F.g1[k].ib, F.g1[k].ie,
+                                                       F.g1[k].tg, F.g1[k].lam, 0.0f);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < cnt2) r = r + fast_crow(c.I, n2, F.c2[k], F.c2[k].lam);
+        }
+        const bool cross = c.active && c.merged;  // same on both lanes of an env
+        if (__ballot(cross) != 0ull && cross) {
+            cross_view(S, c.T, c.I, second);
+            pair_normal_rows<5>(S, c.T, second, P, pool0, rc);
+            pair_normal_rows<6>(S, c.T, second, P, pool0, rc);
+            pair_normal_rows<7>(S, c.T, second, P, pool0, rc);
+            pair_normal_rows<8>(S, c.T, second, P, pool0, rc);
+            cross_back(c.I, S, second);
+        }
+        if (c.active) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (k < fc1) {
+                    const float bound = c.mu1 * F.g1[k].lam;
+                    r = r + fast_grow<true>(c.I.d2, c.I.im2, F.t1, F.f1[k].rbt1, F.f1[k].ib1, F.f1[k].ie1, 0.0f,
+                                            F.f1[k].l1, bound);
+                    r = r + fast_grow<true>(c.I.d2, c.I.im2, F.t2, F.f1[k].rbt2, F.f1[k].ib2, F.f1[k].ie2, 0.0f,
+                                            F.f1[k].l2, bound);
+                }
+            }
+        }
+        if (__ballot(cross) != 0ull && cross) {
+            cross_view(S, c.T, c.I, second);
+            pair_friction_rows<5>(S, c.T, second, P, pool0, rc);
+            pair_friction_rows<6>(S, c.T, second, P, pool0, rc);
+            pair_friction_rows<7>(S, c.T, second, P, pool0, rc);
+            pair_friction_rows<8>(S, c.T, second, P, pool0, rc);
+            cross_back(c.I, S, second);
+        }
+        const float rp = partner(r);  // every lane that entered the loop is here (pairs together)
+        const float joint = second ? (rp + r) + rc : (r + rp) + rc;
+        if (c.active && (c.merged ? joint : r) <= thr) c.active = false;
+    }
+}
+
+// the island rows' impulses back into the pool (substep_finish refreshes the
+// warm-start cache from it)
+CP_DEV void fast_store(const FastIsl& F, const Ctx& c, float* pool) {
+    const int cnt0 = pk_cnt(c.T.pk[0]), cnt1 = pk_cnt(c.T.pk[1]), cnt2 = pk_cnt(c.T.pk[2]);
+    const int b0 = pk_base(c.T.pk[0]), b1 = pk_base(c.T.pk[1]), b2 = pk_base(c.T.pk[2]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (k < cnt0) pool_n(pool, F_LAM, b0 + k) = F.g0[k].lam;
+        if (k < cnt1) pool_n(pool, F_LAM, b1 + k) = F.g1[k].lam;
+        if (k < cnt2) pool_n(pool, F_LAM, b2 + k) = F.c2[k].lam;
+    }
+}
+
+// Class-specialised fast sweeps for the tail kernel.  Tail envs are sorted into
+// classes by the row groups of their unconverged islands: CLS 0 = ground-cart +
+// cart-pole rows (a pole standing on its cart: ~85% of the islands that reach the
+// sweep cap), CLS 1 = ground-cart + ground-pole rows with the pole's friction rows.
+// Neither class has a merged env or friction on local pairs 0 / 2.  Absent row groups
+// compile away, so each loop keeps its rows in architectural VGPRs.
+template <int CLS>
+CP_DEV void fast_build_cls(FastIsl& F, const Ctx& c, float* pool) {
+    fast_ground_rows<0>(F.g0, c, pool);
+    if constexpr (CLS == 1) {
+        fast_ground_rows<1>(F.g1, c, pool);
+        const uint32_t pk = c.T.pk[1];
+        const int fcnt = pk_fcnt(pk), base = pk_base(pk), fbase = pk_fbase(pk);
+        plane_space(c.T.n[1], F.t1, F.t2);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k < fcnt) {
+                const int s = base + k, fs = fbase + k;
+                const V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
+                FRow& R = F.f1[k];
+                R.rbt1 = cross(rb, F.t1);
+                R.ib1 = symv(c.I.d2.M, R.rbt1);
+                R.rbt2 = cross(rb, F.t2);
+                R.ib2 = symv(c.I.d2.M, R.rbt2);
+                R.ie1 = pool_f(pool, FF_IE1, fs);
+                R.ie2 = pool_f(pool, FF_IE2, fs);
+                R.l1 = pool_f(pool, FF_L1, fs);
+                R.l2 = pool_f(pool, FF_L2, fs);
+            }
+        }
+    } else {
+        const uint32_t pk = c.T.pk[2];
+        const int cnt = pk_cnt(pk), base = pk_base(pk);
+        const V3 n = c.T.n[2];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k < cnt) {
+                const int s = base + k;
+                const V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
+                CRow& R = F.c2[k];
+                R.rbt = cross(rb, n);
+                R.ib = symv(c.I.d2.M, R.rbt);
+                const V3 ra = add(rb, sub(c.I.d2.x, c.I.d1.x));
+                R.rat = cross(ra, n);
+                R.ia = symv(c.I.d1.M, R.rat);
+                R.ie = pool_n(pool, F_IE, s);
+                R.tg = pool_n(pool, F_TG, s);
+                R.lam = pool_n(pool, F_LAM, s);
+            }
+        }
+    }
+}
+
+template <int CLS>
+CP_DEV void sweeps_cls(Ctx& c, FastIsl& F, const cp_physics& P, bool second, int it0, int it1, Stamps& ST) {
+    const float thr = P.residual_threshold;
+    const int cnt0 = pk_cnt(c.T.pk[0]);
+    const int cnt1 = CLS == 1 ? pk_cnt(c.T.pk[1]) : 0, fc1 = CLS == 1 ? pk_fcnt(c.T.pk[1]) : 0;
+    const int cnt2 = CLS == 0 ? pk_cnt(c.T.pk[2]) : 0;
+    const V3 n0 = c.T.n[0], n1 = c.T.n[1], n2 = c.T.n[2];
+    for (int it = it0; it < it1; ++it) {
+        if (__ballot(c.active) == 0ull) break;
+#ifdef CP_STAMPS
+        ST.sweeps += 1;
+#endif
+        float r = 0.0f;
+        if (c.active) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < cnt0) r = r + fast_grow<false>(c.I.d1, c.I.im1, n0, F.g0[k].rbt, F.g0[k].ib, F.g0[k].ie,
+                                                       F.g0[k].tg, F.g0[k].lam, 0.0f);
+            if constexpr (CLS == 1) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (k < cnt1) r = r + fast_grow<false>(c.I.d2, c.I.im2, n1, F.g1[k].rbt, F.g1[k].ib,
+                                                           F.g1[k].ie, F.g1[k].tg, F.g1[k].lam, 0.0f);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (k < fc1) {
+                        const float bound = c.mu1 * F.g1[k].lam;
+                        r = r + fast_grow<true>(c.I.d2, c.I.im2, F.t1, F.f1[k].rbt1, F.f1[k].ib1, F.f1[k].ie1, 0.0f,
+                                                F.f1[k].l1, bound);
+                        r = r + fast_grow<true>(c.I.d2, c.I.im2, F.t2, F.f1[k].rbt2, F.f1[k].ib2, F.f1[k].ie2, 0.0f,
+                                                F.f1[k].l2, bound);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (k < cnt2) r = r + fast_crow(c.I, n2, F.c2[k], F.c2[k].lam);
+            }
+        }
+        if (c.active && r <= thr) c.active = false;  // no merged env in these classes
+    }
+}
+
+template <int CLS>
+CP_DEV void fast_store_cls(const FastIsl& F, const Ctx& c, float* pool) {
+    const int cnt0 = pk_cnt(c.T.pk[0]), b0 = pk_base(c.T.pk[0]);
+    const int cnt1 = pk_cnt(c.T.pk[1]), b1 = pk_base(c.T.pk[1]);
+    const int cnt2 = pk_cnt(c.T.pk[2]), b2 = pk_base(c.T.pk[2]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (k < cnt0) pool_n(pool, F_LAM, b0 + k) = F.g0[k].lam;
+        if (CLS == 1 && k < cnt1) pool_n(pool, F_LAM, b1 + k) = F.g1[k].lam;
+        if (CLS == 0 && k < cnt2) pool_n(pool, F_LAM, b2 + k) = F.c2[k].lam;
+    }
+}
+
+// tail class of an env whose islands are not all converged (both lanes of the pair
+// call it in converged code: the DPP read needs the partner lane)
+CP_DEV int tail_class(const Ctx& c) {
+    const uint32_t own = c.active ? ((pk_cnt(c.T.pk[1]) > 0 ? 1u : 0u) | (pk_cnt(c.T.pk[2]) > 0 ? 2u : 0u) |
+                                     (fast_ok(c) ? 0u : 4u))
+                                  : 0u;
+    const uint32_t both = own | partner_u(own);
+    if (c.merged || (both & 4u)) return 2;
+    if (!(both & 1u)) return 0;
+    if (!(both & 2u)) return 1;
+    return 2;
+}
+
+// PGS sweeps [it0, it1) of the lane's island.  FAST: fast-form island rows when no
+// lane of the wave has friction rows on local pairs 0 / 2 (wave-uniform choice; the
+// fast form needs a register budget only the tail kernel has).
+template <bool FAST>
+CP_DEV void solve_range(Ctx& c, Sim& S, const cp_physics& P, float* pool, float* pool0, bool second, int it0, int it1,
+                        Stamps& ST) {
+#ifndef CP_NO_FAST_ROWS
+    if constexpr (FAST) {
+        if (__ballot(!fast_ok(c)) == 0ull) {
+            FastIsl F;
+            fast_build(F, c, pool);
+            sweeps_fast(c, F, S, P, pool, pool0, second, it0, it1, ST);
+            fast_store(F, c, pool);
+            return;
+        }
+    }
+#endif
+    sweeps(c, S, P, pool, pool0, second, it0, it1, ST);
+}
+
+// the lane's island view: its two bodies (cart, pole or cart2, pole2) with their world
+// inverse inertias, and the island's friction products
+CP_DEV void island_view(const Sim& S, const Lane& L, Ctx& c) {
+    const bool second = L.isl != 0;
+    Isl& I = c.I;
+    I.d1.x = selv(second, S.b[2].x, S.b[0].x);
+    I.d1.v = selv(second, S.b[2].v, S.b[0].v);
+    I.d1.w = selv(second, S.b[2].w, S.b[0].w);
+    I.d2.x = selv(second, S.b[3].x, S.b[1].x);
+    I.d2.v = selv(second, S.b[3].v, S.b[1].v);
+    I.d2.w = selv(second, S.b[3].w, S.b[1].w);
+    const float cq0 = second ? S.b[2].q[0] : S.b[0].q[0], cq1 = second ? S.b[2].q[1] : S.b[0].q[1];
+    const float cq2 = second ? S.b[2].q[2] : S.b[0].q[2], cq3 = second ? S.b[2].q[3] : S.b[0].q[3];
+    const float pq0 = second ? S.b[3].q[0] : S.b[1].q[0], pq1 = second ? S.b[3].q[1] : S.b[1].q[1];
+    const float pq2 = second ? S.b[3].q[2] : S.b[1].q[2], pq3 = second ? S.b[3].q[3] : S.b[1].q[3];
+    I.d1.M = world_inv_inertia(quat_axes(cq0, cq1, cq2, cq3), L.ii1[0], L.ii1[1], L.ii1[2]);
+    I.d2.M = world_inv_inertia(quat_axes(pq0, pq1, pq2, pq3), L.ii2[0], L.ii2[1], L.ii2[2]);
+    I.im1 = L.im1;
+    I.im2 = L.im2;
+    c.mu0 = L.mu0;
+    c.mu1 = L.mu1;
+    c.mu2 = L.mu2;
+}
+
 // Phase 1 of one p.stepSimulation() (DESIGN.md §Physics model 1-5a): narrowphase and
 // row setup of the lane's island, unconstrained velocity update of the whole env,
 // the island view and the warm start.  A lane with live == false (done env, padding)
@@ -1053,27 +1428,8 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, float* pool
     c.used = used;
     c.tot = used + (int)partner_u((uint32_t)used);
     const bool second = L.isl != 0;
-    // the island's two bodies (cart, pole or cart2, pole2) with their world inverse inertia
+    island_view(S, L, c);
     Isl& I = c.I;
-    {
-        I.d1.x = selv(second, S.b[2].x, S.b[0].x);
-        I.d1.v = selv(second, S.b[2].v, S.b[0].v);
-        I.d1.w = selv(second, S.b[2].w, S.b[0].w);
-        I.d2.x = selv(second, S.b[3].x, S.b[1].x);
-        I.d2.v = selv(second, S.b[3].v, S.b[1].v);
-        I.d2.w = selv(second, S.b[3].w, S.b[1].w);
-        const float cq0 = second ? S.b[2].q[0] : S.b[0].q[0], cq1 = second ? S.b[2].q[1] : S.b[0].q[1];
-        const float cq2 = second ? S.b[2].q[2] : S.b[0].q[2], cq3 = second ? S.b[2].q[3] : S.b[0].q[3];
-        const float pq0 = second ? S.b[3].q[0] : S.b[1].q[0], pq1 = second ? S.b[3].q[1] : S.b[1].q[1];
-        const float pq2 = second ? S.b[3].q[2] : S.b[1].q[2], pq3 = second ? S.b[3].q[3] : S.b[1].q[3];
-        I.d1.M = world_inv_inertia(quat_axes(cq0, cq1, cq2, cq3), L.ii1[0], L.ii1[1], L.ii1[2]);
-        I.d2.M = world_inv_inertia(quat_axes(pq0, pq1, pq2, pq3), L.ii2[0], L.ii2[1], L.ii2[2]);
-        I.im1 = L.im1;
-        I.im2 = L.im2;
-    }
-    c.mu0 = L.mu0;
-    c.mu1 = L.mu1;
-    c.mu2 = L.mu2;
     CP_STAMP(t2);
     CP_ACC(vel, t1, t2);
     // Island rows run per lane; the rows of the two islands touch disjoint bodies,
@@ -1165,7 +1521,7 @@ CP_DEV void substep(Sim& S, const cp_physics& P, const Lane& L, float* pool, flo
     Ctx c;
     substep_prep(S, P, L, pool, pool0, overflow, G, ST, live, c);
     CP_STAMP(t2);
-    sweeps(c, S, P, pool, pool0, L.isl != 0, 0, P.solver_iterations, ST);
+    solve_range<false>(c, S, P, pool, pool0, L.isl != 0, 0, P.solver_iterations, ST);
     CP_STAMP(t3);
     CP_ACC(solve, t2, t3);
     substep_finish(S, P, L, c, pool, G, ST, live);

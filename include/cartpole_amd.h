@@ -215,12 +215,13 @@ int cp_timing_begin(cp_handle* h, int max_launches);
 int cp_timing_end(cp_handle* h, double* step_ms, int32_t* step_launches, double* reset_ms,
                   int32_t* reset_launches);
 
-/* Diagnostics of a stamp build (-DCP_STAMPS): host array of 8 counters summed over
- * the step-kernel waves since the last reset: s_memtime cycles in narrowphase,
- * velocity update + warm start, PGS sweeps, integration + cache; sweep count,
- * substep count, total kernel cycles, waves.  Synchronises the device.  Returns 1
- * in a stamp build, 0 otherwise (counters then stay 0). */
-int cp_debug_stamps(cp_handle* h, uint64_t* out8, int reset);
+/* Diagnostics of a stamp build (-DCP_STAMPS): host array of 16 counters summed over
+ * waves since the last reset, 8 for the step / head kernel then 8 for the tail
+ * kernel: s_memtime cycles in narrowphase, velocity update + warm start, PGS sweeps,
+ * integration + cache; sweep count, substep count, total kernel cycles, waves.
+ * Synchronises the device.  Returns 1 in a stamp build, 0 otherwise (counters then
+ * stay 0). */
+int cp_debug_stamps(cp_handle* h, uint64_t* out16, int reset);
 
 /* ---- Raster observation (--use-raw-pixels) ----------
  * Replaces render_rgb + set_state_element_for_repeat (bullet_cartpole.py:277-306):

@@ -23,18 +23,21 @@ acts = torch.randint(0, 5, (steps + 20, B, 2), dtype=torch.int8, device="cuda", 
 env.reset()
 for t in range(20):
     env.step(acts[t])
-out = (C.c_uint64 * 8)()
+out = (C.c_uint64 * 16)()
 rc = env.lib.cp_debug_stamps(env.h, out, 1)
 assert rc == 1, "not a stamp build (set CP_LIB_PATH to libcartpole_hip_stamps.so)"
 for t in range(steps):
     env.step(acts[20 + t])
 env.lib.cp_debug_stamps(env.h, out, 0)
-narrow, vel, solve, integ, sweeps, substeps, total, waves = list(out)
-per = lambda x: x / max(1, substeps)
-res = {"B": B, "steps": steps, "waves": waves, "substeps_per_wave": substeps / max(1, waves),
-       "cycles_per_wave_substep": {"narrowphase+setup": per(narrow), "velocity+warmstart": per(vel),
-                                   "pgs_sweeps": per(solve), "integrate+cache": per(integ),
-                                   "kernel_total_per_substep": total / max(1, substeps)},
-       "sweeps_per_wave_substep": sweeps / max(1, substeps),
-       "cycles_per_sweep": solve / max(1, sweeps)}
+res = {"B": B, "steps": steps}
+for name, vals in (("head", list(out)[:8]), ("tail", list(out)[8:])):
+    narrow, vel, solve, integ, sweeps, substeps, total, waves = vals
+    per = lambda x: x / max(1, substeps)
+    res[name] = {"waves": waves, "substeps_per_wave": substeps / max(1, waves),
+                 "cycles_per_wave_substep": {"narrowphase+setup": per(narrow), "velocity+warmstart": per(vel),
+                                             "pgs_sweeps": per(solve), "integrate+cache": per(integ),
+                                             "kernel_total_per_substep": total / max(1, substeps)},
+                 "sweeps_per_wave_substep": sweeps / max(1, substeps),
+                 "cycles_per_sweep": solve / max(1, sweeps),
+                 "kernel_cycles_per_wave": total / max(1, waves)}
 print(json.dumps(res, indent=1))
