@@ -5,7 +5,9 @@
 
 hipcc cross-compiles for gfx950 without a GPU.  -ffp-contract=off: only the
 explicit __builtin_fmaf calls fuse, which is what makes the kernel agree bit for
-bit with the CPU oracle.
+bit with the CPU oracle.  -fno-slp-vectorize: the SLP pass packs
+independent fp32 FMAs into v_pk_fma_f32 and then pays register-pair moves and
+pressure for it (step kernel scratch 324 -> 148 B/lane without it).
 """
 import os
 import subprocess
@@ -20,7 +22,7 @@ STAMPS_LIB = os.path.join(HERE, "libcartpole_hip_stamps.so")
 ARCH = os.environ.get("CP_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
+FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-fPIC", "-shared",
          "-Wno-unused-result"]
 
 

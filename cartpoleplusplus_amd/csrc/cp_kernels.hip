@@ -805,11 +805,13 @@ cp_tail_kernel(cp_config cfg, Bufs b, StepArgs a) {
         const Soa sg = Soa::make(b.stage, 2 * B, STAGE_FIELDS);
         Sim S;
         Ctx c;
+        CP_STAMP(s0);
         stage_in(sg, G.xoff, c, S, L, pool);
         float u[2][2] = {{0.0f, 0.0f}, {0.0f, 0.0f}};
         bool lqr_out = false;
         if constexpr (LQR) lqr_load(b, B, i, u, lqr_out);
         CP_STAMP(s2);
+        CP_ACC(narrow, s0, s2);  // tail: stage-in time in the narrowphase slot
         const int it0 = min(a.head, cfg.phys.solver_iterations), it1 = cfg.phys.solver_iterations;
         if (cls == 2) {
             solve_range<true>(c, S, cfg.phys, pool, pool0, isl != 0, it0, it1, ST);
@@ -828,7 +830,10 @@ cp_tail_kernel(cp_config cfg, Bufs b, StepArgs a) {
         CP_STAMP(s3);
         CP_ACC(solve, s2, s3);
         substep_finish(S, cfg.phys, L, c, pool, G, ST, true);
+        CP_STAMP(s4);
         post_substep<KIND, LQR>(S, cfg, b, a, G, i, lead, u, lqr_out, want_reset, render_me);
+        CP_STAMP(s5);
+        CP_ACC(vel, s4, s5);  // tail: post-substep time in the velocity slot
     }
 #ifdef CP_STAMPS
     CP_STAMP(k1);
