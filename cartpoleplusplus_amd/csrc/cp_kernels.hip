@@ -57,7 +57,7 @@ struct Bufs {
     int32_t* rlist;    // [B] envs to render after the step kernel
     int32_t* rcount;   // [1]
     uint8_t* stepped;  // [B] 1 = simulated by the last cp_step (event log: done-before envs are not logged)
-    float* stage;      // [STAGE_FIELDS][2B] solve context of the tail envs, one column per lane
+    float* stage;      // [STAGE_FIELDS][3][2B] solve context of the tail envs, one column per lane, at list position
     int32_t* slist;    // [3][B] tail envs of the current substep, per tail class
     int32_t* scount;   // [R*S][3] their counts, per substep of the step
     float* lqr;        // [5][B] LQR forces u (2 x 2) and the both-pairs-out flag between substep launches
@@ -589,24 +589,43 @@ CP_DEV void lqr_save(const Bufs& b, int B, int i, const float u[2][2], bool out)
 // Everything cp_step_kernel does after substep() for substep a.t of env i: the
 // action (+ LQR) forces, readbacks, the obs row at a repeat end, and at the step's
 // last substep steps / done / reward / returns; the env state goes back to HBM.
-template <int KIND, bool LQR>
-CP_DEV void post_substep(Sim& S, const cp_config& cfg, const Bufs& b, const StepArgs& a, const Mem& G, int i,
-                         bool lead, float u[2][2], bool lqr_out, bool& want_reset, bool& render_me) {
-    const int B = cfg.num_envs;
-    const int R = cfg.action_repeats, SR = cfg.steps_per_repeat, T = R * SR;
-    const int r = a.t / SR, s = a.t - r * SR;
-    float a00, a01, a10, a11;
+// Per-env inputs of post_substep, loaded before the solve so their latency overlaps it.
+struct PostIn {
+    float a00, a01, a10, a11;  // action (table entries for discrete actions)
+    int steps;                 // step counter before this step (read at the step's last substep)
+    float ret;                 // return accumulator
+};
+template <int KIND>
+CP_DEV PostIn post_inputs(const cp_config& cfg, const Bufs& b, const StepArgs& a, const Mem& G, int i) {
+    PostIn q;
     if constexpr (KIND == CP_ACTION_CONTINUOUS) {
         const float4 av = reinterpret_cast<const float4*>(a.actions)[i];
-        a00 = av.x; a01 = av.y; a10 = av.z; a11 = av.w;
+        q.a00 = av.x; q.a01 = av.y; q.a10 = av.z; q.a11 = av.w;
     } else {
         const char2 av = reinterpret_cast<const char2*>(a.actions)[i];
         int k0 = av.x, k1 = av.y;
         k0 = (k0 < 0 || k0 >= CP_NUM_DISCRETE) ? 0 : k0;
         k1 = (k1 < 0 || k1 >= CP_NUM_DISCRETE) ? 0 : k1;
-        a00 = kDiscrete[k0][0]; a01 = kDiscrete[k0][1];
-        a10 = kDiscrete[k1][0]; a11 = kDiscrete[k1][1];
+        q.a00 = kDiscrete[k0][0]; q.a01 = kDiscrete[k0][1];
+        q.a10 = kDiscrete[k1][0]; q.a11 = kDiscrete[k1][1];
     }
+    const bool last = a.t == cfg.action_repeats * cfg.steps_per_repeat - 1;
+    q.steps = last ? ldi(G.st, CP_SF_STEPS, G.off) : 0;
+    q.ret = last ? b.ret_acc[i] : 0.0f;
+    return q;
+}
+
+// Everything cp_step_kernel does after substep() for substep a.t of env i: the
+// action (+ LQR) forces, readbacks, the obs row at a repeat end, and at the step's
+// last substep steps / done / reward / returns; the env state goes back to HBM.
+template <int KIND, bool LQR>
+CP_DEV void post_substep(Sim& S, const cp_config& cfg, const Bufs& b, const StepArgs& a, const Mem& G, int i,
+                         bool lead, const PostIn& q, float u[2][2], bool lqr_out, bool& want_reset,
+                         bool& render_me) {
+    const int B = cfg.num_envs;
+    const int R = cfg.action_repeats, SR = cfg.steps_per_repeat, T = R * SR;
+    const int r = a.t / SR, s = a.t - r * SR;
+    const float a00 = q.a00, a01 = q.a01, a10 = q.a10, a11 = q.a11;
     const float F = cfg.action_force;
     const float f00 = a00 * F, f01 = a01 * F, f10 = a10 * F, f11 = a11 * F;
     if constexpr (LQR) {  // disturbance + control (:897-901), control from the pre-substep state
@@ -639,7 +658,7 @@ CP_DEV void post_substep(Sim& S, const cp_config& cfg, const Bufs& b, const Step
         return;
     }
     render_me = lead && b.rposes != nullptr;
-    const int steps = ldi(G.st, CP_SF_STEPS, G.off) + 1;
+    const int steps = q.steps + 1;
     bool done = steps >= cfg.max_episode_len;
     if (cfg.done_on_bounds && bounds_exceeded(S, cfg)) done = true;
     if (LQR && lqr_out) done = true;
@@ -649,7 +668,7 @@ CP_DEV void post_substep(Sim& S, const cp_config& cfg, const Bufs& b, const Step
     a.reward_out[i] = 1.0f;  // bullet_cartpole.py:260
     a.done_out[i] = done ? 1 : 0;
     const Soa term = Soa::make(b.term_obs, B, R * 14);
-    const float ret = b.ret_acc[i] + 1.0f;
+    const float ret = q.ret + 1.0f;
     if (done) {
         b.last_ret[i] = ret;
         b.last_len[i] = steps;
@@ -699,6 +718,10 @@ __global__ void CP_PHYS_ATTR cp_head_kernel(cp_config cfg, Bufs b, StepArgs a) {
     int cls = 0;
     Stamps ST;
     CP_STAMP(k0);
+    Sim S;
+    Ctx c;
+    float u[2][2] = {{0.0f, 0.0f}, {0.0f, 0.0f}};
+    bool lqr_out = false;
     if (i < B) {
         const Mem G = Mem::make(b.state, b.scratch, B, i, isl);
         bool run;
@@ -718,10 +741,8 @@ __global__ void CP_PHYS_ATTR cp_head_kernel(cp_config cfg, Bufs b, StepArgs a) {
         }
         if (run) {
             const Lane L = Lane::make(isl, cfg.phys);
-            Sim S;
             load_sim(S, G.st, G.off);
-            float u[2][2] = {{0.0f, 0.0f}, {0.0f, 0.0f}};
-            bool lqr_out = false;
+            const PostIn q = post_inputs<KIND>(cfg, b, a, G, i);
             if constexpr (LQR) {
                 if (a.t == 0) {  // control from the pre-step state
                     const float* K = a.lq.gains + (a.lq.per_env ? (size_t)i * 32 : 0);
@@ -731,7 +752,6 @@ __global__ void CP_PHYS_ATTR cp_head_kernel(cp_config cfg, Bufs b, StepArgs a) {
                 }
             }
             int ov = 0;
-            Ctx c;
             substep_prep(S, cfg.phys, L, pool, pool0, ov, G, ST, true, c);
             CP_STAMP(s2);
             sweeps(c, S, cfg.phys, pool, pool0, isl != 0, 0, min(a.head, cfg.phys.solver_iterations), ST);
@@ -744,13 +764,9 @@ __global__ void CP_PHYS_ATTR cp_head_kernel(cp_config cfg, Bufs b, StepArgs a) {
             const uint32_t pact = partner_u(c.active ? 1u : 0u);
             tail = c.active || pact != 0u;
             cls = tail_class(c);
-            if (tail) {
-                const Soa sg = Soa::make(b.stage, 2 * B, STAGE_FIELDS);
-                stage_out(sg, G.xoff, c, S, pool);
-                if (LQR && lead && a.t == 0) lqr_save(b, B, i, u, lqr_out);
-            } else {
+            if (!tail) {
                 substep_finish(S, cfg.phys, L, c, pool, G, ST, true);
-                post_substep<KIND, LQR>(S, cfg, b, a, G, i, lead, u, lqr_out, want_reset, render_me);
+                post_substep<KIND, LQR>(S, cfg, b, a, G, i, lead, q, u, lqr_out, want_reset, render_me);
             }
         }
     }
@@ -758,6 +774,7 @@ __global__ void CP_PHYS_ATTR cp_head_kernel(cp_config cfg, Bufs b, StepArgs a) {
     CP_STAMP(k1);
     flush_stamps(ST, b.stamps, k1 - k0);
 #endif
+    int pos = 0;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {  // tail envs per class, in pairs of lanes: one list entry per env (lead lane)
         const bool put = tail && lead && cls == k;
@@ -767,7 +784,16 @@ __global__ void CP_PHYS_ATTR cp_head_kernel(cp_config cfg, Bufs b, StepArgs a) {
         int base = 0;
         if (lane == 0 && n) base = atomicAdd(b.scount + 3 * a.t + k, n);
         base = __shfl(base, 0);
-        if (put) b.slist[(size_t)k * B + base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
+        if (put) {
+            pos = base + __popcll(bal & ((1ull << lane) - 1ull));
+            b.slist[(size_t)k * B + pos] = i;
+        }
+    }
+    pos = __shfl(pos, threadIdx.x & ~1u);  // the pair's list position (lead lane)
+    if (tail) {  // the solve context, at the env's list position (coalesced for the tail kernel)
+        const Soa sg = Soa::make(b.stage, 6 * B, STAGE_FIELDS);
+        stage_out(sg, (uint32_t)(cls * 2 * B + 2 * pos + isl) * 4u, c, S, pool);
+        if (LQR && lead && a.t == 0) lqr_save(b, B, i, u, lqr_out);
     }
     if (a.t == T - 1) append_lists(cfg, b, i, want_reset, render_me);
 }
@@ -802,11 +828,12 @@ cp_tail_kernel(cp_config cfg, Bufs b, StepArgs a) {
         i = b.slist[(size_t)cls * B + p];
         const Mem G = Mem::make(b.state, b.scratch, B, i, isl);
         const Lane L = Lane::make(isl, cfg.phys);
-        const Soa sg = Soa::make(b.stage, 2 * B, STAGE_FIELDS);
+        const Soa sg = Soa::make(b.stage, 6 * B, STAGE_FIELDS);
         Sim S;
         Ctx c;
         CP_STAMP(s0);
-        stage_in(sg, G.xoff, c, S, L, pool);
+        const PostIn q = post_inputs<KIND>(cfg, b, a, G, i);
+        stage_in(sg, (uint32_t)(cls * 2 * B + 2 * p + isl) * 4u, c, S, L, pool);
         float u[2][2] = {{0.0f, 0.0f}, {0.0f, 0.0f}};
         bool lqr_out = false;
         if constexpr (LQR) lqr_load(b, B, i, u, lqr_out);
@@ -831,7 +858,7 @@ cp_tail_kernel(cp_config cfg, Bufs b, StepArgs a) {
         CP_ACC(solve, s2, s3);
         substep_finish(S, cfg.phys, L, c, pool, G, ST, true);
         CP_STAMP(s4);
-        post_substep<KIND, LQR>(S, cfg, b, a, G, i, lead, u, lqr_out, want_reset, render_me);
+        post_substep<KIND, LQR>(S, cfg, b, a, G, i, lead, q, u, lqr_out, want_reset, render_me);
         CP_STAMP(s5);
         CP_ACC(vel, s4, s5);  // tail: post-substep time in the velocity slot
     }
@@ -1096,7 +1123,13 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     CP_ALLOC(h->b.scratch, (size_t)4 * CP_ISLAND_PAIRS * 2 * B * sizeof(float));
     CP_ALLOC(h->b.stamps, 16 * sizeof(uint64_t));
     CP_ALLOC(h->b.stepped, B * sizeof(uint8_t));
-    CP_ALLOC(h->b.stage, (size_t)cp::STAGE_FIELDS * 2 * B * sizeof(float));
+    if (!h->mono) {  // pipeline mode only
+        if ((unsigned long long)cp::STAGE_FIELDS * 6ull * B * 4ull >= (1ull << 32)) {
+            cp_destroy(h);
+            return fail(nullptr, "cp_create: num_envs too large for the pipeline's staging array (4 GiB)");
+        }
+        CP_ALLOC(h->b.stage, (size_t)cp::STAGE_FIELDS * 6 * B * sizeof(float));
+    }
     CP_ALLOC(h->b.slist, 3 * B * sizeof(int32_t));
     CP_ALLOC(h->b.scount, (size_t)3 * R * cfg->steps_per_repeat * sizeof(int32_t));
     CP_ALLOC(h->b.lqr, 5 * B * sizeof(float));
