@@ -67,6 +67,25 @@ def pmc_traffic(kernel, batch, repeats):
     return None, None
 
 
+def pmc_valu(kernel, batch, repeats):
+    """VALU wave-instructions per launch of `kernel` (SQ_INSTS_VALU) from the newest
+    committed PMC summary of this workload, else None."""
+    import glob
+    for p in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))):
+        with open(p) as f:
+            d = json.load(f)
+        k = d.get("kernels", {}).get(kernel)
+        if k and "SQ_INSTS_VALU" in k.get("sq_per_launch", {}) and d.get("batch", batch) == batch \
+                and d.get("repeats", repeats) == repeats:
+            return k["sq_per_launch"]["SQ_INSTS_VALU"], os.path.relpath(p, ROOT)
+    return None, None
+
+
+# MI355X_MICROARCH.md: 256 CUs x 4 SIMD-32, a wave64 VALU instruction takes 2 issue
+# cycles of its SIMD (one wave alone sustains one per 4), 2.4 GHz max clock
+VALU_PEAK_WINST_PER_S = 256 * 4 * 2.4e9 / 2
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -187,6 +206,15 @@ def main():
         achieved = bytes_launch / per_launch_s / 1e9
         kernel = "cp_render_small_kernel"
         traffic, traffic_src = pmc_traffic(kernel, B, R)
+    valu = None
+    if not args.raster:
+        vi, vsrc = pmc_valu(kernel, B, R)
+        if vi is not None:
+            ach = vi / per_launch_s
+            valu = {"bound": "valu-issue (secondary; the kernel is latency-bound, DESIGN.md §5)",
+                    "wave_instructions_per_launch": vi, "achieved": round(ach / 1e12, 4),
+                    "peak": round(VALU_PEAK_WINST_PER_S / 1e12, 4), "unit": "T wave-instr/s",
+                    "frac": round(ach / VALU_PEAK_WINST_PER_S, 4), "source": vsrc + " SQ_INSTS_VALU"}
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -220,6 +248,7 @@ def main():
                      "reset_kernel_avg_ms": round(tm["reset_ms"] / max(1, tm["reset_launches"]), 4),
                      **({"step_kernel_avg_ms": round(tm["step_ms"] / max(1, tm["step_launches"]), 4),
                          "render_launches": tm["render_launches"]} if args.raster else {})},
+        "valu": valu,
         "episode_return_hist_nonzero": None if hist is None else int((hist > 0).sum().item()),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
