@@ -85,6 +85,11 @@ CP_DEV void flush_stamps(const Stamps& ST, uint64_t* dst, uint64_t total) {
         atomicAdd((unsigned long long*)&dst[5], (unsigned long long)ST.substeps);
         atomicAdd((unsigned long long*)&dst[6], (unsigned long long)total);
         atomicAdd((unsigned long long*)&dst[7], 1ull);
+        if (ST.bb) {  // narrowphase split of the fused / head kernel into the spare tail slots
+            atomicAdd((unsigned long long*)&dst[8], (unsigned long long)ST.sel);
+            atomicAdd((unsigned long long*)&dst[9], (unsigned long long)ST.bb);
+            atomicAdd((unsigned long long*)&dst[10], (unsigned long long)ST.rows);
+        }
     }
 #else
     (void)ST; (void)dst; (void)total;

@@ -20,6 +20,7 @@ namespace cp {
 // Wave-uniform cycle counters from s_memtime, accumulated per wave.
 struct Stamps {
     uint64_t narrow = 0, vel = 0, solve = 0, integ = 0, sweeps = 0, substeps = 0;
+    uint64_t sel = 0, bb = 0, rows = 0;  // narrowphase split: box/inertia selection, box_box, row setup
 };
 #ifdef CP_STAMPS
 #define CP_STAMP(var) uint64_t var = __builtin_amdgcn_s_memtime()
@@ -1319,21 +1320,28 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, float* pool
     for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
         const int g = island_pair(L.isl, j);
         const int a = pair_a(g), b = pair_b(g);
+        CP_STAMP(n0);
+        // warm-start cache of the pair, loaded first: its latency overlaps the narrowphase
+        const uint32_t oid = __float_as_uint(G.lw(CP_SF_WS_ID(0, j)));
+        const float ol0 = G.ll(CP_SF_WS_LAM(0, j, 0)), ol1 = G.ll(CP_SF_WS_LAM(0, j, 1));
+        const float ol2 = G.ll(CP_SF_WS_LAM(0, j, 2)), ol3 = G.ll(CP_SF_WS_LAM(0, j, 3));
         const Box A = box_sel(a, S, P), Bx = box_sel(b, S, P);
         Contact C;
         C.m = 0;
         C.n = mk(0.0f, 0.0f, 1.0f);
+        CP_STAMP(n1);
         if (live && !face_separated(A, Bx, P.contact_margin)) box_box(A, Bx, P.contact_margin, P.edge_bias, C);
+        CP_STAMP(n2);
+        CP_ACC(sel, n0, n1);
+        CP_ACC(bb, n1, n2);
+        const int base = used, fbase = fused;
+        int m = 0, fm = 0;
+        uint32_t nid = 0xFFFFFFFFu;
+        if (__ballot(C.m > 0) != 0ull) {  // row setup, skipped when no lane of the wave has a contact
         const float mu = sel5p(a, P.friction) * sel5p(b, P.friction);
         const float ima = sel5p(a, P.inv_mass), imb = sel5p(b, P.inv_mass);
         const V3 xa = A.c, xb = Bx.c;
         const Sym Ma = inertia_sel(a, A, P), Mb = inertia_sel(b, Bx, P);
-        const uint32_t oid = __float_as_uint(G.lw(CP_SF_WS_ID(0, j)));
-        const float ol0 = G.ll(CP_SF_WS_LAM(0, j, 0)), ol1 = G.ll(CP_SF_WS_LAM(0, j, 1));
-        const float ol2 = G.ll(CP_SF_WS_LAM(0, j, 2)), ol3 = G.ll(CP_SF_WS_LAM(0, j, 3));
-        const int base = used, fbase = fused;
-        int m = 0, fm = 0;
-        uint32_t nid = 0xFFFFFFFFu;
         V3 t1 = mk(0.0f, 0.0f, 0.0f), t2 = t1;
         if (mu > 0.0f) plane_space(C.n, t1, t2);
 #pragma unroll
@@ -1376,8 +1384,11 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, float* pool
                 }
             }
         }
+        }
         used = base + m;
         fused = fbase + fm;
+        CP_STAMP(n3);
+        CP_ACC(rows, n2, n3);
         const uint32_t pk = (uint32_t)m | ((uint32_t)base << 3) | ((uint32_t)fm << 8) | ((uint32_t)fbase << 11);
         G.sx(4 * j + 0, C.n.x);
         G.sx(4 * j + 1, C.n.y);
