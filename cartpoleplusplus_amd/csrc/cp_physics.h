@@ -1390,17 +1390,31 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, float* pool
         CP_STAMP(n3);
         CP_ACC(rows, n2, n3);
         const uint32_t pk = (uint32_t)m | ((uint32_t)base << 3) | ((uint32_t)fm << 8) | ((uint32_t)fbase << 11);
+#ifdef CP_HDR_SCRATCH
         G.sx(4 * j + 0, C.n.x);
         G.sx(4 * j + 1, C.n.y);
         G.sx(4 * j + 2, C.n.z);
         G.sx(4 * j + 3, __uint_as_float(pk));
+#else
+        // the pair's manifold header into registers: j is wave-uniform, so this is a
+        // scalar switch, not a dynamically indexed register array
+        switch (j) {
+            case 0: T.n[0] = C.n; T.pk[0] = pk; break;
+            case 1: T.n[1] = C.n; T.pk[1] = pk; break;
+            case 2: T.n[2] = C.n; T.pk[2] = pk; break;
+            case 3: T.n[3] = C.n; T.pk[3] = pk; break;
+            default: T.n[4] = C.n; T.pk[4] = pk; break;
+        }
+#endif
         if (live) G.sw(CP_SF_WS_ID(0, j), __uint_as_float(nid));
     }
+#ifdef CP_HDR_SCRATCH
 #pragma unroll
     for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
         T.n[j] = mk(G.lx(4 * j + 0), G.lx(4 * j + 1), G.lx(4 * j + 2));
         T.pk[j] = __float_as_uint(G.lx(4 * j + 3));
     }
+#endif
     CP_STAMP(t1);
     CP_ACC(narrow, t0, t1);
     // 3. unconstrained velocity update (both lanes, whole env)
