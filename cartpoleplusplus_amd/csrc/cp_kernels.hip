@@ -49,7 +49,8 @@ struct Bufs {
     int32_t* last_len; // [B]
     int32_t* overflow; // [B]
     int32_t* list;     // [B] reset list
-    int32_t* count;    // [1] reset list length
+    int32_t* count;    // reset list length (one of the handle's two counters, by step parity)
+    int32_t* count_next;  // the other counter: zeroed by the reset kernel for the next call
     float* scratch;    // [4*CP_ISLAND_PAIRS][2B] manifold headers of the current substep, per lane
     uint64_t* stamps;  // [waves][8] diagnostic phase cycles (CP_STAMPS builds only)
     float* rposes;     // [B][R][4][7] repeat-end poses for the raster obs (NULL: raster off)
@@ -290,6 +291,7 @@ __global__ void CP_PHYS_ATTR cp_reset_kernel(cp_config cfg, Bufs b, float* obs_o
     __shared__ float lds_pool[POOL_FLOATS * WAVE];
     const int B = cfg.num_envs;
     const int t = blockIdx.x * WAVE + threadIdx.x;
+    if (t == 0 && b.count_next) *b.count_next = 0;  // the next cp_step's list starts empty
     const int n = *b.count;
     if ((t >> 1) >= n) return;  // lane pairs past the compacted list
     const int isl = t & 1;
@@ -974,6 +976,8 @@ struct cp_handle {
     cp_raster_config raster;
     uint16_t* pixels;  // raster obs output (NULL: raster off)
     int mono;          // 1: one fused cp_step_kernel per step (default), 0: head/tail pipeline (CP_PIPELINE=1)
+    int32_t* count2;   // [2] reset-list counters, alternating by call: each reset launch zeroes the other one
+    int par;           // counter the next call appends to
     int head;          // PGS sweeps of the head kernel (CP_HEAD_SWEEPS, default 6)
     std::string err;
 };
@@ -1124,7 +1128,7 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     CP_ALLOC(h->b.last_len, B * sizeof(int32_t));
     CP_ALLOC(h->b.overflow, B * sizeof(int32_t));
     CP_ALLOC(h->b.list, B * sizeof(int32_t));
-    CP_ALLOC(h->b.count, sizeof(int32_t));
+    CP_ALLOC(h->count2, 2 * sizeof(int32_t));
     CP_ALLOC(h->b.scratch, (size_t)4 * CP_ISLAND_PAIRS * 2 * B * sizeof(float));
     CP_ALLOC(h->b.stamps, 16 * sizeof(uint64_t));
     CP_ALLOC(h->b.stepped, B * sizeof(uint8_t));
@@ -1139,6 +1143,10 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     CP_ALLOC(h->b.scount, (size_t)3 * R * cfg->steps_per_repeat * sizeof(int32_t));
     CP_ALLOC(h->b.lqr, 5 * B * sizeof(float));
 #undef CP_ALLOC
+    e = hipMemset(h->count2, 0, 2 * sizeof(int32_t));
+    if (e != hipSuccess) return fail_free(e, "hipMemset");
+    h->b.count = h->count2;
+    h->b.count_next = nullptr;
     e = hipMemset(h->b.stepped, 0, B * sizeof(uint8_t));
     if (e != hipSuccess) return fail_free(e, "hipMemset");
     e = hipMemset(h->b.stamps, 0, 16 * sizeof(uint64_t));
@@ -1168,7 +1176,7 @@ void cp_destroy(cp_handle* h) {
     (void)hipFree(h->b.last_len);
     (void)hipFree(h->b.overflow);
     (void)hipFree(h->b.list);
-    (void)hipFree(h->b.count);
+    (void)hipFree(h->count2);
     (void)hipFree(h->b.scratch);
     (void)hipFree(h->b.stamps);
     (void)hipFree(h->b.stepped);
@@ -1205,6 +1213,13 @@ static int launch_render(cp_handle* h, const int32_t* list, const int32_t* count
     return 0;
 }
 
+// the reset list's counter for this call: the one the previous call's reset launch zeroed
+static void use_counter(cp_handle* h) {
+    h->b.count = h->count2 + h->par;
+    h->b.count_next = h->count2 + (h->par ^ 1);
+    h->par ^= 1;
+}
+
 static int launch_reset_from_list(cp_handle* h, float* obs_out, hipStream_t st, bool render) {
     const int B = h->cfg.num_envs;
     hipEvent_t* ev = timing_slot(h, 1);
@@ -1221,6 +1236,7 @@ int cp_reset(cp_handle* h, const uint8_t* env_mask, float* obs_out, void* stream
     hipStream_t st = (hipStream_t)stream;
     const int B = h->cfg.num_envs;
     CP_TRY(h, hipSetDevice(h->device));
+    use_counter(h);
     CP_TRY(h, hipMemsetAsync(h->b.count, 0, sizeof(int32_t), st));
     hipLaunchKernelGGL(cp::cp_mask_to_list_kernel, dim3(grid_for(B, 256)), dim3(256), 0, st, B, env_mask, h->b.list,
                        h->b.count);
@@ -1236,7 +1252,7 @@ int cp_step(cp_handle* h, const void* actions, int action_kind, float* obs_out, 
     hipStream_t st = (hipStream_t)stream;
     const int B = h->cfg.num_envs;
     CP_TRY(h, hipSetDevice(h->device));
-    if (h->cfg.autoreset) CP_TRY(h, hipMemsetAsync(h->b.count, 0, sizeof(int32_t), st));
+    if (h->cfg.autoreset) use_counter(h);  // zeroed by the previous call's reset launch
     if (h->pixels) CP_TRY(h, hipMemsetAsync(h->b.rcount, 0, sizeof(int32_t), st));
     dim3 grid(grid_for(2 * B, cp::WAVE)), block(cp::WAVE);  // two lanes per env
     hipEvent_t* ev = timing_slot(h, 0);
