@@ -21,7 +21,7 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
-#ifdef ORC_DEBUG
+#if defined(ORC_DEBUG) || defined(ORC_STATS)
 #include <stdio.h>
 #endif
 #ifdef _OPENMP
@@ -678,6 +678,23 @@ typedef struct {
     int used, fused;
 } island_t;
 
+#ifdef ORC_STATS
+/* one line per island solve: cnt of local pairs 0..4, fcnt of 0..4, merged, sweeps (stdout of a
+ * single-threaded run; env order, then substep, then island) */
+static FILE* orc_stats_f = NULL;
+void orc_stats_open(const char* path) {  /* NULL: stop recording */
+    if (orc_stats_f) fclose(orc_stats_f);
+    orc_stats_f = path ? fopen(path, "w") : NULL;
+}
+static void orc_stats_island(const island_t* I, int merged, int it) {
+    FILE* f = orc_stats_f;
+    if (!f) return;
+    for (int j = 0; j < CP_ISLAND_PAIRS; ++j) fprintf(f, "%d ", I->man[j].cnt);
+    for (int j = 0; j < CP_ISLAND_PAIRS; ++j) fprintf(f, "%d ", I->man[j].fcnt);
+    fprintf(f, "%d %d\n", merged, it);
+}
+#endif
+
 /* row sweep helpers: all normal rows, then all friction rows, of local pairs [j0, j1) */
 static void sweep_normal(sim_t* S, const cp_physics* P, island_t* I, int isl, int j, real* r) {
     int g = ISLAND_PAIR[isl][j];
@@ -830,6 +847,9 @@ static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* i
             }
             if (it > it_max) it_max = it;
             if (isl_iters && it > isl_iters[p]) isl_iters[p] = it;
+#ifdef ORC_STATS  /* diagnostic build only (tools/row_classes.py): row structure + sweeps per island */
+            orc_stats_island(I, 0, it);
+#endif
         }
     } else {
         /* global order: (0,0) (1,0) (0,1) (1,1) (0,2) (1,2) then cross (0,3) (0,4) (1,3) (1,4) */
@@ -855,6 +875,9 @@ static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* i
         if (isl_iters)
             for (int p = 0; p < CP_NUM_ISLANDS; ++p)
                 if (it > isl_iters[p]) isl_iters[p] = it;
+#ifdef ORC_STATS
+        for (int p = 0; p < CP_NUM_ISLANDS; ++p) orc_stats_island(&isl[p], 1, it);
+#endif
     }
     /* 4c. refresh the warm-start cache */
     for (int p = 0; p < CP_NUM_ISLANDS; ++p) {
