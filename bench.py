@@ -17,6 +17,8 @@ roofline: the step kernel's algorithmic HBM bytes per launch (DESIGN.md §Roofli
 its average duration from HIP events recorded on its launch stream in the timed region.
 cpu_baseline: the CPU oracle (a port: same algorithm, gcc -O2, OpenMP) on a bounded
 sample of the same workload, rank 0 at N = 1 only.
+parity: max |pose diff| over 200 steps of 512 C3 envs against the oracle's fp32 build
+(bit-exact bar) and its fp64 build (drift), rank 0 at N = 1 only, after the timed region.
 """
 import argparse
 import json
@@ -125,6 +127,50 @@ def cpu_baseline(R, budget_s):
             "sample": f"oracle/cp_oracle.c fp32 (same algorithm, gcc -O2 -march=x86-64-v3, OpenMP) on {B} envs x "
                       f"{steps} steps of the same workload (R={R}, discrete random actions, autoreset incl.); "
                       f"{dt:.1f} s wall on {used} threads"}
+
+
+def parity_check(device, R, B=512, steps=WINDOW):
+    """Checker leg (rank 0, N = 1, next to cpu_baseline): the second half of the metric,
+    max |pose - ref| over 200 steps.  pybullet is absent, so the refs are
+    the oracle's fp32 build (the kernel's bar: bit-exact) and its fp64 build (the
+    precision pybullet's double btScalar would compute the same algorithm in).  Same C3
+    config as the timed run (seed 1234, random discrete actions, autoreset), B envs,
+    `steps` steps from reset; obs = (R, 2, 7) cart + pole poses per repeat."""
+    import numpy as np
+
+    from cartpoleplusplus_amd import abi
+    from oracle import oracle as O
+    O.build()
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    cfg = O.default_config(num_envs=B, action_repeats=R, initial_force=55.0, seed=1234, autoreset=1)
+    gpu = BatchedCartpole(B, device.index, config=abi.cp_config.from_buffer_copy(cfg))
+    orc = {p: O.Envs(abi.cp_config.from_buffer_copy(cfg), precision=p) for p in ("f32", "f64")}
+    g = gpu.reset().cpu().numpy()
+    o = {p: e.reset() for p, e in orc.items()}
+    rng = np.random.default_rng(1234)
+    d64 = np.zeros((steps + 1, B))
+    d32 = np.abs(g - o["f32"]).reshape(B, -1).max(1)
+    d64[0] = np.abs(g.astype(np.float64) - o["f64"]).reshape(B, -1).max(1)
+    rew = np.zeros(B, np.float32)
+    done = np.zeros(B, np.uint8)
+    for t in range(steps):
+        a = rng.integers(0, 5, (B, 2)).astype(np.int8)
+        g = gpu.step(torch.from_numpy(a).to(device))[0].cpu().numpy()
+        for p, e in orc.items():
+            o[p] = np.zeros((B, R, 2, 7), np.float32)
+            e.step_omp(a, abi.CP_ACTION_DISCRETE, o[p], rew, done, threads)
+        d32 = np.maximum(d32, np.abs(g - o["f32"]).reshape(B, -1).max(1))
+        d64[t + 1] = np.abs(g.astype(np.float64) - o["f64"]).reshape(B, -1).max(1)
+    gpu.close()
+    per_env = d64.max(0)
+    return {"envs": B, "steps": steps, "workload": "C3 config (seed 1234, random discrete actions, autoreset)",
+            "max_abs_pose_diff_vs_oracle_f32": float(d32.max()), "bit_exact_vs_oracle_f32": bool(d32.max() == 0.0),
+            "max_abs_pose_drift_vs_oracle_f64": float(per_env.max()),
+            "median_env_max_drift_vs_oracle_f64": float(np.median(per_env)),
+            "max_drift_vs_oracle_f64_after_step": {str(k): float(d64[k].max()) for k in (1, 20, 100, steps)},
+            "vs_pybullet": None,
+            "note": "pybullet is not installed (parity with it unpinned); the fp64 column is the same algorithm in "
+                    "double precision: fp32 rounding differences grow through contact events (DESIGN.md §7)"}
 
 
 def main():
@@ -254,6 +300,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
         out["cpu_baseline"] = cpu_baseline(R, args.cpu_seconds)
+        log("parity vs oracle ...")
+        out["parity"] = parity_check(dev, R)
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:
