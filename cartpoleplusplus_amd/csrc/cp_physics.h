@@ -591,17 +591,23 @@ CP_DEV void isl_normal_rows(Isl& I, const Step& T, float* pool, float& resid) {
     }
 }
 
-template <int J>
-CP_DEV void isl_friction_rows(Isl& I, const Step& T, float mu, float* pool, float& resid) {
+template <int J, bool HOISTED = false>
+CP_DEV void isl_friction_rows(Isl& I, const Step& T, float mu, float* pool, float& resid, V3 ht1 = V3{},
+                              V3 ht2 = V3{}) {
     const uint32_t pk = T.pk[J];
     const int fcnt = pk_fcnt(pk);
     if (fcnt == 0) return;
     const int base = pk_base(pk), fbase = pk_fbase(pk);
-    // tangent basis inside the sweep (hoisted out of the PGS loop it pins VGPRs)
-    V3 n = T.n[J];
-    asm volatile("" : "+v"(n.x), "+v"(n.y), "+v"(n.z));
     V3 t1, t2;
-    plane_space(n, t1, t2);
+    if constexpr (HOISTED) {
+        t1 = ht1;
+        t2 = ht2;
+    } else {
+        // tangent basis inside the sweep (cross pairs: hoisted it would pin VGPRs for rare rows)
+        V3 n = T.n[J];
+        asm volatile("" : "+v"(n.x), "+v"(n.y), "+v"(n.z));
+        plane_space(n, t1, t2);
+    }
     for (int k = 0; k < fcnt; ++k) {
         const int s = base + k, fs = fbase + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
@@ -890,6 +896,11 @@ struct Ctx {
 CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, float* pool, float* pool0, bool second, int it0, int it1,
                    Stamps& ST) {
     const float thr = P.residual_threshold;
+    // the ground-pole pair's tangent basis (with the URDF frictions the only island pair with
+    // friction rows: the carts' friction is 0), once per substep instead of once per sweep:
+    // step kernel 0.772 -> 0.753 ms
+    V3 h1, h2;
+    plane_space(c.T.n[1], h1, h2);
     for (int it = it0; it < it1; ++it) {
         if (__ballot(c.active) == 0ull) break;
 #ifdef CP_STAMPS
@@ -912,7 +923,7 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, float* pool, float* pool
         }
         if (c.active) {
             isl_friction_rows<0>(c.I, c.T, c.mu0, pool, r);
-            isl_friction_rows<1>(c.I, c.T, c.mu1, pool, r);
+            isl_friction_rows<1, true>(c.I, c.T, c.mu1, pool, r, h1, h2);
             isl_friction_rows<2>(c.I, c.T, c.mu2, pool, r);
         }
         if (__ballot(cross) != 0ull && cross) {
