@@ -561,6 +561,50 @@ CP_DEV float isl_row(Isl& I, V3 rb, V3 t, float inv_eff, float target, float& la
     return fabsf(e * dl);
 }
 
+// isl_row<0, B> for a ground manifold whose normal is exactly +z (the static ground's top
+// face is the reference face: every pole-ground manifold of the bench steady state,
+// tools/row_classes.py).  Then plane_space gives t1 = (0, -1, 0), t2 = (1, -0, -0), and
+// every term of isl_row that multiplies an exact 0 or +-1 drops out value-exactly:
+// FMA(+-0, x, y) = y and FMA(+-1, x, y) = y +- x (finite operands; only the sign of an
+// exact zero result can differ).  KIND 0: t = n, 1: t = t1, 2: t = t2.  Same values as
+// isl_row, about 60 % of its VALU work (no r x t, 6 of the 9 products of M (r x t)).
+template <int B, int KIND, bool FRICTION>
+CP_DEV float isl_row_ez(Isl& I, V3 rb, float inv_eff, float target, float& lam, float bound) {
+    Dyn& b = dyn<B>(I);
+    const float imb = dyn_im<B>(I);
+    const Sym& M = b.M;
+    V3 ib;
+    float vn;
+    if constexpr (KIND == 0) {         // r x n = (rb.y, -rb.x, 0)
+        const float px = rb.y, py = -rb.x;
+        ib = mk(fmaf_(M.m0, px, M.m1 * py), fmaf_(M.m1, px, M.m3 * py), fmaf_(M.m2, px, M.m4 * py));
+        vn = b.v.z + fmaf_(b.w.x, px, b.w.y * py);
+    } else if constexpr (KIND == 1) {  // r x t1 = (rb.z, 0, -rb.x)
+        const float px = rb.z, pz = -rb.x;
+        ib = mk(fmaf_(M.m0, px, M.m2 * pz), fmaf_(M.m1, px, M.m4 * pz), fmaf_(M.m2, px, M.m5 * pz));
+        vn = -b.v.y + fmaf_(b.w.x, px, b.w.z * pz);
+    } else {                           // r x t2 = (0, rb.z, -rb.y)
+        const float py = rb.z, pz = -rb.y;
+        ib = mk(fmaf_(M.m1, py, M.m2 * pz), fmaf_(M.m3, py, M.m4 * pz), fmaf_(M.m4, py, M.m5 * pz));
+        vn = b.v.x + fmaf_(b.w.y, py, b.w.z * pz);
+    }
+    float e = target - vn;
+    float dl = e * inv_eff;
+    float l0 = lam + dl;
+    float ln;
+    if constexpr (!FRICTION) ln = l0 > 0.0f ? l0 : 0.0f;
+    else ln = l0 > bound ? bound : (l0 < -bound ? -bound : l0);
+    dl = ln - lam;
+    lam = ln;
+    float sb = dl * imb;
+    if constexpr (KIND == 0) b.v.z = b.v.z + sb;
+    else if constexpr (KIND == 1) b.v.y = b.v.y - sb;
+    else b.v.x = b.v.x + sb;
+    b.w = madd(b.w, ib, dl);
+    return fabsf(e * dl);
+}
+CP_DEV bool is_plus_z(V3 n) { return n.x == 0.0f && n.y == 0.0f && n.z == 1.0f; }
+
 // local pair j (0..2) of the island: (ground, cart), (ground, pole), (cart, pole)
 template <int J> constexpr int loc_a() { return J == 2 ? 1 : 0; }
 template <int J> constexpr int loc_b() { return J == 0 ? 1 : 2; }
@@ -616,6 +660,43 @@ CP_DEV void isl_friction_rows(Isl& I, const Step& T, float mu, float* pool, floa
         float r1 = isl_row<loc_a<J>(), loc_b<J>(), true>(I, rb, t1, pool_f(pool, FF_IE1, fs), 0.0f, l1, bound);
         resid = resid + r1;
         float r2 = isl_row<loc_a<J>(), loc_b<J>(), true>(I, rb, t2, pool_f(pool, FF_IE2, fs), 0.0f, l2, bound);
+        resid = resid + r2;
+        pool_f(pool, FF_L1, fs) = l1;
+        pool_f(pool, FF_L2, fs) = l2;
+    }
+}
+
+// The rows of ground pair J (0 or 1) when every lane of the wave with rows on it has a +z
+// normal (wave-uniform choice in sweeps()): the same sweep with isl_row_ez.
+template <int J>
+CP_DEV void isl_normal_rows_ez(Isl& I, const Step& T, float* pool, float& resid) {
+    static_assert(loc_a<J>() == 0, "ground pairs only");
+    const uint32_t pk = T.pk[J];
+    const int cnt = pk_cnt(pk), base = pk_base(pk);
+    for (int k = 0; k < cnt; ++k) {
+        const int s = base + k;
+        V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
+        float lam = pool_n(pool, F_LAM, s);
+        float r = isl_row_ez<loc_b<J>(), 0, false>(I, rb, pool_n(pool, F_IE, s), pool_n(pool, F_TG, s), lam, 0.0f);
+        pool_n(pool, F_LAM, s) = lam;
+        resid = resid + r;
+    }
+}
+template <int J>
+CP_DEV void isl_friction_rows_ez(Isl& I, const Step& T, float mu, float* pool, float& resid) {
+    static_assert(loc_a<J>() == 0, "ground pairs only");
+    const uint32_t pk = T.pk[J];
+    const int fcnt = pk_fcnt(pk);
+    if (fcnt == 0) return;
+    const int base = pk_base(pk), fbase = pk_fbase(pk);
+    for (int k = 0; k < fcnt; ++k) {
+        const int s = base + k, fs = fbase + k;
+        V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
+        float bound = mu * pool_n(pool, F_LAM, s);
+        float l1 = pool_f(pool, FF_L1, fs), l2 = pool_f(pool, FF_L2, fs);
+        float r1 = isl_row_ez<loc_b<J>(), 1, true>(I, rb, pool_f(pool, FF_IE1, fs), 0.0f, l1, bound);
+        resid = resid + r1;
+        float r2 = isl_row_ez<loc_b<J>(), 2, true>(I, rb, pool_f(pool, FF_IE2, fs), 0.0f, l2, bound);
         resid = resid + r2;
         pool_f(pool, FF_L1, fs) = l1;
         pool_f(pool, FF_L2, fs) = l2;
@@ -901,6 +982,17 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, float* pool, float* pool
     // step kernel 0.772 -> 0.753 ms
     V3 h1, h2;
     plane_space(c.T.n[1], h1, h2);
+    // ground pairs whose rows all have a +z normal in this wave run isl_row_ez (wave-uniform):
+    // the ground-pole pair in every measured wave, the ground-cart pair in ~3 of 4
+#ifdef CP_NO_EZ
+    const bool ez0 = false, ez1 = false;
+#elif defined(CP_EZ1_ONLY)
+    const bool ez0 = false;
+    const bool ez1 = __ballot(pk_cnt(c.T.pk[1]) > 0 && !is_plus_z(c.T.n[1])) == 0ull;
+#else
+    const bool ez0 = __ballot(pk_cnt(c.T.pk[0]) > 0 && !is_plus_z(c.T.n[0])) == 0ull;
+    const bool ez1 = __ballot(pk_cnt(c.T.pk[1]) > 0 && !is_plus_z(c.T.n[1])) == 0ull;
+#endif
     for (int it = it0; it < it1; ++it) {
         if (__ballot(c.active) == 0ull) break;
 #ifdef CP_STAMPS
@@ -908,8 +1000,10 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, float* pool, float* pool
 #endif
         float r = 0.0f, rc = 0.0f;
         if (c.active) {
-            isl_normal_rows<0>(c.I, c.T, pool, r);
-            isl_normal_rows<1>(c.I, c.T, pool, r);
+            if (ez0) isl_normal_rows_ez<0>(c.I, c.T, pool, r);
+            else isl_normal_rows<0>(c.I, c.T, pool, r);
+            if (ez1) isl_normal_rows_ez<1>(c.I, c.T, pool, r);
+            else isl_normal_rows<1>(c.I, c.T, pool, r);
             isl_normal_rows<2>(c.I, c.T, pool, r);
         }
         const bool cross = c.active && c.merged;  // same on both lanes of an env
@@ -922,8 +1016,10 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, float* pool, float* pool
             cross_back(c.I, S, second);
         }
         if (c.active) {
-            isl_friction_rows<0>(c.I, c.T, c.mu0, pool, r);
-            isl_friction_rows<1, true>(c.I, c.T, c.mu1, pool, r, h1, h2);
+            if (ez0) isl_friction_rows_ez<0>(c.I, c.T, c.mu0, pool, r);
+            else isl_friction_rows<0>(c.I, c.T, c.mu0, pool, r);
+            if (ez1) isl_friction_rows_ez<1>(c.I, c.T, c.mu1, pool, r);
+            else isl_friction_rows<1, true>(c.I, c.T, c.mu1, pool, r, h1, h2);
             isl_friction_rows<2>(c.I, c.T, c.mu2, pool, r);
         }
         if (__ballot(cross) != 0ull && cross) {

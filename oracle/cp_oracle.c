@@ -691,7 +691,11 @@ static void orc_stats_island(const island_t* I, int merged, int it) {
     if (!f) return;
     for (int j = 0; j < CP_ISLAND_PAIRS; ++j) fprintf(f, "%d ", I->man[j].cnt);
     for (int j = 0; j < CP_ISLAND_PAIRS; ++j) fprintf(f, "%d ", I->man[j].fcnt);
-    fprintf(f, "%d %d\n", merged, it);
+    fprintf(f, "%d %d", merged, it);
+    /* per pair: 1 when the manifold normal is exactly +z (the ground's top face is the reference) */
+    for (int j = 0; j < CP_ISLAND_PAIRS; ++j)
+        fprintf(f, " %d", I->man[j].n.x == RC(0) && I->man[j].n.y == RC(0) && I->man[j].n.z == RC(1));
+    fprintf(f, "\n");
 }
 #endif
 

@@ -66,7 +66,7 @@ def main():
     a = np.loadtxt(path, dtype=np.int64)
     # rows: per step, per env, per substep, 2 islands (merged envs also emit 2 lines)
     a = a.reshape(args.steps, B, R, 2, -1)
-    cnt, fcnt, merged, sw = a[..., 0:5], a[..., 5:10], a[..., 10], a[..., 11]
+    cnt, fcnt, merged, sw, ez = a[..., 0:5], a[..., 5:10], a[..., 10], a[..., 11], a[..., 12:17]
     print(f"island solves: {sw.size}, merged env-substeps {merged[..., 0].mean():.4f}")
     print(f"sweeps: mean {sw.mean():.2f}, median {np.median(sw):.0f}, capped(50) {np.mean(sw >= 50):.3f}")
     sig = [tuple(x) for x in np.concatenate([cnt[..., :3], fcnt[..., :3]], -1).reshape(-1, 6)]
