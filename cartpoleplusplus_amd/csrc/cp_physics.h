@@ -666,6 +666,9 @@ CP_DEV void isl_friction_rows(Isl& I, const Step& T, float mu, float* pool, floa
     }
 }
 
+// row loops unrolled to the 4-point manifold bound (a box pair makes at most 4 points):
+// step kernel 0.709 -> 0.692 ms against the counted loop
+#define CP_EZ_LOOP(k, n) _Pragma("unroll") for (int k = 0; k < 4; ++k) if (k < (n))
 // The rows of ground pair J (0 or 1) when every lane of the wave with rows on it has a +z
 // normal (wave-uniform choice in sweeps()): the same sweep with isl_row_ez.
 template <int J>
@@ -673,7 +676,7 @@ CP_DEV void isl_normal_rows_ez(Isl& I, const Step& T, float* pool, float& resid)
     static_assert(loc_a<J>() == 0, "ground pairs only");
     const uint32_t pk = T.pk[J];
     const int cnt = pk_cnt(pk), base = pk_base(pk);
-    for (int k = 0; k < cnt; ++k) {
+    CP_EZ_LOOP(k, cnt) {
         const int s = base + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
         float lam = pool_n(pool, F_LAM, s);
@@ -689,7 +692,7 @@ CP_DEV void isl_friction_rows_ez(Isl& I, const Step& T, float mu, float* pool, f
     const int fcnt = pk_fcnt(pk);
     if (fcnt == 0) return;
     const int base = pk_base(pk), fbase = pk_fbase(pk);
-    for (int k = 0; k < fcnt; ++k) {
+    CP_EZ_LOOP(k, fcnt) {
         const int s = base + k, fs = fbase + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
         float bound = mu * pool_n(pool, F_LAM, s);
