@@ -14,7 +14,8 @@ global env ids offset rank*B); the only collective is an RCCL all-gather of the
 episode returns once per 200-step window (C4).  value = N*B*K / max-over-ranks wall.
 
 roofline: the step kernel's algorithmic HBM bytes per launch over
-its average duration from HIP events recorded on its launch stream in the timed region.
+its average duration from HIP events recorded on its launch stream in the timed region
+(every 4th launch sampled: the events themselves cost wall time).
 cpu_baseline: the CPU oracle (a port: same algorithm, gcc -O2, OpenMP) on a bounded
 sample of the same workload, rank 0 at N = 1 only.
 parity: max |pose diff| over 200 steps of 512 C3 envs against the oracle's fp32 build
@@ -38,6 +39,10 @@ from cartpoleplusplus_amd.dist import gather_returns, return_histogram, shard_sp
 METRIC = "env-steps/sec at batch=65,536, 1→8 MI355X; max |pose−pybullet| over 200 steps"
 HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s spec, 6.29 measured)
 WINDOW = 200            # episode-return reporting window (steps)
+# HIP events around every 4th step-kernel launch (every reset launch): each recorded event
+# costs the stream a few microseconds (tools/timing_overhead.py: 0.761 ms/step with events on
+# every launch, 0.755 with this sampling, 0.748 without events)
+STEP_EVENT_STRIDE = 4
 
 
 def step_kernel_bytes(R, action_bytes):
@@ -218,6 +223,7 @@ def main():
     log(f"rank {rank}: B={B} R={R} warmup {W} done; timing {K} steps")
 
     env.timing_begin(K)
+    env.timing_stride(STEP_EVENT_STRIDE, 1)
     hist = None
     if world > 1:
         dist.barrier()
@@ -291,6 +297,7 @@ def main():
                      "bytes_per_launch": bytes_launch,
                      "avg_launch_ms": round(per_launch_s * 1e3, 4),
                      "launches": tm["step_launches"],
+                     "launch_sample_stride": STEP_EVENT_STRIDE,
                      "reset_kernel_avg_ms": round(tm["reset_ms"] / max(1, tm["reset_launches"]), 4),
                      **({"step_kernel_avg_ms": round(tm["step_ms"] / max(1, tm["step_launches"]), 4),
                          "render_launches": tm["render_launches"]} if args.raster else {})},

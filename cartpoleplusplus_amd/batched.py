@@ -167,6 +167,11 @@ class BatchedCartpole:
         """Record HIP events around every step / reset kernel launch (see cp_timing_begin)."""
         native.check(self.h, self.lib.cp_timing_begin(self.h, int(max_launches)), "cp_timing_begin")
 
+    def timing_stride(self, step_stride=1, reset_stride=1):
+        """Sample the events: every step_stride-th step launch, reset_stride-th reset launch."""
+        native.check(self.h, self.lib.cp_timing_stride(self.h, int(step_stride), int(reset_stride)),
+                     "cp_timing_stride")
+
     def timing_end(self):
         """-> dict(step_ms, step_launches, reset_ms, reset_launches); synchronises."""
         sm, rm = C.c_double(), C.c_double()

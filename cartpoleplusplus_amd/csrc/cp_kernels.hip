@@ -960,6 +960,8 @@ __global__ void __launch_bounds__(256) cp_copy_kernel(const float* src, float* d
 struct cp_timing {
     int cap = 0;                             // event pairs per kind
     int nstep = 0, nreset = 0, nrender = 0;  // pairs recorded
+    int stride[3] = {1, 1, 1};               // record every stride-th launch of a kind
+    int seen[3] = {0, 0, 0};                 // launches of a kind since cp_timing_begin
     double render_ms = 0.0;                  // summed by cp_timing_end
     int render_launches = 0;
     std::vector<hipEvent_t> ev;  // [0, 2cap): step pairs, [2cap, 4cap): reset, [4cap, 6cap): render
@@ -986,11 +988,13 @@ static void timing_free(cp_timing& t) {
     for (hipEvent_t e : t.ev) (void)hipEventDestroy(e);
     t.ev.clear();
     t.cap = t.nstep = t.nreset = t.nrender = 0;
+    for (int k = 0; k < 3; ++k) t.stride[k] = 1, t.seen[k] = 0;
 }
 // returns the event pair to record around a launch of `kind` (0 step, 1 reset, 2 render), or nullptr
 static hipEvent_t* timing_slot(cp_handle* h, int kind) {
     cp_timing& t = h->timing;
     if (t.cap == 0) return nullptr;
+    if (t.seen[kind]++ % t.stride[kind] != 0) return nullptr;
     int& n = kind == 0 ? t.nstep : (kind == 1 ? t.nreset : t.nrender);
     if (n >= (kind == 2 ? 2 * t.cap : t.cap)) return nullptr;  // up to 2 render launches per step
     hipEvent_t* p = &t.ev[(size_t)(kind * t.cap + n) * 2];
@@ -1385,6 +1389,13 @@ int cp_timing_begin(cp_handle* h, int max_launches) {
     h->timing.ev.resize((size_t)max_launches * 8);
     for (auto& e : h->timing.ev) CP_TRY(h, hipEventCreate(&e));
     h->timing.cap = max_launches;
+    return 0;
+}
+
+int cp_timing_stride(cp_handle* h, int step_stride, int reset_stride) {
+    if (!h || step_stride <= 0 || reset_stride <= 0) return fail(h, "cp_timing_stride: bad argument");
+    h->timing.stride[0] = step_stride;
+    h->timing.stride[1] = reset_stride;
     return 0;
 }
 

@@ -17,6 +17,7 @@ EXPORTS = (
     "cp_default_config", "cp_create", "cp_destroy", "cp_last_error", "cp_abi_version",
     "cp_reset", "cp_step", "cp_set_readback", "cp_set_bump_forces", "cp_get_state",
     "cp_set_state", "cp_episode_returns", "cp_overflow_counts", "cp_timing_begin", "cp_timing_end",
+    "cp_timing_stride",
     "cp_debug_stamps", "cp_default_raster_config", "cp_set_raster", "cp_timing_render",
     "cp_event_record_bytes", "cp_encode_events", "cp_eventlog_open", "cp_eventlog_write", "cp_eventlog_close",
     "cp_set_lqr", "cp_get_stepped", "cp_replay_init", "cp_replay_add", "cp_replay_sample",
@@ -56,6 +57,7 @@ def load():
         "cp_episode_returns": (I, [VP, VP, VP, VP]),
         "cp_overflow_counts": (I, [VP, VP, VP]),
         "cp_timing_begin": (I, [VP, I]),
+        "cp_timing_stride": (I, [VP, I, I]),
         "cp_debug_stamps": (I, [VP, P(C.c_uint64), I]),
         "cp_timing_end": (I, [VP, P(C.c_double), P(C.c_int32), P(C.c_double), P(C.c_int32)]),
         "cp_default_raster_config": (None, [P(abi.cp_raster_config)]),

@@ -214,6 +214,12 @@ int cp_overflow_counts(cp_handle* h, int32_t* out, void* stream);
 int cp_timing_begin(cp_handle* h, int max_launches);
 int cp_timing_end(cp_handle* h, double* step_ms, int32_t* step_launches, double* reset_ms,
                   int32_t* reset_launches);
+/* Record events around every `step_stride`-th step-kernel launch and every
+ * `reset_stride`-th reset-kernel launch only (default 1, 1; set after cp_timing_begin,
+ * which resets them): each recorded event costs the stream a few microseconds, so a
+ * sampled average keeps that cost out of the timed throughput.  The launch counts
+ * returned by cp_timing_end are the sampled ones. */
+int cp_timing_stride(cp_handle* h, int step_stride, int reset_stride);
 
 /* Diagnostics of a stamp build (-DCP_STAMPS): host array of 16 counters summed over
  * waves since the last reset, 8 for the step / head kernel then 8 for the tail
