@@ -190,6 +190,9 @@ def main():
     ap.add_argument("--raster", action="store_true",
                     help="BASELINE.json configs[4] (C5): + in-kernel 50x50x3 fp16 raster obs per repeat")
     ap.add_argument("--cameras", type=int, default=1)
+    ap.add_argument("--done-on-bounds", action="store_true",
+                    help="the reference's commented-out bounds termination (bullet_cartpole.py:243-253): "
+                         "episodes end early, so the C4 return histogram is not degenerate (diagnostic config)")
     ap.add_argument("--solver-iterations", type=int, default=None,
                     help="override the PGS sweep cap (default: the model's 50; non-default runs are diagnostics)")
     args = ap.parse_args()
@@ -207,7 +210,7 @@ def main():
     B, R, K, W = args.batch, args.repeats, args.steps, args.warmup
     spec = shard_spec(B, rank, world, seed=1234 + rank)
     env = BatchedCartpole(B, local, action_repeats=R, steps_per_repeat=1, max_episode_len=200,
-                          initial_force=55.0, autoreset=True, seed=spec["seed"],
+                          initial_force=55.0, autoreset=True, seed=spec["seed"], done_on_bounds=args.done_on_bounds,
                           env_id_offset=spec["env_id_offset"],
                           **({} if args.solver_iterations is None else {"solver_iterations": args.solver_iterations}))
     if args.raster:
@@ -303,6 +306,7 @@ def main():
                          "render_launches": tm["render_launches"]} if args.raster else {})},
         "valu": valu,
         "episode_return_hist_nonzero": None if hist is None else int((hist > 0).sum().item()),
+        "done_on_bounds": bool(args.done_on_bounds),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
