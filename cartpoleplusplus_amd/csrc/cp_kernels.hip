@@ -287,7 +287,14 @@ __global__ void __launch_bounds__(256) cp_mask_to_list_kernel(int B, const uint8
     if (want) list[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
 }
 
-__global__ void CP_PHYS_ATTR cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
+// LAT = false: the throughput shape of the step kernel (2 waves per SIMD), for reset bursts
+// (fixed-length episodes end together).  LAT = true: one wave per SIMD with 512 registers and
+// fast-form rows, for the short lists of desynchronised episodes (bounds termination), where
+// the 130 serial substeps of one wave are the whole latency of the step.
+template <bool LAT>
+__global__ void __launch_bounds__(WAVE)
+__attribute__((amdgpu_waves_per_eu(LAT ? 1 : CP_WAVES_PER_EU, LAT ? 1 : CP_WAVES_PER_EU)))
+cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     __shared__ float lds_pool[POOL_FLOATS * WAVE];
     const int B = cfg.num_envs;
     const int t = blockIdx.x * WAVE + threadIdx.x;
@@ -321,7 +328,7 @@ __global__ void CP_PHYS_ATTR cp_reset_kernel(cp_config cfg, Bufs b, float* obs_o
     int ov = 0;
     const int nsub = cfg.settle_steps + cfg.initial_force_steps;
     for (int s = 0; s < nsub; ++s) {
-        substep(S, cfg.phys, L, pool, pool0, ov, G, ST);
+        substep<LAT>(S, cfg.phys, L, pool, pool0, ov, G, ST);
         const int k = s - cfg.settle_steps;
         if (k >= 0) {
             float fx, fy;
@@ -981,8 +988,11 @@ struct cp_handle {
     int32_t* count2;   // [2] reset-list counters, alternating by call: each reset launch zeroes the other one
     int par;           // counter the next call appends to
     int head;          // PGS sweeps of the head kernel (CP_HEAD_SWEEPS, default 6)
+    int reset_lat;     // 1: latency-shaped autoreset kernel (episodes end at different steps)
     std::string err;
 };
+
+static void choose_reset_shape(cp_handle* h);
 
 static void timing_free(cp_timing& t) {
     for (hipEvent_t e : t.ev) (void)hipEventDestroy(e);
@@ -1110,6 +1120,7 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
         h->head = hs ? std::atoi(hs) : 6;
         if (h->head < 0) h->head = 0;
     }
+    choose_reset_shape(h);
     cp_default_raster_config(&h->raster);
     std::memset(&h->b, 0, sizeof(h->b));
     const size_t B = (size_t)cfg->num_envs;
@@ -1224,11 +1235,30 @@ static void use_counter(cp_handle* h) {
     h->par ^= 1;
 }
 
+// Which autoreset kernel shape (cp_reset_kernel<LAT>): episodes that can end early (bounds
+// termination, LQR done thresholds) end at different steps, so every step resets a short list
+// and its latency is the step's; fixed-length episodes end together in bursts (throughput).
+// CP_RESET_LATENCY=0/1 overrides (diagnostics).
+static void choose_reset_shape(cp_handle* h) {
+    const char* e = std::getenv("CP_RESET_LATENCY");
+    if (e && (e[0] == '0' || e[0] == '1')) {
+        h->reset_lat = e[0] == '1';
+        return;
+    }
+    const bool lqr_done = h->lqr.gains && (h->lqr.done_pos > 0.0f || h->lqr.done_angle > 0.0f);
+    h->reset_lat = (h->cfg.done_on_bounds || lqr_done) ? 1 : 0;
+}
+
 static int launch_reset_from_list(cp_handle* h, float* obs_out, hipStream_t st, bool render) {
     const int B = h->cfg.num_envs;
     hipEvent_t* ev = timing_slot(h, 1);
     if (ev) CP_TRY(h, hipEventRecord(ev[0], st));
-    hipLaunchKernelGGL(cp::cp_reset_kernel, dim3(grid_for(2 * B, cp::WAVE)), dim3(cp::WAVE), 0, st, h->cfg, h->b, obs_out);
+    if (h->reset_lat)
+        hipLaunchKernelGGL(cp::cp_reset_kernel<true>, dim3(grid_for(2 * B, cp::WAVE)), dim3(cp::WAVE), 0, st, h->cfg,
+                           h->b, obs_out);
+    else
+        hipLaunchKernelGGL(cp::cp_reset_kernel<false>, dim3(grid_for(2 * B, cp::WAVE)), dim3(cp::WAVE), 0, st, h->cfg,
+                           h->b, obs_out);
     if (check(h, hipGetLastError(), "cp_reset_kernel")) return -1;
     if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
     if (render && h->pixels) return launch_render(h, h->b.list, h->b.count, st);
@@ -1323,6 +1353,7 @@ int cp_set_lqr(cp_handle* h, const float* gains, int per_env, float* state8_out,
     h->lqr.state8 = state8_out;
     h->lqr.done_pos = done_pos;
     h->lqr.done_angle = done_angle;
+    choose_reset_shape(h);
     return 0;
 }
 

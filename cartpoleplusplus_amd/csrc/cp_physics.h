@@ -1651,12 +1651,14 @@ CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx
 
 
 // One p.stepSimulation() for this lane's env, without migration (all sweeps in place).
+// FAST: fast-form island rows where the wave allows them (the 512-register kernels).
+template <bool FAST = false>
 CP_DEV void substep(Sim& S, const cp_physics& P, const Lane& L, float* pool, float* pool0, int& overflow,
                     const Mem& G, Stamps& ST, bool live = true) {
     Ctx c;
     substep_prep(S, P, L, pool, pool0, overflow, G, ST, live, c);
     CP_STAMP(t2);
-    solve_range<false>(c, S, P, pool, pool0, L.isl != 0, 0, P.solver_iterations, ST);
+    solve_range<FAST>(c, S, P, pool, pool0, L.isl != 0, 0, P.solver_iterations, ST);
     CP_STAMP(t3);
     CP_ACC(solve, t2, t3);
     substep_finish(S, P, L, c, pool, G, ST, live);
