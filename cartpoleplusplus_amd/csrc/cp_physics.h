@@ -14,6 +14,8 @@
 #include "../../include/cartpole_amd.h"
 #include "cp_math.h"
 
+#include <type_traits>
+
 namespace cp {
 
 // Diagnostic phase stamps (built only with -DCP_STAMPS; see cp_debug_stamps).
@@ -1426,16 +1428,28 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, float* pool
     // 2. narrowphase + row setup of the lane's island: wave-uniform loop over its 5
     //    local pairs (the global pair, hence the bodies, differ between the two lanes)
     int used = 0, fused = 0;
-#pragma unroll 1
-    for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
+    // one local pair; GROUND: j is 0 or 1, whose first body is the static ground on both
+    // islands, so its box is compile-time (centre 0, identity axes: box_sel's exact values)
+    auto pair_body = [&](auto ground_tag, const int j) {
+        constexpr bool GROUND = decltype(ground_tag)::value;
         const int g = island_pair(L.isl, j);
-        const int a = pair_a(g), b = pair_b(g);
+        const int a = GROUND ? 0 : pair_a(g), b = pair_b(g);
         CP_STAMP(n0);
         // warm-start cache of the pair, loaded first: its latency overlaps the narrowphase
         const uint32_t oid = __float_as_uint(G.lw(CP_SF_WS_ID(0, j)));
         const float ol0 = G.ll(CP_SF_WS_LAM(0, j, 0)), ol1 = G.ll(CP_SF_WS_LAM(0, j, 1));
         const float ol2 = G.ll(CP_SF_WS_LAM(0, j, 2)), ol3 = G.ll(CP_SF_WS_LAM(0, j, 3));
-        const Box A = box_sel(a, S, P), Bx = box_sel(b, S, P);
+        Box A;
+        if constexpr (GROUND) {
+            A.c = mk(0.0f, 0.0f, 0.0f);
+            A.ax = quat_axes(0.0f, 0.0f, 0.0f, 1.0f);
+            A.h0 = P.half_extents[0][0];
+            A.h1 = P.half_extents[0][1];
+            A.h2 = P.half_extents[0][2];
+        } else {
+            A = box_sel(a, S, P);
+        }
+        const Box Bx = box_sel(b, S, P);
         Contact C;
         C.m = 0;
         C.n = mk(0.0f, 0.0f, 1.0f);
@@ -1517,7 +1531,16 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, float* pool
         }
 #endif
         if (live) G.sw(CP_SF_WS_ID(0, j), __uint_as_float(nid));
-    }
+    };
+#ifdef CP_NO_GROUND_PEEL
+#pragma unroll 1
+    for (int j = 0; j < CP_ISLAND_PAIRS; ++j) pair_body(std::false_type{}, j);
+#else
+#pragma unroll 1
+    for (int j = 0; j < 2; ++j) pair_body(std::true_type{}, j);
+#pragma unroll 1
+    for (int j = 2; j < CP_ISLAND_PAIRS; ++j) pair_body(std::false_type{}, j);
+#endif
 #ifdef CP_HDR_SCRATCH
 #pragma unroll
     for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
