@@ -595,7 +595,13 @@ CP_DEV float isl_row_ez(Isl& I, V3 rb, float inv_eff, float target, float& lam, 
     float l0 = lam + dl;
     float ln;
     if constexpr (!FRICTION) ln = l0 > 0.0f ? l0 : 0.0f;
+#ifdef CP_NO_MED3
     else ln = l0 > bound ? bound : (l0 < -bound ? -bound : l0);
+#else
+    // the friction clamp as one v_med3_f32 (bound >= 0): the same value as the oracle's
+    // compare chain for every non-NaN l0, one dependent instruction instead of three
+    else ln = __builtin_amdgcn_fmed3f(l0, -bound, bound);
+#endif
     dl = ln - lam;
     lam = ln;
     float sb = dl * imb;
