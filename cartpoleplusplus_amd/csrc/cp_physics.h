@@ -997,9 +997,6 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, float* pool, float* pool
     // the ground-pole pair in every measured wave, the ground-cart pair in ~3 of 4
 #ifdef CP_NO_EZ
     const bool ez0 = false, ez1 = false;
-#elif defined(CP_EZ1_ONLY)
-    const bool ez0 = false;
-    const bool ez1 = __ballot(pk_cnt(c.T.pk[1]) > 0 && !is_plus_z(c.T.n[1])) == 0ull;
 #else
     const bool ez0 = __ballot(pk_cnt(c.T.pk[0]) > 0 && !is_plus_z(c.T.n[0])) == 0ull;
     const bool ez1 = __ballot(pk_cnt(c.T.pk[1]) > 0 && !is_plus_z(c.T.n[1])) == 0ull;
