@@ -1237,7 +1237,8 @@ static void use_counter(cp_handle* h) {
 
 // Which autoreset kernel shape (cp_reset_kernel<LAT>): episodes that can end early (bounds
 // termination, LQR done thresholds) end at different steps, so every step resets a short list
-// and its latency is the step's; fixed-length episodes end together in bursts (throughput).
+// and its latency is the step's; fixed-length episodes end together in bursts (throughput),
+// except in batches small enough that a burst fits one wave per SIMD.
 // CP_RESET_LATENCY=0/1 overrides (diagnostics).
 static void choose_reset_shape(cp_handle* h) {
     const char* e = std::getenv("CP_RESET_LATENCY");
@@ -1246,7 +1247,10 @@ static void choose_reset_shape(cp_handle* h) {
         return;
     }
     const bool lqr_done = h->lqr.gains && (h->lqr.done_pos > 0.0f || h->lqr.done_angle > 0.0f);
-    h->reset_lat = (h->cfg.done_on_bounds || lqr_done) ? 1 : 0;
+    // up to 32,768 envs every reset wave gets a SIMD of its own even in a full burst (1,024 SIMDs),
+    // so the latency shape is never the slower one there
+    const bool small = h->cfg.num_envs <= 32768;
+    h->reset_lat = (h->cfg.done_on_bounds || lqr_done || small) ? 1 : 0;
 }
 
 static int launch_reset_from_list(cp_handle* h, float* obs_out, hipStream_t st, bool render) {
