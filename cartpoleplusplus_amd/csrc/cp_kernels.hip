@@ -357,10 +357,13 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     b.ret_acc[i] = 0.0f;
 }
 
-template <int KIND, bool LQR>
-__global__ void CP_PHYS_ATTR cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out,
-                                                        float* reward_out, uint8_t* done_out, float* term_out,
-                                                        float* readback, int rb_bug, Lqr lq) {
+// LAT: the latency shape of cp_reset_kernel<true> (1 wave per SIMD, 512 registers, fast-form
+// rows) for batches whose waves all get a SIMD of their own (<= 32,768 envs)
+template <int KIND, bool LQR, bool LAT>
+__global__ void __launch_bounds__(WAVE)
+__attribute__((amdgpu_waves_per_eu(LAT ? 1 : CP_WAVES_PER_EU, LAT ? 1 : CP_WAVES_PER_EU)))
+cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float* reward_out, uint8_t* done_out,
+               float* term_out, float* readback, int rb_bug, Lqr lq) {
     __shared__ float lds_pool[POOL_FLOATS * WAVE];
     const int B = cfg.num_envs;
     const int t = blockIdx.x * WAVE + threadIdx.x;
@@ -414,7 +417,7 @@ __global__ void CP_PHYS_ATTR cp_step_kernel(cp_config cfg, Bufs b, const void* a
             }
             for (int r = 0; r < R; ++r) {
                 for (int s = 0; s < SR; ++s) {
-                    substep(S, cfg.phys, L, pool, pool0, ov, G, ST);
+                    substep<LAT>(S, cfg.phys, L, pool, pool0, ov, G, ST);
                     if constexpr (LQR) {  // disturbance + control (:897-901), control from the pre-step state
                         apply_force_link<0>(S, f00 + u[0][0], f01 + u[0][1]);
                         apply_force_link<1>(S, f10 + u[1][0], f11 + u[1][1]);
@@ -989,6 +992,7 @@ struct cp_handle {
     int par;           // counter the next call appends to
     int head;          // PGS sweeps of the head kernel (CP_HEAD_SWEEPS, default 6)
     int reset_lat;     // 1: latency-shaped autoreset kernel (episodes end at different steps)
+    int step_lat;      // 1: latency-shaped step kernel (every wave gets a SIMD of its own)
     std::string err;
 };
 
@@ -1239,18 +1243,17 @@ static void use_counter(cp_handle* h) {
 // termination, LQR done thresholds) end at different steps, so every step resets a short list
 // and its latency is the step's; fixed-length episodes end together in bursts (throughput),
 // except in batches small enough that a burst fits one wave per SIMD.
-// CP_RESET_LATENCY=0/1 overrides (diagnostics).
+// The step kernel has the same two shapes, chosen by batch size alone.  CP_RESET_LATENCY=0/1 and
+// CP_STEP_LATENCY=0/1 override (diagnostics).
 static void choose_reset_shape(cp_handle* h) {
-    const char* e = std::getenv("CP_RESET_LATENCY");
-    if (e && (e[0] == '0' || e[0] == '1')) {
-        h->reset_lat = e[0] == '1';
-        return;
-    }
     const bool lqr_done = h->lqr.gains && (h->lqr.done_pos > 0.0f || h->lqr.done_angle > 0.0f);
-    // up to 32,768 envs every reset wave gets a SIMD of its own even in a full burst (1,024 SIMDs),
-    // so the latency shape is never the slower one there
+    // up to 32,768 envs every wave gets a SIMD of its own even in a full burst (1,024 SIMDs), so
+    // the latency shape is never the slower one there
     const bool small = h->cfg.num_envs <= 32768;
-    h->reset_lat = (h->cfg.done_on_bounds || lqr_done || small) ? 1 : 0;
+    const char* e = std::getenv("CP_RESET_LATENCY");
+    h->reset_lat = (e && (e[0] == '0' || e[0] == '1')) ? e[0] == '1' : (h->cfg.done_on_bounds || lqr_done || small);
+    const char* es = std::getenv("CP_STEP_LATENCY");
+    h->step_lat = (es && (es[0] == '0' || es[0] == '1')) ? es[0] == '1' : small;
 }
 
 static int launch_reset_from_list(cp_handle* h, float* obs_out, hipStream_t st, bool render) {
@@ -1297,9 +1300,17 @@ int cp_step(cp_handle* h, const void* actions, int action_kind, float* obs_out, 
     if (ev) CP_TRY(h, hipEventRecord(ev[0], st));
     const bool lqr = h->lqr.gains != nullptr;
     if (h->mono) {
-#define CP_LAUNCH_STEP(K, Q)                                                                                   \
-    hipLaunchKernelGGL((cp::cp_step_kernel<K, Q>), grid, block, 0, st, h->cfg, h->b, actions, obs_out, reward_out, \
-                       done_out, terminal_obs_out, h->readback, h->readback_bug, h->lqr)
+#define CP_LAUNCH_STEP(K, Q)                                                                                    \
+    do {                                                                                                        \
+        if (h->step_lat)                                                                                        \
+            hipLaunchKernelGGL((cp::cp_step_kernel<K, Q, true>), grid, block, 0, st, h->cfg, h->b, actions,     \
+                               obs_out, reward_out, done_out, terminal_obs_out, h->readback, h->readback_bug,    \
+                               h->lqr);                                                                         \
+        else                                                                                                    \
+            hipLaunchKernelGGL((cp::cp_step_kernel<K, Q, false>), grid, block, 0, st, h->cfg, h->b, actions,    \
+                               obs_out, reward_out, done_out, terminal_obs_out, h->readback, h->readback_bug,    \
+                               h->lqr);                                                                         \
+    } while (0)
         if (action_kind == CP_ACTION_CONTINUOUS) {
             if (lqr) CP_LAUNCH_STEP(CP_ACTION_CONTINUOUS, true);
             else CP_LAUNCH_STEP(CP_ACTION_CONTINUOUS, false);
