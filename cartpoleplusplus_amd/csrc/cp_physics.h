@@ -548,7 +548,7 @@ CP_DEV float isl_row(Isl& I, V3 rb, V3 t, float inv_eff, float target, float& la
     float l0 = lam + dl;
     float ln;
     if constexpr (!FRICTION) ln = l0 > 0.0f ? l0 : 0.0f;
-    else ln = l0 > bound ? bound : (l0 < -bound ? -bound : l0);
+    else ln = __builtin_amdgcn_fmed3f(l0, -bound, bound);  // = the oracle's clamp (see isl_row_ez)
     dl = ln - lam;
     lam = ln;
     float sb = dl * imb;
@@ -773,7 +773,7 @@ CP_DEV float solve_row(Sim& S, const Step& T, const cp_physics& P, V3 rb, V3 t, 
     float l0 = lam + dl;
     float ln;
     if constexpr (!FRICTION) ln = l0 > 0.0f ? l0 : 0.0f;
-    else ln = l0 > bound ? bound : (l0 < -bound ? -bound : l0);
+    else ln = __builtin_amdgcn_fmed3f(l0, -bound, bound);  // = the oracle's clamp (see isl_row_ez)
     dl = ln - lam;
     lam = ln;
     float sb = dl * imb;
@@ -1152,7 +1152,7 @@ CP_DEV float fast_grow(Dyn& b, float imb, V3 t, V3 rbt, V3 ib, float inv_eff, fl
     const float l0 = lam + dl;
     float ln;
     if constexpr (!FRICTION) ln = l0 > 0.0f ? l0 : 0.0f;
-    else ln = l0 > bound ? bound : (l0 < -bound ? -bound : l0);
+    else ln = __builtin_amdgcn_fmed3f(l0, -bound, bound);  // = the oracle's clamp (see isl_row_ez)
     dl = ln - lam;
     lam = ln;
     const float sb = dl * imb;
