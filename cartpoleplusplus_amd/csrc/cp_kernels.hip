@@ -58,10 +58,6 @@ struct Bufs {
     int32_t* rlist;    // [B] envs to render after the step kernel
     int32_t* rcount;   // [1]
     uint8_t* stepped;  // [B] 1 = simulated by the last cp_step (event log: done-before envs are not logged)
-    float* stage;      // [STAGE_FIELDS][3][2B] solve context of the tail envs, one column per lane, at list position
-    int32_t* slist;    // [3][B] tail envs of the current substep, per tail class
-    int32_t* scount;   // [R*S][3] their counts, per substep of the step
-    float* lqr;        // [5][B] LQR forces u (2 x 2) and the both-pairs-out flag between substep launches
 };
 
 // raster obs: the repeat-end pose of the 4 bodies (xyz, quat xyzw) for the render kernel
@@ -86,7 +82,7 @@ CP_DEV void flush_stamps(const Stamps& ST, uint64_t* dst, uint64_t total) {
         atomicAdd((unsigned long long*)&dst[5], (unsigned long long)ST.substeps);
         atomicAdd((unsigned long long*)&dst[6], (unsigned long long)total);
         atomicAdd((unsigned long long*)&dst[7], 1ull);
-        if (ST.bb) {  // narrowphase split of the fused / head kernel into the spare tail slots
+        if (ST.bb) {  // narrowphase split into the spare slots 8-10
             atomicAdd((unsigned long long*)&dst[8], (unsigned long long)ST.sel);
             atomicAdd((unsigned long long*)&dst[9], (unsigned long long)ST.bb);
             atomicAdd((unsigned long long*)&dst[10], (unsigned long long)ST.rows);
@@ -496,397 +492,6 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
 }
 
 // ---------------------------------------------------------------------------
-// Two-phase substep pipeline.  cp_step runs each of the step's R x S
-// substeps as two launches instead of one cp_step_kernel:
-//   cp_head_kernel  (occupancy 2, every env): load, narrowphase, row setup, velocity
-//                   update, warm start and the first `head` PGS sweeps.  An env whose
-//                   two islands have converged finishes the substep here; the others
-//                   stage their solve context and are appended (wave ballot) to a list.
-//   cp_tail_kernel  (dense waves of listed envs, a register file without the
-//                   narrowphase): the remaining sweeps with fast-form island rows, then
-//                   the same finish.
-// ~70% of islands converge within 6 sweeps but ~13% run to the 50-sweep cap, and a
-// 64-lane wave pays for its slowest lane; the tail kernel packs the slow ones.  The
-// arithmetic and its order are those of substep(): bit-identical results.
-constexpr int ST_N = 0, ST_PK = 15, ST_V = 20, ST_USED = 32, ST_TOT = 33, ST_FLAGS = 34, ST_X = 35, ST_Q = 47,
-              ST_POOL = 63;
-constexpr int STAGE_FIELDS = ST_POOL + POOL_FLOATS;
-
-struct StepArgs {
-    const void* actions;
-    float* obs_out;
-    float* reward_out;
-    uint8_t* done_out;
-    float* term_out;
-    float* readback;
-    int rb_bug;
-    Lqr lq;
-    int t;     // substep of the step: r * steps_per_repeat + s
-    int head;  // sweeps run by the head kernel
-};
-
-CP_DEV void stage_out(const Soa& sg, uint32_t xo, const Ctx& c, const Sim& S, const float* pool) {
-#pragma unroll
-    for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
-        sg.st(ST_N + 3 * j + 0, xo, c.T.n[j].x);
-        sg.st(ST_N + 3 * j + 1, xo, c.T.n[j].y);
-        sg.st(ST_N + 3 * j + 2, xo, c.T.n[j].z);
-        sg.st(ST_PK + j, xo, __uint_as_float(c.T.pk[j]));
-    }
-    const V3 vv[4] = {c.I.d1.v, c.I.d1.w, c.I.d2.v, c.I.d2.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        sg.st(ST_V + 3 * k + 0, xo, vv[k].x);
-        sg.st(ST_V + 3 * k + 1, xo, vv[k].y);
-        sg.st(ST_V + 3 * k + 2, xo, vv[k].z);
-    }
-    sg.st(ST_USED, xo, __int_as_float(c.used));
-    sg.st(ST_TOT, xo, __int_as_float(c.tot));
-    sg.st(ST_FLAGS, xo, __int_as_float((c.merged ? 1 : 0) | (c.active ? 2 : 0)));
-#pragma unroll
-    for (int d = 0; d < CP_NUM_DYN; ++d) {
-        sg.st(ST_X + 3 * d + 0, xo, S.b[d].x.x);
-        sg.st(ST_X + 3 * d + 1, xo, S.b[d].x.y);
-        sg.st(ST_X + 3 * d + 2, xo, S.b[d].x.z);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) sg.st(ST_Q + 4 * d + k, xo, S.b[d].q[k]);
-    }
-#pragma unroll
-    for (int f = 0; f < POOL_FLOATS; ++f) sg.st(ST_POOL + f, xo, pool[f * WAVE]);
-}
-
-// the staged context back: poses into S, the island view rebuilt from them (same
-// arithmetic as in substep_prep), its velocities and the manifold headers restaged
-CP_DEV void stage_in(const Soa& sg, uint32_t xo, Ctx& c, Sim& S, const Lane& L, float* pool) {
-#pragma unroll
-    for (int d = 0; d < CP_NUM_DYN; ++d) {
-        S.b[d].x = mk(sg.ld(ST_X + 3 * d + 0, xo), sg.ld(ST_X + 3 * d + 1, xo), sg.ld(ST_X + 3 * d + 2, xo));
-#pragma unroll
-        for (int k = 0; k < 4; ++k) S.b[d].q[k] = sg.ld(ST_Q + 4 * d + k, xo);
-        S.b[d].v = mk(0.0f, 0.0f, 0.0f);
-        S.b[d].w = mk(0.0f, 0.0f, 0.0f);
-    }
-    S.f0 = mk(0.0f, 0.0f, 0.0f);  // consumed by this substep's velocity update
-    S.f2 = mk(0.0f, 0.0f, 0.0f);
-    island_view(S, L, c);
-    c.I.d1.v = mk(sg.ld(ST_V + 0, xo), sg.ld(ST_V + 1, xo), sg.ld(ST_V + 2, xo));
-    c.I.d1.w = mk(sg.ld(ST_V + 3, xo), sg.ld(ST_V + 4, xo), sg.ld(ST_V + 5, xo));
-    c.I.d2.v = mk(sg.ld(ST_V + 6, xo), sg.ld(ST_V + 7, xo), sg.ld(ST_V + 8, xo));
-    c.I.d2.w = mk(sg.ld(ST_V + 9, xo), sg.ld(ST_V + 10, xo), sg.ld(ST_V + 11, xo));
-#pragma unroll
-    for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
-        c.T.n[j] = mk(sg.ld(ST_N + 3 * j + 0, xo), sg.ld(ST_N + 3 * j + 1, xo), sg.ld(ST_N + 3 * j + 2, xo));
-        c.T.pk[j] = __float_as_uint(sg.ld(ST_PK + j, xo));
-    }
-    c.used = __float_as_int(sg.ld(ST_USED, xo));
-    c.tot = __float_as_int(sg.ld(ST_TOT, xo));
-    const int fl = __float_as_int(sg.ld(ST_FLAGS, xo));
-    c.merged = (fl & 1) != 0;
-    c.active = (fl & 2) != 0;
-#pragma unroll
-    for (int f = 0; f < POOL_FLOATS; ++f) pool[f * WAVE] = sg.ld(ST_POOL + f, xo);
-}
-
-// LQR forces between substep launches (lead lane writes, both lanes read)
-CP_DEV void lqr_load(const Bufs& b, int B, int i, float u[2][2], bool& out) {
-    u[0][0] = b.lqr[(size_t)0 * B + i];
-    u[0][1] = b.lqr[(size_t)1 * B + i];
-    u[1][0] = b.lqr[(size_t)2 * B + i];
-    u[1][1] = b.lqr[(size_t)3 * B + i];
-    out = b.lqr[(size_t)4 * B + i] != 0.0f;
-}
-CP_DEV void lqr_save(const Bufs& b, int B, int i, const float u[2][2], bool out) {
-    b.lqr[(size_t)0 * B + i] = u[0][0];
-    b.lqr[(size_t)1 * B + i] = u[0][1];
-    b.lqr[(size_t)2 * B + i] = u[1][0];
-    b.lqr[(size_t)3 * B + i] = u[1][1];
-    b.lqr[(size_t)4 * B + i] = out ? 1.0f : 0.0f;
-}
-
-// Everything cp_step_kernel does after substep() for substep a.t of env i: the
-// action (+ LQR) forces, readbacks, the obs row at a repeat end, and at the step's
-// last substep steps / done / reward / returns; the env state goes back to HBM.
-// Per-env inputs of post_substep, loaded before the solve so their latency overlaps it.
-struct PostIn {
-    float a00, a01, a10, a11;  // action (table entries for discrete actions)
-    int steps;                 // step counter before this step (read at the step's last substep)
-    float ret;                 // return accumulator
-};
-template <int KIND>
-CP_DEV PostIn post_inputs(const cp_config& cfg, const Bufs& b, const StepArgs& a, const Mem& G, int i) {
-    PostIn q;
-    if constexpr (KIND == CP_ACTION_CONTINUOUS) {
-        const float4 av = reinterpret_cast<const float4*>(a.actions)[i];
-        q.a00 = av.x; q.a01 = av.y; q.a10 = av.z; q.a11 = av.w;
-    } else {
-        const char2 av = reinterpret_cast<const char2*>(a.actions)[i];
-        int k0 = av.x, k1 = av.y;
-        k0 = (k0 < 0 || k0 >= CP_NUM_DISCRETE) ? 0 : k0;
-        k1 = (k1 < 0 || k1 >= CP_NUM_DISCRETE) ? 0 : k1;
-        q.a00 = kDiscrete[k0][0]; q.a01 = kDiscrete[k0][1];
-        q.a10 = kDiscrete[k1][0]; q.a11 = kDiscrete[k1][1];
-    }
-    const bool last = a.t == cfg.action_repeats * cfg.steps_per_repeat - 1;
-    q.steps = last ? ldi(G.st, CP_SF_STEPS, G.off) : 0;
-    q.ret = last ? b.ret_acc[i] : 0.0f;
-    return q;
-}
-
-// Everything cp_step_kernel does after substep() for substep a.t of env i: the
-// action (+ LQR) forces, readbacks, the obs row at a repeat end, and at the step's
-// last substep steps / done / reward / returns; the env state goes back to HBM.
-template <int KIND, bool LQR>
-CP_DEV void post_substep(Sim& S, const cp_config& cfg, const Bufs& b, const StepArgs& a, const Mem& G, int i,
-                         bool lead, const PostIn& q, float u[2][2], bool lqr_out, bool& want_reset,
-                         bool& render_me) {
-    const int B = cfg.num_envs;
-    const int R = cfg.action_repeats, SR = cfg.steps_per_repeat, T = R * SR;
-    const int r = a.t / SR, s = a.t - r * SR;
-    const float a00 = q.a00, a01 = q.a01, a10 = q.a10, a11 = q.a11;
-    const float F = cfg.action_force;
-    const float f00 = a00 * F, f01 = a01 * F, f10 = a10 * F, f11 = a11 * F;
-    if constexpr (LQR) {  // disturbance + control (:897-901), control from the pre-substep state
-        apply_force_link<0>(S, f00 + u[0][0], f01 + u[0][1]);
-        apply_force_link<1>(S, f10 + u[1][0], f11 + u[1][1]);
-        const float* K = a.lq.gains + (a.lq.per_env ? (size_t)i * 32 : 0);
-        float* s8 = (a.lq.state8 && lead) ? a.lq.state8 + (((size_t)i * R + r) * SR + s) * 16 : nullptr;
-        lqr_out |= lqr_observe(S, cfg, a.lq, K, u, s8);
-        if (lead && a.t < T - 1) lqr_save(b, B, i, u, lqr_out);
-    } else {
-        apply_force_link<0>(S, f00, f01);
-        apply_force_link<1>(S, f10, f11);
-    }
-    if (a.readback && lead) {
-        float* rb = a.readback + (size_t)i * 2 * R * SR * 12;
-        readback_pole<1, 1>(S, rb + ((size_t)(0 * R + r) * SR + s) * 12);
-        if (a.rb_bug) readback_pole<3, 1>(S, rb + ((size_t)(1 * R + r) * SR + s) * 12);
-        else readback_pole<3, 3>(S, rb + ((size_t)(1 * R + r) * SR + s) * 12);
-    }
-    float* obs = a.obs_out + (size_t)i * R * 14;
-    if (s == SR - 1 && lead) {
-        float row[14];
-        write_obs_row(S, row);
-#pragma unroll
-        for (int f = 0; f < 14; ++f) obs[r * 14 + f] = row[f];
-        if (b.rposes) write_rposes(S, b.rposes + ((size_t)i * R + r) * CP_NUM_DYN * 7);
-    }
-    if (a.t < T - 1) {
-        if (lead) store_sim(S, G.st, G.off);
-        return;
-    }
-    render_me = lead && b.rposes != nullptr;
-    const int steps = q.steps + 1;
-    bool done = steps >= cfg.max_episode_len;
-    if (cfg.done_on_bounds && bounds_exceeded(S, cfg)) done = true;
-    if (LQR && lqr_out) done = true;
-    if (!lead) return;
-    store_sim(S, G.st, G.off);
-    sti(G.st, CP_SF_STEPS, G.off, steps);
-    a.reward_out[i] = 1.0f;  // bullet_cartpole.py:260
-    a.done_out[i] = done ? 1 : 0;
-    const Soa term = Soa::make(b.term_obs, B, R * 14);
-    const float ret = q.ret + 1.0f;
-    if (done) {
-        b.last_ret[i] = ret;
-        b.last_len[i] = steps;
-        b.ret_acc[i] = 0.0f;
-        for (int f = 0; f < R * 14; ++f) term.st(f, G.off, obs[f]);
-        if (a.term_out)
-            for (int f = 0; f < R * 14; ++f) a.term_out[(size_t)i * R * 14 + f] = obs[f];
-        sti(G.st, CP_SF_DONE, G.off, 1);
-        want_reset = cfg.autoreset != 0;
-    } else {
-        b.ret_acc[i] = ret;
-    }
-}
-
-// wave ballot compaction of the step's finishing envs into the reset / render lists
-CP_DEV void append_lists(const cp_config& cfg, const Bufs& b, int i, bool want_reset, bool render_me) {
-    const int lane = threadIdx.x & (WAVE - 1);
-    if (cfg.autoreset) {
-        const uint64_t bal = __ballot(want_reset);
-        const int n = __popcll(bal);
-        int base = 0;
-        if (lane == 0 && n) base = atomicAdd(b.count, n);
-        base = __shfl(base, 0);
-        if (want_reset) b.list[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
-    }
-    if (b.rposes) {
-        const uint64_t bal = __ballot(render_me);
-        const int n = __popcll(bal);
-        int base = 0;
-        if (lane == 0 && n) base = atomicAdd(b.rcount, n);
-        base = __shfl(base, 0);
-        if (render_me) b.rlist[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
-    }
-}
-
-template <int KIND, bool LQR>
-__global__ void CP_PHYS_ATTR cp_head_kernel(cp_config cfg, Bufs b, StepArgs a) {
-    __shared__ float lds_pool[POOL_FLOATS * WAVE];
-    const int B = cfg.num_envs;
-    const int tl = blockIdx.x * WAVE + threadIdx.x;
-    const int i = tl >> 1, isl = tl & 1;
-    const bool lead = isl == 0;
-    const int R = cfg.action_repeats, SR = cfg.steps_per_repeat, T = R * SR;
-    float* pool = lds_pool + threadIdx.x;
-    float* pool0 = lds_pool + (threadIdx.x & ~1u);
-    bool want_reset = false, render_me = false, tail = false;
-    int cls = 0;
-    Stamps ST;
-    CP_STAMP(k0);
-    Sim S;
-    Ctx c;
-    float u[2][2] = {{0.0f, 0.0f}, {0.0f, 0.0f}};
-    bool lqr_out = false;
-    if (i < B) {
-        const Mem G = Mem::make(b.state, b.scratch, B, i, isl);
-        bool run;
-        if (a.t == 0) {
-            const bool was_done = ldi(G.st, CP_SF_DONE, G.off) != 0;
-            if (lead) b.stepped[i] = was_done ? 0 : 1;
-            run = !was_done;
-            if (was_done && lead) {  // step after done (bullet_cartpole.py:179-181)
-                const Soa term = Soa::make(b.term_obs, B, R * 14);
-                float* obs = a.obs_out + (size_t)i * R * 14;
-                for (int f = 0; f < R * 14; ++f) obs[f] = term.ld(f, G.off);
-                a.reward_out[i] = 0.0f;
-                a.done_out[i] = 1;
-            }
-        } else {
-            run = b.stepped[i] != 0;
-        }
-        if (run) {
-            const Lane L = Lane::make(isl, cfg.phys);
-            load_sim(S, G.st, G.off);
-            const PostIn q = post_inputs<KIND>(cfg, b, a, G, i);
-            if constexpr (LQR) {
-                if (a.t == 0) {  // control from the pre-step state
-                    const float* K = a.lq.gains + (a.lq.per_env ? (size_t)i * 32 : 0);
-                    lqr_observe(S, cfg, a.lq, K, u, nullptr);
-                } else {
-                    lqr_load(b, B, i, u, lqr_out);
-                }
-            }
-            int ov = 0;
-            substep_prep(S, cfg.phys, L, pool, pool0, ov, G, ST, true, c);
-            CP_STAMP(s2);
-            sweeps(c, S, cfg.phys, pool, pool0, isl != 0, 0, min(a.head, cfg.phys.solver_iterations), ST);
-            CP_STAMP(s3);
-            CP_ACC(solve, s2, s3);
-            ov += (int)partner_u((uint32_t)ov);
-            if (ov && lead) b.overflow[i] += ov;
-            // either island unconverged (the DPP read stays outside any short-circuit: both
-            // lanes of the pair must execute it)
-            const uint32_t pact = partner_u(c.active ? 1u : 0u);
-            tail = c.active || pact != 0u;
-            cls = tail_class(c);
-            if (!tail) {
-                substep_finish(S, cfg.phys, L, c, pool, G, ST, true);
-                post_substep<KIND, LQR>(S, cfg, b, a, G, i, lead, q, u, lqr_out, want_reset, render_me);
-            }
-        }
-    }
-#ifdef CP_STAMPS
-    CP_STAMP(k1);
-    flush_stamps(ST, b.stamps, k1 - k0);
-#endif
-    int pos = 0;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {  // tail envs per class, in pairs of lanes: one list entry per env (lead lane)
-        const bool put = tail && lead && cls == k;
-        const uint64_t bal = __ballot(put);
-        const int lane = threadIdx.x & (WAVE - 1);
-        const int n = __popcll(bal);
-        int base = 0;
-        if (lane == 0 && n) base = atomicAdd(b.scount + 3 * a.t + k, n);
-        base = __shfl(base, 0);
-        if (put) {
-            pos = base + __popcll(bal & ((1ull << lane) - 1ull));
-            b.slist[(size_t)k * B + pos] = i;
-        }
-    }
-    pos = __shfl(pos, threadIdx.x & ~1u);  // the pair's list position (lead lane)
-    if (tail) {  // the solve context, at the env's list position (coalesced for the tail kernel)
-        const Soa sg = Soa::make(b.stage, 6 * B, STAGE_FIELDS);
-        stage_out(sg, (uint32_t)(cls * 2 * B + 2 * pos + isl) * 4u, c, S, pool);
-        if (LQR && lead && a.t == 0) lqr_save(b, B, i, u, lqr_out);
-    }
-    if (a.t == T - 1) append_lists(cfg, b, i, want_reset, render_me);
-}
-
-#ifndef CP_TAIL_WAVES_PER_EU
-#define CP_TAIL_WAVES_PER_EU 1
-#endif
-template <int KIND, bool LQR>
-__global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(CP_TAIL_WAVES_PER_EU, CP_TAIL_WAVES_PER_EU)))
-cp_tail_kernel(cp_config cfg, Bufs b, StepArgs a) {
-    __shared__ float lds_pool[POOL_FLOATS * WAVE];
-    const int B = cfg.num_envs;
-    const int T = cfg.action_repeats * cfg.steps_per_repeat;
-    constexpr int PAIRS = WAVE / 2;  // envs per wave
-    // block -> (class, first env of the class list): class 0 blocks, then 1, then 2
-    const int n0 = b.scount[3 * a.t], n1 = b.scount[3 * a.t + 1], n2 = b.scount[3 * a.t + 2];
-    const int w0 = (n0 + PAIRS - 1) / PAIRS, w1 = (n1 + PAIRS - 1) / PAIRS, w2 = (n2 + PAIRS - 1) / PAIRS;
-    int blk = blockIdx.x, cls, n;
-    if (blk < w0) { cls = 0; n = n0; }
-    else if (blk < w0 + w1) { cls = 1; n = n1; blk -= w0; }
-    else if (blk < w0 + w1 + w2) { cls = 2; n = n2; blk -= w0 + w1; }
-    else return;  // whole wave past the lists
-    const int p = blk * PAIRS + (threadIdx.x >> 1), isl = threadIdx.x & 1;
-    const bool lead = isl == 0;
-    float* pool = lds_pool + threadIdx.x;
-    float* pool0 = lds_pool + (threadIdx.x & ~1u);
-    bool want_reset = false, render_me = false;
-    int i = 0;
-    Stamps ST;
-    CP_STAMP(k0);
-    if (p < n) {
-        i = b.slist[(size_t)cls * B + p];
-        const Mem G = Mem::make(b.state, b.scratch, B, i, isl);
-        const Lane L = Lane::make(isl, cfg.phys);
-        const Soa sg = Soa::make(b.stage, 6 * B, STAGE_FIELDS);
-        Sim S;
-        Ctx c;
-        CP_STAMP(s0);
-        const PostIn q = post_inputs<KIND>(cfg, b, a, G, i);
-        stage_in(sg, (uint32_t)(cls * 2 * B + 2 * p + isl) * 4u, c, S, L, pool);
-        float u[2][2] = {{0.0f, 0.0f}, {0.0f, 0.0f}};
-        bool lqr_out = false;
-        if constexpr (LQR) lqr_load(b, B, i, u, lqr_out);
-        CP_STAMP(s2);
-        CP_ACC(narrow, s0, s2);  // tail: stage-in time in the narrowphase slot
-        const int it0 = min(a.head, cfg.phys.solver_iterations), it1 = cfg.phys.solver_iterations;
-        if (cls == 2) {
-            solve_range<true>(c, S, cfg.phys, pool, pool0, isl != 0, it0, it1, ST);
-        } else {
-            FastIsl F;
-            if (cls == 0) {
-                fast_build_cls<0>(F, c, pool);
-                sweeps_cls<0>(c, F, cfg.phys, isl != 0, it0, it1, ST);
-                fast_store_cls<0>(F, c, pool);
-            } else {
-                fast_build_cls<1>(F, c, pool);
-                sweeps_cls<1>(c, F, cfg.phys, isl != 0, it0, it1, ST);
-                fast_store_cls<1>(F, c, pool);
-            }
-        }
-        CP_STAMP(s3);
-        CP_ACC(solve, s2, s3);
-        substep_finish(S, cfg.phys, L, c, pool, G, ST, true);
-        CP_STAMP(s4);
-        post_substep<KIND, LQR>(S, cfg, b, a, G, i, lead, q, u, lqr_out, want_reset, render_me);
-        CP_STAMP(s5);
-        CP_ACC(vel, s4, s5);  // tail: post-substep time in the velocity slot
-    }
-#ifdef CP_STAMPS
-    CP_STAMP(k1);
-    flush_stamps(ST, b.stamps + 8, k1 - k0);
-#endif
-    if (a.t == T - 1) append_lists(cfg, b, i, want_reset, render_me);
-}
-
-// ---------------------------------------------------------------------------
 // Event log records (protobuf wire format of event.proto; see cp_encode_events).
 CP_DEV void put_u8(uint8_t*& p, uint32_t v) { *p++ = (uint8_t)v; }
 CP_DEV void put_varint(uint8_t*& p, uint32_t v) {
@@ -987,10 +592,8 @@ struct cp_handle {
     cp_timing timing;
     cp_raster_config raster;
     uint16_t* pixels;  // raster obs output (NULL: raster off)
-    int mono;          // 1: one fused cp_step_kernel per step (default), 0: head/tail pipeline (CP_PIPELINE=1)
     int32_t* count2;   // [2] reset-list counters, alternating by call: each reset launch zeroes the other one
     int par;           // counter the next call appends to
-    int head;          // PGS sweeps of the head kernel (CP_HEAD_SWEEPS, default 6)
     int reset_lat;     // 1: latency-shaped autoreset kernel (episodes end at different steps)
     int step_lat;      // 1: latency-shaped step kernel (every wave gets a SIMD of its own)
     std::string err;
@@ -1117,13 +720,6 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     h->readback_bug = 1;
     h->lqr = cp::Lqr{nullptr, 0, nullptr, 0.0f, 0.0f};
     h->pixels = nullptr;
-    {
-        const char* m = std::getenv("CP_PIPELINE");
-        h->mono = (m && m[0] == '1') ? 0 : 1;
-        const char* hs = std::getenv("CP_HEAD_SWEEPS");
-        h->head = hs ? std::atoi(hs) : 6;
-        if (h->head < 0) h->head = 0;
-    }
     choose_reset_shape(h);
     cp_default_raster_config(&h->raster);
     std::memset(&h->b, 0, sizeof(h->b));
@@ -1151,16 +747,6 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     CP_ALLOC(h->b.scratch, (size_t)4 * CP_ISLAND_PAIRS * 2 * B * sizeof(float));
     CP_ALLOC(h->b.stamps, 16 * sizeof(uint64_t));
     CP_ALLOC(h->b.stepped, B * sizeof(uint8_t));
-    if (!h->mono) {  // pipeline mode only
-        if ((unsigned long long)cp::STAGE_FIELDS * 6ull * B * 4ull >= (1ull << 32)) {
-            cp_destroy(h);
-            return fail(nullptr, "cp_create: num_envs too large for the pipeline's staging array (4 GiB)");
-        }
-        CP_ALLOC(h->b.stage, (size_t)cp::STAGE_FIELDS * 6 * B * sizeof(float));
-    }
-    CP_ALLOC(h->b.slist, 3 * B * sizeof(int32_t));
-    CP_ALLOC(h->b.scount, (size_t)3 * R * cfg->steps_per_repeat * sizeof(int32_t));
-    CP_ALLOC(h->b.lqr, 5 * B * sizeof(float));
 #undef CP_ALLOC
     e = hipMemset(h->count2, 0, 2 * sizeof(int32_t));
     if (e != hipSuccess) return fail_free(e, "hipMemset");
@@ -1199,10 +785,6 @@ void cp_destroy(cp_handle* h) {
     (void)hipFree(h->b.scratch);
     (void)hipFree(h->b.stamps);
     (void)hipFree(h->b.stepped);
-    (void)hipFree(h->b.stage);
-    (void)hipFree(h->b.slist);
-    (void)hipFree(h->b.scount);
-    (void)hipFree(h->b.lqr);
     (void)hipFree(h->b.rposes);
     (void)hipFree(h->b.rlist);
     (void)hipFree(h->b.rcount);
@@ -1299,7 +881,6 @@ int cp_step(cp_handle* h, const void* actions, int action_kind, float* obs_out, 
     hipEvent_t* ev = timing_slot(h, 0);
     if (ev) CP_TRY(h, hipEventRecord(ev[0], st));
     const bool lqr = h->lqr.gains != nullptr;
-    if (h->mono) {
 #define CP_LAUNCH_STEP(K, Q)                                                                                    \
     do {                                                                                                        \
         if (h->step_lat)                                                                                        \
@@ -1311,38 +892,14 @@ int cp_step(cp_handle* h, const void* actions, int action_kind, float* obs_out, 
                                obs_out, reward_out, done_out, terminal_obs_out, h->readback, h->readback_bug,    \
                                h->lqr);                                                                         \
     } while (0)
-        if (action_kind == CP_ACTION_CONTINUOUS) {
-            if (lqr) CP_LAUNCH_STEP(CP_ACTION_CONTINUOUS, true);
-            else CP_LAUNCH_STEP(CP_ACTION_CONTINUOUS, false);
-        } else {
-            if (lqr) CP_LAUNCH_STEP(CP_ACTION_DISCRETE, true);
-            else CP_LAUNCH_STEP(CP_ACTION_DISCRETE, false);
-        }
-#undef CP_LAUNCH_STEP
+    if (action_kind == CP_ACTION_CONTINUOUS) {
+        if (lqr) CP_LAUNCH_STEP(CP_ACTION_CONTINUOUS, true);
+        else CP_LAUNCH_STEP(CP_ACTION_CONTINUOUS, false);
     } else {
-        const int T = h->cfg.action_repeats * h->cfg.steps_per_repeat;
-        CP_TRY(h, hipMemsetAsync(h->b.scount, 0, (size_t)3 * T * sizeof(int32_t), st));
-        cp::StepArgs a{actions, obs_out, reward_out, done_out, terminal_obs_out, h->readback, h->readback_bug,
-                       h->lqr, 0, h->head};
-        const dim3 tgrid(grid.x + 3);  // the three class lists each may end in a partial wave
-        for (int t = 0; t < T; ++t) {
-            a.t = t;
-#define CP_LAUNCH_PAIR(K, Q)                                                                        \
-    do {                                                                                            \
-        hipLaunchKernelGGL((cp::cp_head_kernel<K, Q>), grid, block, 0, st, h->cfg, h->b, a);        \
-        hipLaunchKernelGGL((cp::cp_tail_kernel<K, Q>), tgrid, block, 0, st, h->cfg, h->b, a);       \
-    } while (0)
-            if (action_kind == CP_ACTION_CONTINUOUS) {
-                if (lqr) CP_LAUNCH_PAIR(CP_ACTION_CONTINUOUS, true);
-                else CP_LAUNCH_PAIR(CP_ACTION_CONTINUOUS, false);
-            } else {
-                if (lqr) CP_LAUNCH_PAIR(CP_ACTION_DISCRETE, true);
-                else CP_LAUNCH_PAIR(CP_ACTION_DISCRETE, false);
-            }
-#undef CP_LAUNCH_PAIR
-            CP_TRY(h, hipGetLastError());
-        }
+        if (lqr) CP_LAUNCH_STEP(CP_ACTION_DISCRETE, true);
+        else CP_LAUNCH_STEP(CP_ACTION_DISCRETE, false);
     }
+#undef CP_LAUNCH_STEP
     CP_TRY(h, hipGetLastError());
     if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
     // autoreset envs were simulated this step, so they are in the render list; the reset

@@ -527,7 +527,7 @@ CP_DEV void isl_impulse(Isl& I, V3 rb, V3 t, float lam) {
 }
 
 template <int A, int B, bool FRICTION>
-CP_DEV float isl_row(Isl& I, V3 rb, V3 t, float inv_eff, float target, float& lam, float bound) {
+CP_DEV bool isl_row(Isl& I, V3 rb, V3 t, float inv_eff, float target, float& lam, float bound, float tol) {
     Dyn& b = dyn<B>(I);
     const float imb = dyn_im<B>(I);
     V3 rbt = cross(rb, t);
@@ -548,7 +548,7 @@ CP_DEV float isl_row(Isl& I, V3 rb, V3 t, float inv_eff, float target, float& la
     float l0 = lam + dl;
     float ln;
     if constexpr (!FRICTION) ln = l0 > 0.0f ? l0 : 0.0f;
-    else ln = __builtin_amdgcn_fmed3f(l0, -bound, bound);  // = the oracle's clamp (see isl_row_ez)
+    else ln = bound > 0.0f ? __builtin_amdgcn_fmed3f(l0, -bound, bound) : lam;  // see isl_row_ez
     dl = ln - lam;
     lam = ln;
     float sb = dl * imb;
@@ -560,7 +560,7 @@ CP_DEV float isl_row(Isl& I, V3 rb, V3 t, float inv_eff, float target, float& la
         a.v = madd(a.v, neg(t), sa);
         a.w = madd(a.w, neg(ia), dl);
     }
-    return fabsf(e * dl);
+    return fabsf(dl) > tol * inv_eff;  // Bullet residual test (oracle: solve_row)
 }
 
 // isl_row<0, B> for a ground manifold whose normal is exactly +z (the static ground's top
@@ -571,7 +571,7 @@ CP_DEV float isl_row(Isl& I, V3 rb, V3 t, float inv_eff, float target, float& la
 // exact zero result can differ).  KIND 0: t = n, 1: t = t1, 2: t = t2.  Same values as
 // isl_row, about 60 % of its VALU work (no r x t, 6 of the 9 products of M (r x t)).
 template <int B, int KIND, bool FRICTION>
-CP_DEV float isl_row_ez(Isl& I, V3 rb, float inv_eff, float target, float& lam, float bound) {
+CP_DEV bool isl_row_ez(Isl& I, V3 rb, float inv_eff, float target, float& lam, float bound, float tol) {
     Dyn& b = dyn<B>(I);
     const float imb = dyn_im<B>(I);
     const Sym& M = b.M;
@@ -594,14 +594,12 @@ CP_DEV float isl_row_ez(Isl& I, V3 rb, float inv_eff, float target, float& lam, 
     float dl = e * inv_eff;
     float l0 = lam + dl;
     float ln;
+    // friction rows: Bullet skips the row while the normal impulse is not > 0 (lambda stays,
+    // dl = 0, no residual); else the clamp as one v_med3_f32 (bound > 0): the same value as
+    // the oracle's compare chain for every non-NaN l0, one dependent instruction instead of
+    // three
     if constexpr (!FRICTION) ln = l0 > 0.0f ? l0 : 0.0f;
-#ifdef CP_NO_MED3
-    else ln = l0 > bound ? bound : (l0 < -bound ? -bound : l0);
-#else
-    // the friction clamp as one v_med3_f32 (bound >= 0): the same value as the oracle's
-    // compare chain for every non-NaN l0, one dependent instruction instead of three
-    else ln = __builtin_amdgcn_fmed3f(l0, -bound, bound);
-#endif
+    else ln = bound > 0.0f ? __builtin_amdgcn_fmed3f(l0, -bound, bound) : lam;
     dl = ln - lam;
     lam = ln;
     float sb = dl * imb;
@@ -609,7 +607,7 @@ CP_DEV float isl_row_ez(Isl& I, V3 rb, float inv_eff, float target, float& lam, 
     else if constexpr (KIND == 1) b.v.y = b.v.y - sb;
     else b.v.x = b.v.x + sb;
     b.w = madd(b.w, ib, dl);
-    return fabsf(e * dl);
+    return fabsf(dl) > tol * inv_eff;  // Bullet residual test (oracle: solve_row)
 }
 CP_DEV bool is_plus_z(V3 n) { return n.x == 0.0f && n.y == 0.0f && n.z == 1.0f; }
 
@@ -629,22 +627,21 @@ CP_DEV void isl_warmstart(Isl& I, const Step& T, float* pool) {
 }
 
 template <int J>
-CP_DEV void isl_normal_rows(Isl& I, const Step& T, float* pool, float& resid) {
+CP_DEV void isl_normal_rows(Isl& I, const Step& T, float* pool, float tol, bool& bad) {
     const uint32_t pk = T.pk[J];
     const int cnt = pk_cnt(pk), base = pk_base(pk);
     for (int k = 0; k < cnt; ++k) {
         const int s = base + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
         float lam = pool_n(pool, F_LAM, s);
-        float r = isl_row<loc_a<J>(), loc_b<J>(), false>(I, rb, T.n[J], pool_n(pool, F_IE, s),
-                                                         pool_n(pool, F_TG, s), lam, 0.0f);
+        bad |= isl_row<loc_a<J>(), loc_b<J>(), false>(I, rb, T.n[J], pool_n(pool, F_IE, s),
+                                                      pool_n(pool, F_TG, s), lam, 0.0f, tol);
         pool_n(pool, F_LAM, s) = lam;
-        resid = resid + r;
     }
 }
 
 template <int J, bool HOISTED = false>
-CP_DEV void isl_friction_rows(Isl& I, const Step& T, float mu, float* pool, float& resid, V3 ht1 = V3{},
+CP_DEV void isl_friction_rows(Isl& I, const Step& T, float mu, float* pool, float tol, bool& bad, V3 ht1 = V3{},
                               V3 ht2 = V3{}) {
     const uint32_t pk = T.pk[J];
     const int fcnt = pk_fcnt(pk);
@@ -665,10 +662,8 @@ CP_DEV void isl_friction_rows(Isl& I, const Step& T, float mu, float* pool, floa
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
         float bound = mu * pool_n(pool, F_LAM, s);
         float l1 = pool_f(pool, FF_L1, fs), l2 = pool_f(pool, FF_L2, fs);
-        float r1 = isl_row<loc_a<J>(), loc_b<J>(), true>(I, rb, t1, pool_f(pool, FF_IE1, fs), 0.0f, l1, bound);
-        resid = resid + r1;
-        float r2 = isl_row<loc_a<J>(), loc_b<J>(), true>(I, rb, t2, pool_f(pool, FF_IE2, fs), 0.0f, l2, bound);
-        resid = resid + r2;
+        bad |= isl_row<loc_a<J>(), loc_b<J>(), true>(I, rb, t1, pool_f(pool, FF_IE1, fs), 0.0f, l1, bound, tol);
+        bad |= isl_row<loc_a<J>(), loc_b<J>(), true>(I, rb, t2, pool_f(pool, FF_IE2, fs), 0.0f, l2, bound, tol);
         pool_f(pool, FF_L1, fs) = l1;
         pool_f(pool, FF_L2, fs) = l2;
     }
@@ -680,7 +675,7 @@ CP_DEV void isl_friction_rows(Isl& I, const Step& T, float mu, float* pool, floa
 // The rows of ground pair J (0 or 1) when every lane of the wave with rows on it has a +z
 // normal (wave-uniform choice in sweeps()): the same sweep with isl_row_ez.
 template <int J>
-CP_DEV void isl_normal_rows_ez(Isl& I, const Step& T, float* pool, float& resid) {
+CP_DEV void isl_normal_rows_ez(Isl& I, const Step& T, float* pool, float tol, bool& bad) {
     static_assert(loc_a<J>() == 0, "ground pairs only");
     const uint32_t pk = T.pk[J];
     const int cnt = pk_cnt(pk), base = pk_base(pk);
@@ -688,13 +683,12 @@ CP_DEV void isl_normal_rows_ez(Isl& I, const Step& T, float* pool, float& resid)
         const int s = base + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
         float lam = pool_n(pool, F_LAM, s);
-        float r = isl_row_ez<loc_b<J>(), 0, false>(I, rb, pool_n(pool, F_IE, s), pool_n(pool, F_TG, s), lam, 0.0f);
+        bad |= isl_row_ez<loc_b<J>(), 0, false>(I, rb, pool_n(pool, F_IE, s), pool_n(pool, F_TG, s), lam, 0.0f, tol);
         pool_n(pool, F_LAM, s) = lam;
-        resid = resid + r;
     }
 }
 template <int J>
-CP_DEV void isl_friction_rows_ez(Isl& I, const Step& T, float mu, float* pool, float& resid) {
+CP_DEV void isl_friction_rows_ez(Isl& I, const Step& T, float mu, float* pool, float tol, bool& bad) {
     static_assert(loc_a<J>() == 0, "ground pairs only");
     const uint32_t pk = T.pk[J];
     const int fcnt = pk_fcnt(pk);
@@ -705,10 +699,8 @@ CP_DEV void isl_friction_rows_ez(Isl& I, const Step& T, float mu, float* pool, f
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
         float bound = mu * pool_n(pool, F_LAM, s);
         float l1 = pool_f(pool, FF_L1, fs), l2 = pool_f(pool, FF_L2, fs);
-        float r1 = isl_row_ez<loc_b<J>(), 1, true>(I, rb, pool_f(pool, FF_IE1, fs), 0.0f, l1, bound);
-        resid = resid + r1;
-        float r2 = isl_row_ez<loc_b<J>(), 2, true>(I, rb, pool_f(pool, FF_IE2, fs), 0.0f, l2, bound);
-        resid = resid + r2;
+        bad |= isl_row_ez<loc_b<J>(), 1, true>(I, rb, pool_f(pool, FF_IE1, fs), 0.0f, l1, bound, tol);
+        bad |= isl_row_ez<loc_b<J>(), 2, true>(I, rb, pool_f(pool, FF_IE2, fs), 0.0f, l2, bound, tol);
         pool_f(pool, FF_L1, fs) = l1;
         pool_f(pool, FF_L2, fs) = l2;
     }
@@ -753,8 +745,8 @@ CP_DEV void apply_impulse(Sim& S, const Step& T, const cp_physics& P, V3 rb, V3 
 
 // One PGS row (oracle: solve_row).  Returns |e * dlambda|.
 template <int A, int B, bool FRICTION>
-CP_DEV float solve_row(Sim& S, const Step& T, const cp_physics& P, V3 rb, V3 t, float inv_eff, float target,
-                       float& lam, float bound) {
+CP_DEV bool solve_row(Sim& S, const Step& T, const cp_physics& P, V3 rb, V3 t, float inv_eff, float target,
+                      float& lam, float bound, float tol) {
     float imb = P.inv_mass[B];
     V3 rbt = cross(rb, t);
     V3 ib = symv(T.M[B - 1], rbt);
@@ -773,7 +765,7 @@ CP_DEV float solve_row(Sim& S, const Step& T, const cp_physics& P, V3 rb, V3 t, 
     float l0 = lam + dl;
     float ln;
     if constexpr (!FRICTION) ln = l0 > 0.0f ? l0 : 0.0f;
-    else ln = __builtin_amdgcn_fmed3f(l0, -bound, bound);  // = the oracle's clamp (see isl_row_ez)
+    else ln = bound > 0.0f ? __builtin_amdgcn_fmed3f(l0, -bound, bound) : lam;  // see isl_row_ez
     dl = ln - lam;
     lam = ln;
     float sb = dl * imb;
@@ -784,7 +776,7 @@ CP_DEV float solve_row(Sim& S, const Step& T, const cp_physics& P, V3 rb, V3 t, 
         S.b[A - 1].v = madd(S.b[A - 1].v, neg(t), sa);
         S.b[A - 1].w = madd(S.b[A - 1].w, neg(ia), dl);
     }
-    return fabsf(e * dl);
+    return fabsf(dl) > tol * inv_eff;  // Bullet residual test (oracle: solve_row)
 }
 
 template <int PAIR>
@@ -803,7 +795,7 @@ CP_DEV void pair_warmstart(Sim& S, const Step& T, bool second, const cp_physics&
 
 template <int PAIR>
 CP_DEV void pair_normal_rows(Sim& S, const Step& T, bool second, const cp_physics& P, float* pool0,
-                             float& resid) {
+                             float tol, bool& bad) {
     constexpr int A = pair_a(PAIR), B = pair_b(PAIR);
     float* pool = pool0 + island_of(PAIR);
     const Hdr H = pair_hdr<PAIR>(T, second);
@@ -813,16 +805,15 @@ CP_DEV void pair_normal_rows(Sim& S, const Step& T, bool second, const cp_physic
         const int s = base + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
         float lam = pool_n(pool, F_LAM, s);
-        float r = solve_row<A, B, false>(S, T, P, rb, H.n, pool_n(pool, F_IE, s), pool_n(pool, F_TG, s),
-                                         lam, 0.0f);
+        bad |= solve_row<A, B, false>(S, T, P, rb, H.n, pool_n(pool, F_IE, s), pool_n(pool, F_TG, s),
+                                      lam, 0.0f, tol);
         pool_n(pool, F_LAM, s) = lam;
-        resid = resid + r;
     }
 }
 
 template <int PAIR>
 CP_DEV void pair_friction_rows(Sim& S, const Step& T, bool second, const cp_physics& P, float* pool0,
-                               float& resid) {
+                               float tol, bool& bad) {
     constexpr int A = pair_a(PAIR), B = pair_b(PAIR);
     float* pool = pool0 + island_of(PAIR);
     const Hdr H = pair_hdr<PAIR>(T, second);
@@ -840,10 +831,8 @@ CP_DEV void pair_friction_rows(Sim& S, const Step& T, bool second, const cp_phys
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
         float bound = mu * pool_n(pool, F_LAM, s);
         float l1 = pool_f(pool, FF_L1, fs), l2 = pool_f(pool, FF_L2, fs);
-        float r1 = solve_row<A, B, true>(S, T, P, rb, t1, pool_f(pool, FF_IE1, fs), 0.0f, l1, bound);
-        resid = resid + r1;
-        float r2 = solve_row<A, B, true>(S, T, P, rb, t2, pool_f(pool, FF_IE2, fs), 0.0f, l2, bound);
-        resid = resid + r2;
+        bad |= solve_row<A, B, true>(S, T, P, rb, t1, pool_f(pool, FF_IE1, fs), 0.0f, l1, bound, tol);
+        bad |= solve_row<A, B, true>(S, T, P, rb, t2, pool_f(pool, FF_IE2, fs), 0.0f, l2, bound, tol);
         pool_f(pool, FF_L1, fs) = l1;
         pool_f(pool, FF_L2, fs) = l2;
     }
@@ -946,7 +935,7 @@ CP_DEV void cross_view(Sim& S, Step& T, const Isl& I, bool second) {
     const V3 v1 = partner(I.d1.v), w1 = partner(I.d1.w), v2 = partner(I.d2.v), w2 = partner(I.d2.w);
     const V3 x1 = partner(I.d1.x), x2 = partner(I.d2.x);
     const Sym M1 = partner_sym(I.d1.M), M2 = partner_sym(I.d2.M);
-    S.b[0].x = selv(second, x1, I.d1.x);  // (a lane that adopted the env has no S of its own)
+    S.b[0].x = selv(second, x1, I.d1.x);
     S.b[1].x = selv(second, x2, I.d2.x);
     S.b[2].x = selv(second, I.d1.x, x1);
     S.b[3].x = selv(second, I.d2.x, x2);
@@ -970,10 +959,8 @@ CP_DEV void cross_back(Isl& I, const Sim& S, bool second) {
     I.d2.w = selv(second, S.b[3].w, S.b[1].w);
 }
 
-// Per-lane solve state of one substep, between its phases (prep -> sweeps ->
-// [migration] -> finish).  Everything a lane needs to continue its island's PGS
-// sweeps lives in here (plus its LDS pool column), so another lane of the
-// workgroup can adopt it (cp_kernels.hip: straggler migration).
+// Per-lane solve state of one substep, between its phases (prep -> sweeps -> finish):
+// everything a lane needs to run its island's PGS sweeps, plus its LDS pool column.
 struct Ctx {
     Step T;          // own island's manifold headers (+ whole-env M for the cross rows)
     Isl I;           // own island's bodies
@@ -984,10 +971,12 @@ struct Ctx {
 
 // One PGS sweep range [it0, it1) over the lane's island (+ the cross rows of a merged
 // env).  S supplies positions for the cross rows and is scratch for their whole-env
-// view.  Lanes stop after the sweep whose residual is <= the threshold.
+// view.  Both lanes of an env stop together, after the first sweep in which no row of
+// the env (island 0, island 1, cross) has a squared residual above the threshold:
+// Bullet solves the two islands as one group (oracle: substep, step 4).
 CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, float* pool, float* pool0, bool second, int it0, int it1,
                    Stamps& ST) {
-    const float thr = P.residual_threshold;
+    const float tol = sqrtf(P.residual_threshold);
     // the ground-pole pair's tangent basis (with the URDF frictions the only island pair with
     // friction rows: the carts' friction is 0), once per substep instead of once per sweep:
     // step kernel 0.772 -> 0.753 ms
@@ -1006,41 +995,41 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, float* pool, float* pool
 #ifdef CP_STAMPS
         ST.sweeps += 1;
 #endif
-        float r = 0.0f, rc = 0.0f;
+        bool bad = false, badc = false;
         if (c.active) {
-            if (ez0) isl_normal_rows_ez<0>(c.I, c.T, pool, r);
-            else isl_normal_rows<0>(c.I, c.T, pool, r);
-            if (ez1) isl_normal_rows_ez<1>(c.I, c.T, pool, r);
-            else isl_normal_rows<1>(c.I, c.T, pool, r);
-            isl_normal_rows<2>(c.I, c.T, pool, r);
+            if (ez0) isl_normal_rows_ez<0>(c.I, c.T, pool, tol, bad);
+            else isl_normal_rows<0>(c.I, c.T, pool, tol, bad);
+            if (ez1) isl_normal_rows_ez<1>(c.I, c.T, pool, tol, bad);
+            else isl_normal_rows<1>(c.I, c.T, pool, tol, bad);
+            isl_normal_rows<2>(c.I, c.T, pool, tol, bad);
         }
         const bool cross = c.active && c.merged;  // same on both lanes of an env
         if (__ballot(cross) != 0ull && cross) {
             cross_view(S, c.T, c.I, second);
-            pair_normal_rows<5>(S, c.T, second, P, pool0, rc);
-            pair_normal_rows<6>(S, c.T, second, P, pool0, rc);
-            pair_normal_rows<7>(S, c.T, second, P, pool0, rc);
-            pair_normal_rows<8>(S, c.T, second, P, pool0, rc);
+            pair_normal_rows<5>(S, c.T, second, P, pool0, tol, badc);
+            pair_normal_rows<6>(S, c.T, second, P, pool0, tol, badc);
+            pair_normal_rows<7>(S, c.T, second, P, pool0, tol, badc);
+            pair_normal_rows<8>(S, c.T, second, P, pool0, tol, badc);
             cross_back(c.I, S, second);
         }
         if (c.active) {
-            if (ez0) isl_friction_rows_ez<0>(c.I, c.T, c.mu0, pool, r);
-            else isl_friction_rows<0>(c.I, c.T, c.mu0, pool, r);
-            if (ez1) isl_friction_rows_ez<1>(c.I, c.T, c.mu1, pool, r);
-            else isl_friction_rows<1, true>(c.I, c.T, c.mu1, pool, r, h1, h2);
-            isl_friction_rows<2>(c.I, c.T, c.mu2, pool, r);
+            if (ez0) isl_friction_rows_ez<0>(c.I, c.T, c.mu0, pool, tol, bad);
+            else isl_friction_rows<0>(c.I, c.T, c.mu0, pool, tol, bad);
+            if (ez1) isl_friction_rows_ez<1>(c.I, c.T, c.mu1, pool, tol, bad);
+            else isl_friction_rows<1, true>(c.I, c.T, c.mu1, pool, tol, bad, h1, h2);
+            isl_friction_rows<2>(c.I, c.T, c.mu2, pool, tol, bad);
         }
         if (__ballot(cross) != 0ull && cross) {
             cross_view(S, c.T, c.I, second);
-            pair_friction_rows<5>(S, c.T, second, P, pool0, rc);
-            pair_friction_rows<6>(S, c.T, second, P, pool0, rc);
-            pair_friction_rows<7>(S, c.T, second, P, pool0, rc);
-            pair_friction_rows<8>(S, c.T, second, P, pool0, rc);
+            pair_friction_rows<5>(S, c.T, second, P, pool0, tol, badc);
+            pair_friction_rows<6>(S, c.T, second, P, pool0, tol, badc);
+            pair_friction_rows<7>(S, c.T, second, P, pool0, tol, badc);
+            pair_friction_rows<8>(S, c.T, second, P, pool0, tol, badc);
             cross_back(c.I, S, second);
         }
-        const float rp = partner(r);  // every lane that entered the loop is here (pairs together)
-        const float joint = second ? (rp + r) + rc : (r + rp) + rc;
-        if (c.active && (c.merged ? joint : r) <= thr) c.active = false;
+        // every lane that entered the loop is here (pairs together): the env's joint decision
+        const uint32_t pbad = partner_u(bad ? 1u : 0u);
+        if (c.active && !bad && !badc && pbad == 0u) c.active = false;
     }
 }
 
@@ -1144,25 +1133,25 @@ CP_DEV void fast_build(FastIsl& F, const Ctx& c, float* pool) {
 // one ground row (A = static ground) on body b: isl_row<0, B, FRICTION> with r x t
 // and M (r x t) precomputed
 template <bool FRICTION>
-CP_DEV float fast_grow(Dyn& b, float imb, V3 t, V3 rbt, V3 ib, float inv_eff, float target, float& lam,
-                       float bound) {
+CP_DEV bool fast_grow(Dyn& b, float imb, V3 t, V3 rbt, V3 ib, float inv_eff, float target, float& lam,
+                      float bound, float tol) {
     const float vn = dot(t, b.v) + dot(b.w, rbt);
     const float e = target - vn;
     float dl = e * inv_eff;
     const float l0 = lam + dl;
     float ln;
     if constexpr (!FRICTION) ln = l0 > 0.0f ? l0 : 0.0f;
-    else ln = __builtin_amdgcn_fmed3f(l0, -bound, bound);  // = the oracle's clamp (see isl_row_ez)
+    else ln = bound > 0.0f ? __builtin_amdgcn_fmed3f(l0, -bound, bound) : lam;  // see isl_row_ez
     dl = ln - lam;
     lam = ln;
     const float sb = dl * imb;
     b.v = madd(b.v, t, sb);
     b.w = madd(b.w, ib, dl);
-    return fabsf(e * dl);
+    return fabsf(dl) > tol * inv_eff;  // Bullet residual test (oracle: solve_row)
 }
 
 // one cart-pole normal row: isl_row<1, 2, false> with both bodies' terms precomputed
-CP_DEV float fast_crow(Isl& I, V3 t, const CRow& R, float& lam) {
+CP_DEV bool fast_crow(Isl& I, V3 t, const CRow& R, float& lam, float tol) {
     const float vn = (dot(t, sub(I.d2.v, I.d1.v)) + dot(I.d2.w, R.rbt)) - dot(I.d1.w, R.rat);
     const float e = R.tg - vn;
     float dl = e * R.ie;
@@ -1176,13 +1165,13 @@ CP_DEV float fast_crow(Isl& I, V3 t, const CRow& R, float& lam) {
     const float sa = dl * I.im1;
     I.d1.v = madd(I.d1.v, neg(t), sa);
     I.d1.w = madd(I.d1.w, neg(R.ia), dl);
-    return fabsf(e * dl);
+    return fabsf(dl) > tol * R.ie;  // Bullet residual test (oracle: solve_row)
 }
 
-// sweeps() with the island rows in fast form (same row order, same residual sums)
+// sweeps() with the island rows in fast form (same row order, same stopping rule)
 CP_DEV void sweeps_fast(Ctx& c, FastIsl& F, Sim& S, const cp_physics& P, float* pool, float* pool0, bool second,
                         int it0, int it1, Stamps& ST) {
-    const float thr = P.residual_threshold;
+    const float tol = sqrtf(P.residual_threshold);
     const int cnt0 = pk_cnt(c.T.pk[0]), cnt1 = pk_cnt(c.T.pk[1]), cnt2 = pk_cnt(c.T.pk[2]);
     const int fc1 = pk_fcnt(c.T.pk[1]);
     const V3 n0 = c.T.n[0], n1 = c.T.n[1], n2 = c.T.n[2];
@@ -1191,27 +1180,27 @@ CP_DEV void sweeps_fast(Ctx& c, FastIsl& F, Sim& S, const cp_physics& P, float* 
 #ifdef CP_STAMPS
         ST.sweeps += 1;
 #endif
-        float r = 0.0f, rc = 0.0f;
+        bool bad = false, badc = false;
         if (c.active) {
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if (k < cnt0) r = r + fast_grow<false>(c.I.d1, c.I.im1, n0, F.g0[k].rbt, F.g0[k].ib, F.g0[k].ie,
-                                                       F.g0[k].tg, F.g0[k].lam, 0.0f);
+                if (k < cnt0) bad |= fast_grow<false>(c.I.d1, c.I.im1, n0, F.g0[k].rbt, F.g0[k].ib, F.g0[k].ie,
+                                                      F.g0[k].tg, F.g0[k].lam, 0.0f, tol);
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if (k < cnt1) r = r + fast_grow<false>(c.I.d2, c.I.im2, n1, F.g1[k].rbt, F.g1[k].ib, F.g1[k].ie,
-                                                       F.g1[k].tg, F.g1[k].lam, 0.0f);
+                if (k < cnt1) bad |= fast_grow<false>(c.I.d2, c.I.im2, n1, F.g1[k].rbt, F.g1[k].ib, F.g1[k].ie,
+                                                      F.g1[k].tg, F.g1[k].lam, 0.0f, tol);
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if (k < cnt2) r = r + fast_crow(c.I, n2, F.c2[k], F.c2[k].lam);
+                if (k < cnt2) bad |= fast_crow(c.I, n2, F.c2[k], F.c2[k].lam, tol);
         }
         const bool cross = c.active && c.merged;  // same on both lanes of an env
         if (__ballot(cross) != 0ull && cross) {
             cross_view(S, c.T, c.I, second);
-            pair_normal_rows<5>(S, c.T, second, P, pool0, rc);
-            pair_normal_rows<6>(S, c.T, second, P, pool0, rc);
-            pair_normal_rows<7>(S, c.T, second, P, pool0, rc);
-            pair_normal_rows<8>(S, c.T, second, P, pool0, rc);
+            pair_normal_rows<5>(S, c.T, second, P, pool0, tol, badc);
+            pair_normal_rows<6>(S, c.T, second, P, pool0, tol, badc);
+            pair_normal_rows<7>(S, c.T, second, P, pool0, tol, badc);
+            pair_normal_rows<8>(S, c.T, second, P, pool0, tol, badc);
             cross_back(c.I, S, second);
         }
         if (c.active) {
@@ -1219,24 +1208,23 @@ CP_DEV void sweeps_fast(Ctx& c, FastIsl& F, Sim& S, const cp_physics& P, float* 
             for (int k = 0; k < 4; ++k) {
                 if (k < fc1) {
                     const float bound = c.mu1 * F.g1[k].lam;
-                    r = r + fast_grow<true>(c.I.d2, c.I.im2, F.t1, F.f1[k].rbt1, F.f1[k].ib1, F.f1[k].ie1, 0.0f,
-                                            F.f1[k].l1, bound);
-                    r = r + fast_grow<true>(c.I.d2, c.I.im2, F.t2, F.f1[k].rbt2, F.f1[k].ib2, F.f1[k].ie2, 0.0f,
-                                            F.f1[k].l2, bound);
+                    bad |= fast_grow<true>(c.I.d2, c.I.im2, F.t1, F.f1[k].rbt1, F.f1[k].ib1, F.f1[k].ie1, 0.0f,
+                                           F.f1[k].l1, bound, tol);
+                    bad |= fast_grow<true>(c.I.d2, c.I.im2, F.t2, F.f1[k].rbt2, F.f1[k].ib2, F.f1[k].ie2, 0.0f,
+                                           F.f1[k].l2, bound, tol);
                 }
             }
         }
         if (__ballot(cross) != 0ull && cross) {
             cross_view(S, c.T, c.I, second);
-            pair_friction_rows<5>(S, c.T, second, P, pool0, rc);
-            pair_friction_rows<6>(S, c.T, second, P, pool0, rc);
-            pair_friction_rows<7>(S, c.T, second, P, pool0, rc);
-            pair_friction_rows<8>(S, c.T, second, P, pool0, rc);
+            pair_friction_rows<5>(S, c.T, second, P, pool0, tol, badc);
+            pair_friction_rows<6>(S, c.T, second, P, pool0, tol, badc);
+            pair_friction_rows<7>(S, c.T, second, P, pool0, tol, badc);
+            pair_friction_rows<8>(S, c.T, second, P, pool0, tol, badc);
             cross_back(c.I, S, second);
         }
-        const float rp = partner(r);  // every lane that entered the loop is here (pairs together)
-        const float joint = second ? (rp + r) + rc : (r + rp) + rc;
-        if (c.active && (c.merged ? joint : r) <= thr) c.active = false;
+        const uint32_t pbad = partner_u(bad ? 1u : 0u);  // every lane that entered the loop is here
+        if (c.active && !bad && !badc && pbad == 0u) c.active = false;
     }
 }
 
@@ -1253,131 +1241,9 @@ CP_DEV void fast_store(const FastIsl& F, const Ctx& c, float* pool) {
     }
 }
 
-// Class-specialised fast sweeps for the tail kernel.  Tail envs are sorted into
-// classes by the row groups of their unconverged islands: CLS 0 = ground-cart +
-// cart-pole rows (a pole standing on its cart: ~85% of the islands that reach the
-// sweep cap), CLS 1 = ground-cart + ground-pole rows with the pole's friction rows.
-// Neither class has a merged env or friction on local pairs 0 / 2.  Absent row groups
-// compile away, so each loop keeps its rows in architectural VGPRs.
-template <int CLS>
-CP_DEV void fast_build_cls(FastIsl& F, const Ctx& c, float* pool) {
-    fast_ground_rows<0>(F.g0, c, pool);
-    if constexpr (CLS == 1) {
-        fast_ground_rows<1>(F.g1, c, pool);
-        const uint32_t pk = c.T.pk[1];
-        const int fcnt = pk_fcnt(pk), base = pk_base(pk), fbase = pk_fbase(pk);
-        plane_space(c.T.n[1], F.t1, F.t2);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (k < fcnt) {
-                const int s = base + k, fs = fbase + k;
-                const V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
-                FRow& R = F.f1[k];
-                R.rbt1 = cross(rb, F.t1);
-                R.ib1 = symv(c.I.d2.M, R.rbt1);
-                R.rbt2 = cross(rb, F.t2);
-                R.ib2 = symv(c.I.d2.M, R.rbt2);
-                R.ie1 = pool_f(pool, FF_IE1, fs);
-                R.ie2 = pool_f(pool, FF_IE2, fs);
-                R.l1 = pool_f(pool, FF_L1, fs);
-                R.l2 = pool_f(pool, FF_L2, fs);
-            }
-        }
-    } else {
-        const uint32_t pk = c.T.pk[2];
-        const int cnt = pk_cnt(pk), base = pk_base(pk);
-        const V3 n = c.T.n[2];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (k < cnt) {
-                const int s = base + k;
-                const V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
-                CRow& R = F.c2[k];
-                R.rbt = cross(rb, n);
-                R.ib = symv(c.I.d2.M, R.rbt);
-                const V3 ra = add(rb, sub(c.I.d2.x, c.I.d1.x));
-                R.rat = cross(ra, n);
-                R.ia = symv(c.I.d1.M, R.rat);
-                R.ie = pool_n(pool, F_IE, s);
-                R.tg = pool_n(pool, F_TG, s);
-                R.lam = pool_n(pool, F_LAM, s);
-            }
-        }
-    }
-}
-
-template <int CLS>
-CP_DEV void sweeps_cls(Ctx& c, FastIsl& F, const cp_physics& P, bool second, int it0, int it1, Stamps& ST) {
-    const float thr = P.residual_threshold;
-    const int cnt0 = pk_cnt(c.T.pk[0]);
-    const int cnt1 = CLS == 1 ? pk_cnt(c.T.pk[1]) : 0, fc1 = CLS == 1 ? pk_fcnt(c.T.pk[1]) : 0;
-    const int cnt2 = CLS == 0 ? pk_cnt(c.T.pk[2]) : 0;
-    const V3 n0 = c.T.n[0], n1 = c.T.n[1], n2 = c.T.n[2];
-    for (int it = it0; it < it1; ++it) {
-        if (__ballot(c.active) == 0ull) break;
-#ifdef CP_STAMPS
-        ST.sweeps += 1;
-#endif
-        float r = 0.0f;
-        if (c.active) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (k < cnt0) r = r + fast_grow<false>(c.I.d1, c.I.im1, n0, F.g0[k].rbt, F.g0[k].ib, F.g0[k].ie,
-                                                       F.g0[k].tg, F.g0[k].lam, 0.0f);
-            if constexpr (CLS == 1) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (k < cnt1) r = r + fast_grow<false>(c.I.d2, c.I.im2, n1, F.g1[k].rbt, F.g1[k].ib,
-                                                           F.g1[k].ie, F.g1[k].tg, F.g1[k].lam, 0.0f);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    if (k < fc1) {
-                        const float bound = c.mu1 * F.g1[k].lam;
-                        r = r + fast_grow<true>(c.I.d2, c.I.im2, F.t1, F.f1[k].rbt1, F.f1[k].ib1, F.f1[k].ie1, 0.0f,
-                                                F.f1[k].l1, bound);
-                        r = r + fast_grow<true>(c.I.d2, c.I.im2, F.t2, F.f1[k].rbt2, F.f1[k].ib2, F.f1[k].ie2, 0.0f,
-                                                F.f1[k].l2, bound);
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (k < cnt2) r = r + fast_crow(c.I, n2, F.c2[k], F.c2[k].lam);
-            }
-        }
-        if (c.active && r <= thr) c.active = false;  // no merged env in these classes
-    }
-}
-
-template <int CLS>
-CP_DEV void fast_store_cls(const FastIsl& F, const Ctx& c, float* pool) {
-    const int cnt0 = pk_cnt(c.T.pk[0]), b0 = pk_base(c.T.pk[0]);
-    const int cnt1 = pk_cnt(c.T.pk[1]), b1 = pk_base(c.T.pk[1]);
-    const int cnt2 = pk_cnt(c.T.pk[2]), b2 = pk_base(c.T.pk[2]);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        if (k < cnt0) pool_n(pool, F_LAM, b0 + k) = F.g0[k].lam;
-        if (CLS == 1 && k < cnt1) pool_n(pool, F_LAM, b1 + k) = F.g1[k].lam;
-        if (CLS == 0 && k < cnt2) pool_n(pool, F_LAM, b2 + k) = F.c2[k].lam;
-    }
-}
-
-// tail class of an env whose islands are not all converged (both lanes of the pair
-// call it in converged code: the DPP read needs the partner lane)
-CP_DEV int tail_class(const Ctx& c) {
-    const uint32_t own = c.active ? ((pk_cnt(c.T.pk[1]) > 0 ? 1u : 0u) | (pk_cnt(c.T.pk[2]) > 0 ? 2u : 0u) |
-                                     (fast_ok(c) ? 0u : 4u))
-                                  : 0u;
-    const uint32_t both = own | partner_u(own);
-    if (c.merged || (both & 4u)) return 2;
-    if (!(both & 1u)) return 0;
-    if (!(both & 2u)) return 1;
-    return 2;
-}
-
 // PGS sweeps [it0, it1) of the lane's island.  FAST: fast-form island rows when no
 // lane of the wave has friction rows on local pairs 0 / 2 (wave-uniform choice; the
-// fast form needs a register budget only the tail kernel has).
+// fast form needs the register budget of the 1-wave-per-SIMD latency kernels).
 template <bool FAST>
 CP_DEV void solve_range(Ctx& c, Sim& S, const cp_physics& P, float* pool, float* pool0, bool second, int it0, int it1,
                         Stamps& ST) {
@@ -1596,8 +1462,8 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, float* pool
     // Island rows run per lane; the rows of the two islands touch disjoint bodies,
     // so running them side by side equals the oracle's interleaved order.  Cross
     // rows (merged env) run on both lanes on the whole-env view after the island
-    // rows of the same kind, as in the oracle; a merged env stops on the joint
-    // residual (island 0 + island 1) + cross.
+    // rows of the same kind, as in the oracle.  Both lanes sweep until the env's joint
+    // stopping test passes (one solver group, oracle: substep step 4).
     isl_warmstart<0>(I, T, pool);
     isl_warmstart<1>(I, T, pool);
     isl_warmstart<2>(I, T, pool);
@@ -1607,7 +1473,7 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, float* pool
         pair_warmstart<7>(S, T, second, P, pool0); pair_warmstart<8>(S, T, second, P, pool0);
         cross_back(I, S, second);
     }
-    c.active = c.merged ? c.tot > 0 : used > 0;
+    c.active = c.tot > 0;  // same on both lanes of the env
 }
 
 // Phase 3: whole-env velocities from the two lanes' islands (both lanes of every
@@ -1676,7 +1542,7 @@ CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx
 }
 
 
-// One p.stepSimulation() for this lane's env, without migration (all sweeps in place).
+// One p.stepSimulation() for this lane's env.
 // FAST: fast-form island rows where the wave allows them (the 512-register kernels).
 template <bool FAST = false>
 CP_DEV void substep(Sim& S, const cp_physics& P, const Lane& L, float* pool, float* pool0, int& overflow,

@@ -616,9 +616,19 @@ static real row_k(const sim_t* S, const cp_physics* P, int a, int b, v3 rb, v3 t
     return ((ima + imb) + dot(rat, ia)) + dot(rbt, ib);
 }
 
-/* one PGS row (normal when lo==0 && hi<0 sentinel, friction otherwise) */
-static real solve_row(sim_t* S, const cp_physics* P, int a, int b, v3 rb, v3 t,
-                      real inv_eff, real target, real* lam, int friction, real bound) {
+/* One PGS row: Bullet's resolveSingleConstraintRowLowerLimit (normal rows, lambda >= 0)
+ * and resolveSingleConstraintRowGeneric (friction rows, |lambda| <= mu * lambda_n) [ext].
+ * Returns 1 when the row is NOT converged by Bullet's stopping rule: the row residual is
+ * deltaImpulse * (1 / jacDiagABInv) and the solve stops when the max of its square over
+ * all rows is <= leastSquaresResidualThreshold (btSequentialImpulseConstraintSolver::
+ * solveSingleIteration, pybullet's 1e-7).  With inv_eff = jacDiagABInv > 0 that test is
+ * |dl| <= sqrt(threshold) * inv_eff, evaluated here as that product (no division per
+ * row; `tol` = sqrt(threshold)).  A friction row whose normal impulse is not > 0 is
+ * skipped (Bullet: `if (totalImpulse > 0)`): lambda and the velocities stay as they are
+ * and the row adds no residual; written as ln = lam so that it is the kernel's
+ * branch-free form. */
+static int solve_row(sim_t* S, const cp_physics* P, int a, int b, v3 rb, v3 t,
+                     real inv_eff, real target, real* lam, int friction, real bound, real tol) {
     int db_ = b - 1;
     real imb = (real)P->inv_mass[b];
     v3 rbt = cross(rb, t);
@@ -639,7 +649,8 @@ static real solve_row(sim_t* S, const cp_physics* P, int a, int b, v3 rb, v3 t,
     real l0 = *lam + dl;
     real ln;
     if (!friction) ln = l0 > RC(0) ? l0 : RC(0);
-    else ln = l0 > bound ? bound : (l0 < -bound ? -bound : l0);
+    else if (bound > RC(0)) ln = l0 > bound ? bound : (l0 < -bound ? -bound : l0);
+    else ln = *lam;
     dl = ln - *lam;
     *lam = ln;
     real sb = dl * imb;
@@ -650,7 +661,7 @@ static real solve_row(sim_t* S, const cp_physics* P, int a, int b, v3 rb, v3 t,
         S->v[da_] = madd(S->v[da_], neg(t), sa);
         S->w[da_] = madd(S->w[da_], neg(ia), dl);
     }
-    return FABS(e * dl);
+    return FABS(dl) > tol * inv_eff;
 }
 
 /* velocity change of an impulse lam along t at lever arm rb (warm start) */
@@ -699,17 +710,18 @@ static void orc_stats_island(const island_t* I, int merged, int it) {
 }
 #endif
 
-/* row sweep helpers: all normal rows, then all friction rows, of local pairs [j0, j1) */
-static void sweep_normal(sim_t* S, const cp_physics* P, island_t* I, int isl, int j, real* r) {
+/* row sweep helpers: the normal rows, or the friction rows, of local pair j; *bad |= a row
+ * above the residual tolerance */
+static void sweep_normal(sim_t* S, const cp_physics* P, island_t* I, int isl, int j, real tol, int* bad) {
     int g = ISLAND_PAIR[isl][j];
     int a = PAIR_A[g], b = PAIR_B[g];
     manifold_t* m = &I->man[j];
     for (int k = 0; k < m->cnt; ++k) {
         point_t* q = &I->pt[m->base + k];
-        *r = *r + solve_row(S, P, a, b, q->rb, m->n, q->inv_eff, q->target, &q->lam, 0, RC(0));
+        *bad |= solve_row(S, P, a, b, q->rb, m->n, q->inv_eff, q->target, &q->lam, 0, RC(0), tol);
     }
 }
-static void sweep_friction(sim_t* S, const cp_physics* P, island_t* I, int isl, int j, real* r) {
+static void sweep_friction(sim_t* S, const cp_physics* P, island_t* I, int isl, int j, real tol, int* bad) {
     manifold_t* m = &I->man[j];
     if (m->fcnt == 0) return;
     int g = ISLAND_PAIR[isl][j];
@@ -720,8 +732,8 @@ static void sweep_friction(sim_t* S, const cp_physics* P, island_t* I, int isl, 
         point_t* q = &I->pt[m->base + k];
         fpoint_t* f = &I->fp[m->fbase + k];
         real bound = m->mu * q->lam;
-        *r = *r + solve_row(S, P, a, b, q->rb, t1, f->inv_eff1, RC(0), &f->lam1, 1, bound);
-        *r = *r + solve_row(S, P, a, b, q->rb, t2, f->inv_eff2, RC(0), &f->lam2, 1, bound);
+        *bad |= solve_row(S, P, a, b, q->rb, t1, f->inv_eff1, RC(0), &f->lam1, 1, bound, tol);
+        *bad |= solve_row(S, P, a, b, q->rb, t2, f->inv_eff2, RC(0), &f->lam2, 1, bound, tol);
     }
 }
 static void warm_pair(sim_t* S, const cp_physics* P, island_t* I, int isl, int j) {
@@ -823,66 +835,58 @@ static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* i
         S->v[d] = madd(v, acc, dt);
         S->w[d] = madd(w, accw, dt);
     }
-    /* 4. warm start + projected Gauss-Seidel.  Islands without a cross-island contact
-     *    are solved independently (own sweeps, own residual, like Bullet's island
-     *    solving); any cross contact merges everything into one solve in the global
-     *    order 0 2 1 3 4 9 5 6 7 8 with residual (island0 + island1) + cross. */
+    /* 4. warm start + projected Gauss-Seidel over ONE solver group per env.  Bullet's
+     *    island manager batches islands into one solve until the group holds
+     *    m_minimumSolverBatchSize (128) constraints [ext], so the two cart-pole islands
+     *    (<= 40 rows together) are one solve with one stopping decision: the sweep runs
+     *    every normal row, then every friction row, and stops after the sweep whose
+     *    largest squared row residual is <= leastSquaresResidualThreshold
+     *    (solve_row), or after solver_iterations sweeps.  Without a cross-island contact
+     *    the rows of the two islands touch disjoint bodies, so island 0's sweep then
+     *    island 1's gives the same numbers as their rows interleaved; with one, the
+     *    order is 0 2 1 3 4 9 5 6 7 8 (normal rows, then friction rows). */
     const int iters = P->solver_iterations;
-    const real thr = (real)P->residual_threshold;
+    const real tol = SQRT((real)P->residual_threshold);
     int merged = 0;
     for (int p = 0; p < CP_NUM_ISLANDS; ++p) merged |= (isl[p].man[3].cnt + isl[p].man[4].cnt) > 0;
-    int it_max = 0;
+    int it = 0;
     if (!merged) {
-        for (int p = 0; p < CP_NUM_ISLANDS; ++p) {
-            island_t* I = &isl[p];
-            for (int j = 0; j < 3; ++j) warm_pair(S, P, I, p, j);
-            int it = 0;
-            if (I->used > 0) {
-                for (it = 0; it < iters;) {
-                    real r = RC(0);
-                    for (int j = 0; j < 3; ++j) sweep_normal(S, P, I, p, j, &r);
-                    for (int j = 0; j < 3; ++j) sweep_friction(S, P, I, p, j, &r);
-                    ++it;
-#ifdef ORC_DEBUG
-                    if (getenv("ORC_DEBUG")) fprintf(stderr, "isl %d it %d resid %g\n", p, it, (double)r);
-#endif
-                    if (r <= thr) break;
+        for (int p = 0; p < CP_NUM_ISLANDS; ++p)
+            for (int j = 0; j < 3; ++j) warm_pair(S, P, &isl[p], p, j);
+        if (isl[0].used + isl[1].used > 0) {
+            for (it = 0; it < iters;) {
+                int bad = 0;
+                for (int p = 0; p < CP_NUM_ISLANDS; ++p) {
+                    for (int j = 0; j < 3; ++j) sweep_normal(S, P, &isl[p], p, j, tol, &bad);
+                    for (int j = 0; j < 3; ++j) sweep_friction(S, P, &isl[p], p, j, tol, &bad);
                 }
-            }
-            if (it > it_max) it_max = it;
-            if (isl_iters && it > isl_iters[p]) isl_iters[p] = it;
-#ifdef ORC_STATS  /* diagnostic build only (tools/row_classes.py): row structure + sweeps per island */
-            orc_stats_island(I, 0, it);
+                ++it;
+#ifdef ORC_DEBUG
+                if (getenv("ORC_DEBUG")) fprintf(stderr, "it %d bad %d\n", it, bad);
 #endif
+                if (!bad) break;
+            }
         }
     } else {
         /* global order: (0,0) (1,0) (0,1) (1,1) (0,2) (1,2) then cross (0,3) (0,4) (1,3) (1,4) */
         static const int ORD_I[10] = {0, 1, 0, 1, 0, 1, 0, 0, 1, 1};
         static const int ORD_J[10] = {0, 0, 1, 1, 2, 2, 3, 4, 3, 4};
         for (int o = 0; o < 10; ++o) warm_pair(S, P, &isl[ORD_I[o]], ORD_I[o], ORD_J[o]);
-        int it = 0;
         for (it = 0; it < iters;) {
-            real rs[3] = {RC(0), RC(0), RC(0)};
-            for (int o = 0; o < 10; ++o) {
-                int p = ORD_I[o], j = ORD_J[o];
-                sweep_normal(S, P, &isl[p], p, j, &rs[j < 3 ? p : 2]);
-            }
-            for (int o = 0; o < 10; ++o) {
-                int p = ORD_I[o], j = ORD_J[o];
-                sweep_friction(S, P, &isl[p], p, j, &rs[j < 3 ? p : 2]);
-            }
-            real resid = (rs[0] + rs[1]) + rs[2];
+            int bad = 0;
+            for (int o = 0; o < 10; ++o) sweep_normal(S, P, &isl[ORD_I[o]], ORD_I[o], ORD_J[o], tol, &bad);
+            for (int o = 0; o < 10; ++o) sweep_friction(S, P, &isl[ORD_I[o]], ORD_I[o], ORD_J[o], tol, &bad);
             ++it;
-            if (resid <= thr) break;
+            if (!bad) break;
         }
-        it_max = it;
-        if (isl_iters)
-            for (int p = 0; p < CP_NUM_ISLANDS; ++p)
-                if (it > isl_iters[p]) isl_iters[p] = it;
-#ifdef ORC_STATS
-        for (int p = 0; p < CP_NUM_ISLANDS; ++p) orc_stats_island(&isl[p], 1, it);
-#endif
     }
+    const int it_max = it;
+    if (isl_iters)
+        for (int p = 0; p < CP_NUM_ISLANDS; ++p)
+            if (it > isl_iters[p]) isl_iters[p] = it;
+#ifdef ORC_STATS  /* diagnostic build only (tools/row_classes.py): row structure + sweeps per island */
+    for (int p = 0; p < CP_NUM_ISLANDS; ++p) orc_stats_island(&isl[p], merged, it);
+#endif
     /* 4c. refresh the warm-start cache */
     for (int p = 0; p < CP_NUM_ISLANDS; ++p) {
         for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
