@@ -1,25 +1,36 @@
 #!/usr/bin/env python3
 """bench.py — batched cartpole++ env-steps/sec on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]                       # C3 (default)
+    python bench.py --continuous --batch 4096                             # C2
+    python bench.py --raster                                              # C5
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
-        --master-port P bench.py --gpus N --steps K --warmup W
+        --master-port P bench.py --gpus N --steps K --warmup W            # C4 at N = 8
 
-Workload (BASELINE.json configs[2] / SURVEY.md §8d C3, per GPU): 65,536 envs, discrete
-5-action random policy (int8 actions pre-generated in HBM), action_repeats R = 3,
-steps_per_repeat 1, initial_force 55, max_episode_len 200 with in-kernel autoreset,
-fp32.  A "step" is one env-step of every env: one cp_step call = one fused R-substep
-kernel launch + one compacted reset launch.  Envs shard across ranks (seed 1234+rank,
-global env ids offset rank*B); the only collective is an RCCL all-gather of the
-episode returns once per 200-step window (C4).  value = N*B*K / max-over-ranks wall.
+Workloads (the line's config.workload is derived from the arguments):
+  C2  4,096 envs, continuous (B,2,2) U[-1,1] actions, R = 3
+  C3  65,536 envs per GPU, discrete 5-action U{0..4}, R = 3 (the headline, configs[2])
+  C4  C3 on N GPUs: envs shard (global env id = rank*B + i keys the bump Philox stream and
+      the action stream, one seed on every rank), RCCL all-gather of the episode returns
+  C5  C3 + in-kernel 50x50x3 fp16 raster obs
+All: steps_per_repeat 1, initial_force 55, max_episode_len 200, in-kernel autoreset, fp32.
+A "step" is one env-step of every env: one cp_step call = one fused R-substep kernel
+launch + one compacted reset launch.  Actions are pre-generated in HBM (a hash of
+(seed, global env id, step, cart)), so sharded runs see the unsharded job's actions.
 
-roofline: the step kernel's algorithmic HBM bytes per launch over
-its average duration from HIP events recorded on its launch stream in the timed region
+Timing: W untimed steps, then EXACTLY K steps between barrier + synchronize; value =
+N*B*K / max-over-ranks wall.  A K-step window need not contain an autoreset burst (every
+episode is 200 steps) or, at N > 1, a return gather; so the line also reports
+resets_in_window, collectives_in_window, and a steady_state sub-object: one more full
+200-step cycle (its reset burst and one gather included) timed the same way.
+
+roofline: the step kernel's algorithmic HBM bytes per launch over its
+average duration from HIP events recorded on its launch stream in the timed region
 (every 4th launch sampled: the events themselves cost wall time).
-cpu_baseline: the CPU oracle (a port: same algorithm, gcc -O2, OpenMP) on a bounded
-sample of the same workload, rank 0 at N = 1 only.
-parity: max |pose diff| over 200 steps of 512 C3 envs against the oracle's fp32 build
-(bit-exact bar) and its fp64 build (drift), rank 0 at N = 1 only, after the timed region.
+cpu_baseline (rank 0, N = 1): the oracle (a port: same algorithm, gcc -O3 -march=native,
+the kernel's results) on bounded samples: C3 on all cores (OpenMP), C3 on one core, C1.
+parity (rank 0, N = 1): SURVEY.md §8d's matrix, GPU vs the oracle's fp32 build (bit-exact
+bar) and fp64 build (drift), with and without the PGS early exit.
 """
 import argparse
 import json
@@ -33,20 +44,71 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from cartpoleplusplus_amd import abi  # noqa: E402
 from cartpoleplusplus_amd.batched import BatchedCartpole  # noqa: E402
 from cartpoleplusplus_amd.dist import gather_returns, return_histogram, shard_spec  # noqa: E402
 
 METRIC = "env-steps/sec at batch=65,536, 1→8 MI355X; max |pose−pybullet| over 200 steps"
 HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s spec, 6.29 measured)
-WINDOW = 200            # episode-return reporting window (steps)
+WINDOW = 200            # episode length = return-gather window (steps)
+SEED = 1234             # one seed for bumps and actions, on every rank
 # HIP events around every 4th step-kernel launch (every reset launch): each recorded event
 # costs the stream a few microseconds (tools/timing_overhead.py: 0.761 ms/step with events on
 # every launch, 0.755 with this sampling, 0.748 without events)
 STEP_EVENT_STRIDE = 4
+# MI355X_MICROARCH.md: 256 CUs x 4 SIMD-32, a wave64 VALU instruction takes 2 issue
+# cycles of its SIMD (one wave alone sustains one per 4), 2.4 GHz max clock
+VALU_PEAK_WINST_PER_S = 256 * 4 * 2.4e9 / 2
 
 
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+# ----------------------------------------------------------------------- actions
+_M32 = 0xFFFFFFFF
+
+
+def _mix32(x):
+    """lowbias32 integer hash (Wellons), on int64 tensors holding 32-bit values."""
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & _M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & _M32
+    return x ^ (x >> 16)
+
+
+def action_block(continuous, gid, t0, n, seed):
+    """Actions of steps [t0, t0+n) for global env ids `gid` (int64, device): a pure function
+    of (seed, global env id, step, cart), so a shard computes exactly the rows the unsharded
+    job would give its envs.  continuous: float32 (n, B, 2, 2) U[-1, 1) (the declared Box,
+    bullet_cartpole.py:94); discrete: int8 (n, B, 2) U{0..4}."""
+    dev = gid.device
+    t = torch.arange(t0, t0 + n, device=dev, dtype=torch.int64).view(n, 1, 1)
+    c = torch.arange(4 if continuous else 2, device=dev, dtype=torch.int64).view(1, 1, -1)
+    g = gid.view(1, -1, 1)
+    x = _mix32((seed * 0x9E3779B1 + t * 0x85EBCA77 + c * 0xC2B2AE3D) & _M32)
+    x = _mix32((x ^ (g & _M32)) & _M32)
+    x = _mix32((x + ((g >> 32) * 0x27D4EB2F)) & _M32)
+    if continuous:
+        u = (x >> 8).to(torch.float32) * (1.0 / (1 << 24))
+        return (2.0 * u - 1.0).view(n, -1, 2, 2)
+    return ((x * 5) >> 32).to(torch.int8)
+
+
+def make_actions(continuous, B, env_id_offset, steps, seed, dev):
+    gid = torch.arange(env_id_offset, env_id_offset + B, device=dev, dtype=torch.int64)
+    blocks, t, chunk = [], 0, max(1, (1 << 24) // (B * 4))
+    while t < steps:
+        n = min(chunk, steps - t)
+        blocks.append(action_block(continuous, gid, t, n, seed))
+        t += n
+    return torch.cat(blocks)
+
+
+# ------------------------------------------------------------------- roofline
 def step_kernel_bytes(R, action_bytes):
-    """Algorithmic HBM bytes one env moves in one step-kernel launch (DESIGN.md §Roofline)."""
+    """Algorithmic HBM bytes one env moves in one step-kernel launch (DESIGN.md §5)."""
     state_read = 52 + 6 + 2            # 4 bodies x 13, 2 pending forces x 3, steps, done
     state_write = 52 + 6 + 1           # bodies, pending forces, steps
     warm_cache = 2 * (10 + 40)         # warm-start ids + impulses, read + write once per step
@@ -59,134 +121,290 @@ def render_kernel_bytes(H, W, C, R):
     return 2 * H * W * 3 * C * R + 4 * R * 4 * 7 + 4
 
 
-def pmc_traffic(kernel, batch, repeats):
+def _pmc_files():
+    import glob
+    return list(reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))))
+
+
+def _pmc_match(d, batch, repeats, kind):
+    return d.get("batch", batch) == batch and d.get("repeats", repeats) == repeats and \
+        d.get("action_kind", "discrete") == kind
+
+
+def pmc_traffic(kernel, batch, repeats, kind):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
     (profiles/<tag>_pmc.json, tools/profile.sh + tools/summarize_profile.py), if it was
     collected on this workload; else None."""
-    import glob
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
-    for p in reversed(paths):
+    for p in _pmc_files():
         with open(p) as f:
             d = json.load(f)
         k = d.get("kernels", {}).get(kernel)
-        if k and "hbm_bytes_per_launch" in k and d.get("batch", batch) == batch and d.get("repeats", repeats) == repeats:
+        if k and "hbm_bytes_per_launch" in k and _pmc_match(d, batch, repeats, kind):
             return k["hbm_bytes_per_launch"], os.path.relpath(p, ROOT)
     return None, None
 
 
-def pmc_valu(kernel, batch, repeats):
+def pmc_valu(kernel, batch, repeats, kind):
     """VALU wave-instructions per launch of `kernel` (SQ_INSTS_VALU) from the newest
     committed PMC summary of this workload, else None."""
-    import glob
-    for p in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))):
+    for p in _pmc_files():
         with open(p) as f:
             d = json.load(f)
         k = d.get("kernels", {}).get(kernel)
-        if k and "SQ_INSTS_VALU" in k.get("sq_per_launch", {}) and d.get("batch", batch) == batch \
-                and d.get("repeats", repeats) == repeats:
+        if k and "SQ_INSTS_VALU" in k.get("sq_per_launch", {}) and _pmc_match(d, batch, repeats, kind):
             return k["sq_per_launch"]["SQ_INSTS_VALU"], os.path.relpath(p, ROOT)
     return None, None
 
 
-# MI355X_MICROARCH.md: 256 CUs x 4 SIMD-32, a wave64 VALU instruction takes 2 issue
-# cycles of its SIMD (one wave alone sustains one per 4), 2.4 GHz max clock
-VALU_PEAK_WINST_PER_S = 256 * 4 * 2.4e9 / 2
+def step_shape(B):
+    """The step-kernel shape cp_create picks (cp_kernels.hip choose_reset_shape)."""
+    e = os.environ.get("CP_STEP_LATENCY")
+    lat = (e == "1") if e in ("0", "1") else B <= 32768
+    return "latency" if lat else "throughput"
 
 
-def log(*a):
-    print(*a, file=sys.stderr, flush=True)
+# ------------------------------------------------------------------- workload
+def workload(args, world):
+    B, R = args.batch, args.repeats
+    act = "continuous 2D action U[-1,1] (B,2,2) fp32" if args.continuous else "discrete 5-action U{0..4} int8"
+    name = "custom"
+    if args.raster:
+        name = "C5" if (B == 65536 and not args.continuous) else "custom"
+    elif args.continuous:
+        name = "C2" if B == 4096 else "custom"
+    elif B == 65536:
+        name = "C4" if world > 1 else "C3"
+    idx = {"C2": 1, "C3": 2, "C4": 3, "C5": 4}.get(name)
+    s = (f"{name}: batch={B:,} envs/GPU x {world} GPU(s) = {B * world:,} envs, {act}, R={R}, S=1, "
+         f"autoreset at {WINDOW}, initial_force=55, {args.dtype}")
+    if args.raster:
+        s += f", + in-kernel raster obs 50x50x3xR fp16 to HBM ({args.cameras} camera(s))"
+    if world > 1:
+        s += ", RCCL all-gather of episode returns per 200-step window"
+    if args.done_on_bounds:
+        s += ", bounds termination on (bullet_cartpole.py:243-253)"
+    if args.solver_iterations is not None:
+        s += f", solver_iterations={args.solver_iterations} (diagnostic)"
+    if idx is not None:
+        s += f" (BASELINE.json configs[{idx}])"
+    return name, s
 
 
+def episodes(env):
+    """Per-env episode counters (resets so far), int64 on the device."""
+    st = env.get_state()[abi.CP_SF_EPISODE]
+    if st.dtype == torch.float64:
+        return st.view(torch.int32)[0::2].to(torch.int64)
+    return st.view(torch.int32).to(torch.int64)
+
+
+def timed(env, actions, t0, K, world, dev, gather_at_end):
+    """K steps between barrier + synchronize; -> (max-over-ranks seconds, histogram, gathers)."""
+    hist, gathers = None, 0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    start = time.perf_counter()
+    for t in range(K):
+        env.step(actions[t0 + t])
+        if (t0 + t + 1) % WINDOW == 0:
+            r, _ = env.episode_returns()
+            hist = return_histogram(gather_returns(r), WINDOW)   # RCCL all-gather when world > 1
+            gathers += 1
+    if gather_at_end and gathers == 0:
+        r, _ = env.episode_returns()
+        hist = return_histogram(gather_returns(r), WINDOW)
+        gathers += 1
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - start], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    return float(el.item()), hist, gathers
+
+
+# ----------------------------------------------------------------- CPU legs
 def cpu_baseline(R, budget_s):
-    """Oracle (port) on the host: same workload on a bounded env sample."""
+    """The oracle (port) on the host, -O3 -march=native: C3 on all cores, C3 on one core,
+    C1 (B = 1, R = 2) on one core; each a bounded sample of about budget_s seconds."""
     import numpy as np
 
-    from cartpoleplusplus_amd import abi
     from oracle import oracle as O
-    O.build()
     threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    lib = O.load("native")
 
-    def run(B, steps):
-        cfg = O.default_config(num_envs=B, action_repeats=R, initial_force=55.0, seed=1234, autoreset=1)
-        e = O.Envs(cfg)
+    def run(B, steps, threads_, R_, seed):
+        cfg = O.default_config(num_envs=B, action_repeats=R_, initial_force=55.0, seed=seed, autoreset=1)
+        e = O.Envs(cfg, precision="native")
         e.reset()
-        rng = np.random.default_rng(1234)
+        rng = np.random.default_rng(seed)
         acts = rng.integers(0, 5, (steps, B, 2)).astype(np.int8)
-        obs = np.zeros((B, R, 2, 7), np.float32)
+        obs = np.zeros((B, R_, 2, 7), np.float32)
         rew = np.zeros(B, np.float32)
         done = np.zeros(B, np.uint8)
         t0 = time.perf_counter()
         used = 1
         for t in range(steps):
-            used = e.step_omp(acts[t], abi.CP_ACTION_DISCRETE, obs, rew, done, threads)
-        return time.perf_counter() - t0, used
+            used = e.step_omp(acts[t], abi.CP_ACTION_DISCRETE, obs, rew, done, threads_)
+        return time.perf_counter() - t0, used, obs
 
-    probe_b = 256
-    dt, _ = run(probe_b, 20)
-    rate = probe_b * 20 / dt
-    steps = WINDOW + 1                  # one full episode incl. an in-step autoreset
-    B = int(min(65536, max(256, rate * budget_s / steps)))
-    B -= B % 64
-    dt, used = run(B, steps)
-    return {"value": round(B * steps / dt, 1), "unit": "env-steps/s", "cores": used, "kind": "port",
-            "sample": f"oracle/cp_oracle.c fp32 (same algorithm, gcc -O2 -march=x86-64-v3, OpenMP) on {B} envs x "
-                      f"{steps} steps of the same workload (R={R}, discrete random actions, autoreset incl.); "
-                      f"{dt:.1f} s wall on {used} threads"}
+    # the native build computes the parity build's numbers (no fast-math, no contraction)
+    B0 = 64
+    _, _, o_nat = run(B0, 3, 1, R, 7)
+    cfg = O.default_config(num_envs=B0, action_repeats=R, initial_force=55.0, seed=7, autoreset=1)
+    e32 = O.Envs(cfg)
+    e32.reset()
+    rng = np.random.default_rng(7)
+    for _ in range(3):
+        o32 = e32.step(rng.integers(0, 5, (B0, 2)).astype(np.int8))[0]
+    same = bool(np.array_equal(o_nat, o32))
+
+    def sized(threads_, budget):
+        probe_b = 64 * threads_
+        dt, _, _ = run(probe_b, 10, threads_, R, SEED)
+        rate = probe_b * 10 / dt
+        steps = WINDOW + 1                  # one full episode incl. an in-step autoreset
+        B = int(min(65536, max(64, rate * budget / steps)))
+        B -= B % 64
+        dt, used, _ = run(max(B, 64), steps, threads_, R, SEED)
+        return {"value": round(max(B, 64) * steps / dt, 1), "cores": used,
+                "sample": f"{max(B, 64)} envs x {steps} steps ({dt:.1f} s)"}
+
+    omp = sized(threads, budget_s)
+    one = sized(1, budget_s / 2)
+    # C1: B = 1, R = 2 (reference default), discrete random actions, seeds 0..9, autoreset
+    c1_steps, c1_t = 0, 0.0
+    for seed in range(10):
+        dt, _, _ = run(1, 2 * WINDOW, 1, 2, seed)
+        c1_steps += 2 * WINDOW
+        c1_t += dt
+        if c1_t > budget_s / 2:
+            break
+    return {"value": omp["value"], "unit": "env-steps/s", "cores": omp["cores"], "kind": "port",
+            "sample": (f"oracle/cp_oracle.c fp32 built gcc -O3 -march=native (same algorithm; bit-identical "
+                       f"to the parity build: {same}), C3 workload (R={R}, discrete random actions, autoreset "
+                       f"incl.), OpenMP on {omp['cores']} threads: {omp['sample']}"),
+            "single_thread": {"value": one["value"], "unit": "env-steps/s", "cores": 1,
+                              "sample": "C3 workload, " + one["sample"]},
+            "c1_single_thread": {"value": round(c1_steps / c1_t, 1), "unit": "env-steps/s", "cores": 1,
+                                 "sample": f"C1: B=1, R=2, discrete random actions, seeds 0..{seed}, "
+                                           f"{c1_steps} steps incl. {c1_steps // WINDOW} resets ({c1_t:.1f} s)"},
+            "nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            "pybullet": "not importable (SURVEY.md §8c): the reference's own CPU path cannot be timed here"}
 
 
-def parity_check(device, R, B=512, steps=WINDOW):
-    """Checker leg (rank 0, N = 1, next to cpu_baseline): the second half of the metric,
-    max |pose - ref| over 200 steps.  pybullet is absent, so the refs are
-    the oracle's fp32 build (the kernel's bar: bit-exact) and its fp64 build (the
-    precision pybullet's double btScalar would compute the same algorithm in).  Same C3
-    config as the timed run (seed 1234, random discrete actions, autoreset), B envs,
-    `steps` steps from reset; obs = (R, 2, 7) cart + pole poses per repeat."""
+def _pose_diffs(g, o):
+    """per-step max over envs/repeats of |dpos| (xyz of cart + pole) and |dquat|."""
+    import numpy as np
+    d = np.abs(g.astype(np.float64) - o.astype(np.float64))
+    return float(d[..., 0:3].max()), float(d[..., 3:7].max())
+
+
+def parity_case(device, R, B, F, stream, steps, thr=None, seed=0, precision="f32"):
+    """One SURVEY §8d parity run: B envs from reset (seed, F_init = F), 200 steps of one
+    continuous action stream, GPU (precision) vs oracle f32 and f64; per step the max
+    |dpos| and |dquat|."""
     import numpy as np
 
-    from cartpoleplusplus_amd import abi
     from oracle import oracle as O
-    O.build()
     threads = max(1, min(16, len(os.sched_getaffinity(0))))
-    cfg = O.default_config(num_envs=B, action_repeats=R, initial_force=55.0, seed=1234, autoreset=1)
+    over = {} if thr is None else {"residual_threshold": thr}
+    cfg = O.default_config(num_envs=B, action_repeats=R, initial_force=float(F), seed=seed, autoreset=0)
+    for k, v in over.items():
+        setattr(cfg.phys, k, v)
     gpu = BatchedCartpole(B, device.index, config=abi.cp_config.from_buffer_copy(cfg))
     orc = {p: O.Envs(abi.cp_config.from_buffer_copy(cfg), precision=p) for p in ("f32", "f64")}
     g = gpu.reset().cpu().numpy()
     o = {p: e.reset() for p, e in orc.items()}
-    rng = np.random.default_rng(1234)
-    d64 = np.zeros((steps + 1, B))
-    d32 = np.abs(g - o["f32"]).reshape(B, -1).max(1)
-    d64[0] = np.abs(g.astype(np.float64) - o["f64"]).reshape(B, -1).max(1)
+    rng = np.random.default_rng(seed)
+    rows = {p: [_pose_diffs(g, o[p])] for p in orc}
     rew = np.zeros(B, np.float32)
     done = np.zeros(B, np.uint8)
     for t in range(steps):
-        a = rng.integers(0, 5, (B, 2)).astype(np.int8)
+        if stream == "zero":
+            a = np.zeros((B, 2, 2), np.float32)
+        elif stream == "constant":
+            a = np.broadcast_to(np.array([0.5, -0.25], np.float32), (B, 2, 2)).copy()
+        else:
+            a = rng.uniform(-1, 1, (B, 2, 2)).astype(np.float32)
         g = gpu.step(torch.from_numpy(a).to(device))[0].cpu().numpy()
         for p, e in orc.items():
             o[p] = np.zeros((B, R, 2, 7), np.float32)
-            e.step_omp(a, abi.CP_ACTION_DISCRETE, o[p], rew, done, threads)
-        d32 = np.maximum(d32, np.abs(g - o["f32"]).reshape(B, -1).max(1))
-        d64[t + 1] = np.abs(g.astype(np.float64) - o["f64"]).reshape(B, -1).max(1)
+            e.step_omp(a, abi.CP_ACTION_CONTINUOUS, o[p], rew, done, threads)
+            rows[p].append(_pose_diffs(g, o[p]))
     gpu.close()
-    per_env = d64.max(0)
-    return {"envs": B, "steps": steps, "workload": "C3 config (seed 1234, random discrete actions, autoreset)",
-            "max_abs_pose_diff_vs_oracle_f32": float(d32.max()), "bit_exact_vs_oracle_f32": bool(d32.max() == 0.0),
-            "max_abs_pose_drift_vs_oracle_f64": float(per_env.max()),
-            "median_env_max_drift_vs_oracle_f64": float(np.median(per_env)),
-            "max_drift_vs_oracle_f64_after_step": {str(k): float(d64[k].max()) for k in (1, 20, 100, steps)},
-            "vs_pybullet": None,
-            "note": "pybullet is not installed (parity with it unpinned); the fp64 column is the same algorithm in "
-                    "double precision: fp32 rounding differences grow through contact events (DESIGN.md §7)"}
+    out = {}
+    for p, r in rows.items():
+        r = np.array(r)   # (steps + 1, 2): step 0 = after reset
+        first = np.nonzero(r[:, 0] > 1e-4)[0]
+        out[p] = {"max_dpos": float(r[:, 0].max()), "max_dquat": float(r[:, 1].max()),
+                  "dpos_at_step": {str(k): float(r[k, 0]) for k in (0, 1, 20, 100, steps)},
+                  "dquat_at_step": {str(k): float(r[k, 1]) for k in (0, 1, 20, 100, steps)},
+                  "first_step_dpos_over_1e-4": int(first[0]) if len(first) else None}
+    return out
 
 
+def parity_c3(device, R, B=512, steps=WINDOW):
+    """The bench workload itself (C3: random discrete actions, autoreset, seed 1234): GPU vs
+    the fp32 oracle over 200 steps (the bit-exact bar)."""
+    import numpy as np
+
+    from oracle import oracle as O
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    cfg = O.default_config(num_envs=B, action_repeats=R, initial_force=55.0, seed=SEED, autoreset=1)
+    gpu = BatchedCartpole(B, device.index, config=abi.cp_config.from_buffer_copy(cfg))
+    orc = O.Envs(abi.cp_config.from_buffer_copy(cfg))
+    d = np.abs(gpu.reset().cpu().numpy() - orc.reset()).max()
+    acts = make_actions(False, B, 0, steps, SEED, device)
+    rew = np.zeros(B, np.float32)
+    done = np.zeros(B, np.uint8)
+    for t in range(steps):
+        g = gpu.step(acts[t])[0].cpu().numpy()
+        o = np.zeros((B, R, 2, 7), np.float32)
+        orc.step_omp(np.ascontiguousarray(acts[t].cpu().numpy()), abi.CP_ACTION_DISCRETE, o, rew, done, threads)
+        d = max(d, np.abs(g - o).max())
+    gpu.close()
+    return {"envs": B, "steps": steps, "max_abs_pose_diff": float(d), "bit_exact": bool(d == 0.0)}
+
+
+def parity_check(device, R, B=128, steps=WINDOW):
+    """SURVEY.md §8d's parity matrix: seed 0, F_init in {0, 55} x action streams {zero,
+    constant (0.5, -0.25), random U[-1,1]}, 200 steps from reset, |dpos| and |dquat|
+    separately, against the oracle's fp32 build (the kernel's bar: 0) and its fp64 build
+    (the same algorithm in double precision: what pybullet's double btScalar would compute
+    IF its algorithm is this one).  "early_exit": Bullet's stopping rule (max squared row
+    residual <= 1e-7); "fixed_sweeps": threshold 0, every substep runs all 50 sweeps, so
+    drift there is rounding alone, without the early exit's sweep-count jumps."""
+    matrix = {}
+    for variant, thr in (("early_exit", None), ("fixed_sweeps", 0.0)):
+        for F in (0, 55):
+            for stream in ("zero", "constant", "random"):
+                log(f"  parity {variant} F={F} {stream}")
+                matrix[f"{variant}/F{F}/{stream}"] = parity_case(device, R, B, F, stream, steps, thr)
+    worst32 = max(max(v["f32"]["max_dpos"], v["f32"]["max_dquat"]) for v in matrix.values())
+    return {"envs_per_case": B, "steps": steps, "repeats": R, "actions": "continuous (B,2,2)",
+            "bit_exact_vs_oracle_f32": worst32 == 0.0, "max_abs_diff_vs_oracle_f32": worst32,
+            "c3_workload_vs_oracle_f32": parity_c3(device, R),
+            "matrix": matrix, "vs_pybullet": None,
+            "note": "pybullet is not installed (parity with it unpinned, SURVEY.md §8c); f64 = the oracle's "
+                    "algorithm in double precision, state kept in double (DESIGN.md §7)"}
+
+
+# ----------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--batch", type=int, default=None, help="envs per GPU (default 65,536; 4,096 with --continuous)")
     ap.add_argument("--repeats", type=int, default=3)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--continuous", action="store_true", help="C2: continuous (B,2,2) U[-1,1] actions")
+    ap.add_argument("--dtype", choices=("f32",), default="f32")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the cpu_baseline and parity legs")
+    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-steady-state", action="store_true")
     ap.add_argument("--raster", action="store_true",
                     help="BASELINE.json configs[4] (C5): + in-kernel 50x50x3 fp16 raster obs per repeat")
     ap.add_argument("--cameras", type=int, default=1)
@@ -196,6 +414,8 @@ def main():
     ap.add_argument("--solver-iterations", type=int, default=None,
                     help="override the PGS sweep cap (default: the model's 50; non-default runs are diagnostics)")
     args = ap.parse_args()
+    if args.batch is None:
+        args.batch = 4096 if args.continuous else 65536
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -206,53 +426,54 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+    rccl_world = dist.get_world_size() if world > 1 else 1
 
     B, R, K, W = args.batch, args.repeats, args.steps, args.warmup
-    spec = shard_spec(B, rank, world, seed=1234 + rank)
-    env = BatchedCartpole(B, local, action_repeats=R, steps_per_repeat=1, max_episode_len=200,
+    spec = shard_spec(B, rank, world, seed=SEED)
+    env = BatchedCartpole(B, local, action_repeats=R, steps_per_repeat=1, max_episode_len=WINDOW,
                           initial_force=55.0, autoreset=True, seed=spec["seed"], done_on_bounds=args.done_on_bounds,
                           env_id_offset=spec["env_id_offset"],
                           **({} if args.solver_iterations is None else {"solver_iterations": args.solver_iterations}))
     if args.raster:
         env.enable_raster(True, num_cameras=args.cameras)
-    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
-    actions = torch.randint(0, 5, (W + K, B, 2), dtype=torch.int8, device=dev, generator=gen)
+    ss_steps = 0 if args.no_steady_state else WINDOW
+    actions = make_actions(args.continuous, B, spec["env_id_offset"], W + K + ss_steps, SEED, dev)
     env.reset()
     for t in range(W):
         env.step(actions[t])
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
     log(f"rank {rank}: B={B} R={R} warmup {W} done; timing {K} steps")
 
+    ep0 = episodes(env)
     env.timing_begin(K)
     env.timing_stride(STEP_EVENT_STRIDE, 1)
-    hist = None
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for t in range(K):
-        env.step(actions[W + t])
-        if (t + 1) % WINDOW == 0:
-            r, _ = env.episode_returns()
-            hist = return_histogram(gather_returns(r), 200)   # RCCL all-gather when world > 1
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed, hist, gathers = timed(env, actions, W, K, world, dev, gather_at_end=world > 1)
     tm = env.timing_end()
-    el = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
+    resets = int((episodes(env) - ep0).sum().item())
 
+    steady = None
+    if ss_steps:
+        ep1 = episodes(env)
+        el2, hist2, g2 = timed(env, actions, W + K, ss_steps, world, dev, gather_at_end=world > 1)
+        r2 = torch.tensor([int((episodes(env) - ep1).sum().item())], device=dev, dtype=torch.int64)
+        if world > 1:
+            dist.all_reduce(r2)
+        steady = {"steps": ss_steps, "ms_per_step": round(el2 / ss_steps * 1e3, 4),
+                  "value": round(world * B * ss_steps / el2, 1), "resets": int(r2.item()), "collectives": g2,
+                  "note": "one full 200-step episode cycle (its autoreset burst included) right after the timed "
+                          "window, timed the same way"}
+        hist = hist2 if hist2 is not None else hist
+
+    rt = torch.tensor([resets], device=dev, dtype=torch.int64)
+    if world > 1:
+        dist.all_reduce(rt)
     value = world * B * K / elapsed
+    kind = "continuous" if args.continuous else "discrete"
     per_launch_s = tm["step_ms"] / max(1, tm["step_launches"]) / 1e3
-    bytes_launch = B * step_kernel_bytes(R, 2)
+    bytes_launch = B * step_kernel_bytes(R, 16 if args.continuous else 2)
     achieved = bytes_launch / per_launch_s / 1e9
-    kernel = "cp_step_kernel<discrete>"
-    traffic, traffic_src = pmc_traffic(kernel, B, R)
+    kernel = f"cp_step_kernel<{kind}>"
+    traffic, traffic_src = pmc_traffic(kernel, B, R, kind)
     if args.raster:
         # C5: the render kernel writes 2.9 GB per step and is the dominant HBM consumer
         rc = env.raster_cfg
@@ -260,16 +481,17 @@ def main():
         bytes_launch = B * render_kernel_bytes(rc.height, rc.width, rc.num_cameras, R)
         achieved = bytes_launch / per_launch_s / 1e9
         kernel = "cp_render_small_kernel"
-        traffic, traffic_src = pmc_traffic(kernel, B, R)
+        traffic, traffic_src = pmc_traffic(kernel, B, R, kind)
     valu = None
     if not args.raster:
-        vi, vsrc = pmc_valu(kernel, B, R)
+        vi, vsrc = pmc_valu(kernel, B, R, kind)
         if vi is not None:
             ach = vi / per_launch_s
             valu = {"bound": "valu-issue (secondary; the kernel is latency-bound, DESIGN.md §5)",
                     "wave_instructions_per_launch": vi, "achieved": round(ach / 1e12, 4),
                     "peak": round(VALU_PEAK_WINST_PER_S / 1e12, 4), "unit": "T wave-instr/s",
                     "frac": round(ach / VALU_PEAK_WINST_PER_S, 4), "source": vsrc + " SQ_INSTS_VALU"}
+    name, wl = workload(args, world)
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -281,17 +503,18 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic (random discrete actions, Philox bump pushes; no pybullet, see DESIGN.md)",
-        "config": {"workload": ("C5: batch=65,536 envs/GPU, discrete 5-action, R=3, S=1, autoreset at 200, "
-                                "initial_force=55, fp32 physics + in-kernel raster obs 50x50x3xR fp16 to HBM "
-                                f"({args.cameras} camera(s); BASELINE.json configs[4])") if args.raster else
-                               ("C3: batch=65,536 envs/GPU, discrete 5-action, R=3, S=1, autoreset at 200, "
-                                "initial_force=55, fp32 (BASELINE.json configs[2]; N>1 = C4 with RCCL all-gather "
-                                "of episode returns per 200-step window)"),
-                   "global_batch": world * B, "envs_per_gpu": B, "action_repeats": R, "steps_per_repeat": 1,
+        "dtype": args.dtype,
+        "data": "synthetic (hashed random actions keyed by global env id, Philox bump pushes; no pybullet, "
+                "see DESIGN.md)",
+        "config": {"workload": wl, "name": name, "global_batch": world * B, "envs_per_gpu": B, "action_repeats": R,
+                   "steps_per_repeat": 1, "action_kind": kind, "step_kernel_shape": step_shape(B),
                    "parallelism": f"dp{world} (independent env shards, no per-step collective)",
-                   "solver_iterations": env.cfg.phys.solver_iterations},
+                   "solver_iterations": env.cfg.phys.solver_iterations,
+                   "residual_threshold": env.cfg.phys.residual_threshold},
+        "resets_in_window": int(rt.item()),
+        "collectives_in_window": gathers if world > 1 else 0,
+        "rccl_world_size": rccl_world,
+        "steady_state": steady,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                      "traffic_source": traffic_src and (traffic_src + " (2*FETCH_SIZE + WRITE_SIZE) KiB*1024 "
@@ -308,11 +531,14 @@ def main():
         "episode_return_hist_nonzero": None if hist is None else int((hist > 0).sum().item()),
         "done_on_bounds": bool(args.done_on_bounds),
     }
+    env.close()
+    del actions
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
         out["cpu_baseline"] = cpu_baseline(R, args.cpu_seconds)
-        log("parity vs oracle ...")
-        out["parity"] = parity_check(dev, R)
+        if not args.no_parity:
+            log("parity vs oracle ...")
+            out["parity"] = parity_check(dev, R)
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:

@@ -164,3 +164,14 @@ class cp_replay(C.Structure):
 class cp_replay_batch(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ("idx", "state_1", "action", "reward", "terminal_mask", "state_2",
                                           "state_1_idx", "state_2_idx")]
+
+
+def state_ints(values):
+    """Integer state fields (steps, episode, done, warm-start ids) from a state array:
+    float32 holds the int32 bits; a float64 state (fp64 build) holds them in the first 4
+    bytes (the low word on this little-endian ABI) of each 8-byte field."""
+    import numpy as np
+    a = np.ascontiguousarray(values)
+    if a.dtype == np.float64:
+        return a.view(np.int32)[..., 0::2]
+    return a.view(np.int32)

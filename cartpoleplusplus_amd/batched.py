@@ -20,6 +20,25 @@ def _ptr(t):
     return None if t is None else C.c_void_p(t.data_ptr())
 
 
+def _device_buffer(x, shape, dtype, device, name):
+    """x as a contiguous tensor of exactly `shape` / `dtype` on `device`, or ValueError.
+    The C-ABI trusts these sizes (it reads B rows through raw device pointers), so they
+    are checked here, explicitly (not with assert, which python -O strips)."""
+    t = x if isinstance(x, torch.Tensor) else torch.as_tensor(x)
+    if t.dtype != dtype:
+        if t.is_floating_point() != dtype.is_floating_point and dtype != torch.uint8:
+            raise ValueError(f"{name}: dtype {t.dtype} cannot stand for {dtype}")
+        t = t.to(dtype)
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: expected shape {tuple(shape)}, got {tuple(t.shape)}")
+    if t.device != device:
+        t = t.to(device)
+    t = t.contiguous()
+    if t.numel() != int(torch.Size(shape).numel()):
+        raise ValueError(f"{name}: {t.numel()} elements, expected {torch.Size(shape).numel()}")
+    return t
+
+
 class BatchedCartpole:
     def __init__(self, num_envs, device=0, *, action_repeats=2, steps_per_repeat=1, max_episode_len=200,
                  action_force=50.0, initial_force=200.0, random_theta=True, done_on_bounds=False,
@@ -35,7 +54,11 @@ class BatchedCartpole:
                 autoreset=int(bool(autoreset)), seed=int(seed), env_id_offset=int(env_id_offset),
                 bump_mode=abi.CP_BUMP_HOST if bump_mode == "host" else abi.CP_BUMP_PHILOX)
             for k, v in phys.items():
+                if not hasattr(config.phys, k):
+                    raise ValueError(f"unknown physics parameter {k!r}")
                 setattr(config.phys, k, v)
+            if "dt" in phys and "inv_dt" not in phys:  # both are used by the kernels (cp_create checks)
+                config.phys.inv_dt = 1.0 / float(phys["dt"])
         self.cfg = config
         self.B, self.R, self.S = config.num_envs, config.action_repeats, config.steps_per_repeat
         self.discrete_actions = bool(discrete_actions)
@@ -73,25 +96,24 @@ class BatchedCartpole:
         """Reset envs (all, or where mask != 0); returns the obs tensor (B,R,2,7)."""
         m = None
         if mask is not None:
-            m = torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
-            assert m.numel() == self.B
+            m = _device_buffer(torch.as_tensor(mask, device=self.device).reshape(-1).to(torch.uint8), (self.B,),
+                               torch.uint8, self.device, "reset mask")
         native.check(self.h, self.lib.cp_reset(self.h, _ptr(m), _ptr(self.obs), self._stream()), "cp_reset")
         return self.obs
 
     def step(self, actions):
         """One env-step for all envs.  actions: (B,2,2) float32 in [-1,1] (continuous,
         bullet_cartpole.py:201-207) or (B,2) int8 indices into abi.DISCRETE_TABLE."""
+        if not isinstance(actions, torch.Tensor):
+            actions = torch.as_tensor(actions)
         if actions.dtype == torch.int8:
             kind = abi.CP_ACTION_DISCRETE
-            assert actions.shape == (self.B, 2), actions.shape
+            actions = _device_buffer(actions, (self.B, 2), torch.int8, self.device, "discrete actions")
         else:
             kind = abi.CP_ACTION_CONTINUOUS
-            if actions.dtype != torch.float32:
-                actions = actions.float()
-            assert actions.shape == (self.B, 2, 2), actions.shape
-        if actions.device != self.device:
-            actions = actions.to(self.device)
-        actions = actions.contiguous()
+            if not actions.is_floating_point():
+                raise ValueError(f"actions: int8 indices (B, 2) or float (B, 2, 2), got {actions.dtype}")
+            actions = _device_buffer(actions, (self.B, 2, 2), torch.float32, self.device, "continuous actions")
         native.check(self.h, self.lib.cp_step(self.h, _ptr(actions), kind, _ptr(self.obs), _ptr(self.reward),
                                               _ptr(self.done), _ptr(self.terminal_obs), self._stream()),
                      "cp_step")
@@ -133,8 +155,8 @@ class BatchedCartpole:
             self.lqr_gains = self.state8 = None
             native.check(self.h, self.lib.cp_set_lqr(self.h, None, 0, None, 0.0, 0.0), "cp_set_lqr")
             return
-        g = torch.as_tensor(gains, dtype=torch.float32, device=self.device).contiguous()
-        assert g.shape == ((self.B,) if per_env else ()) + (2, 2, 8), g.shape
+        g = _device_buffer(torch.as_tensor(gains, dtype=torch.float32), ((self.B,) if per_env else ()) + (2, 2, 8),
+                           torch.float32, self.device, "LQR gains")
         self.lqr_gains = g
         self.state8 = torch.zeros((self.B, self.R, self.S, 2, 8), device=self.device) if state8 else None
         native.check(self.h, self.lib.cp_set_lqr(self.h, _ptr(g), int(bool(per_env)), _ptr(self.state8),
@@ -142,8 +164,8 @@ class BatchedCartpole:
 
     def set_bump_forces(self, forces):
         """Parity mode (bump_mode='host'): LINK-frame bump forces (B, 30, 2, 2)."""
-        f = torch.as_tensor(forces, dtype=torch.float32, device=self.device).contiguous()
-        assert f.shape == (self.B, self.cfg.initial_force_steps, 2, 2), f.shape
+        f = _device_buffer(torch.as_tensor(forces, dtype=torch.float32), (self.B, self.cfg.initial_force_steps, 2, 2),
+                           torch.float32, self.device, "bump forces")
         native.check(self.h, self.lib.cp_set_bump_forces(self.h, _ptr(f), self._stream()), "cp_set_bump_forces")
 
     def get_state(self):
@@ -152,8 +174,8 @@ class BatchedCartpole:
         return s
 
     def set_state(self, s):
-        s = torch.as_tensor(s, dtype=torch.float32, device=self.device).contiguous()
-        assert s.shape == (abi.CP_STATE_FIELDS, self.B)
+        s = _device_buffer(torch.as_tensor(s, dtype=torch.float32), (abi.CP_STATE_FIELDS, self.B), torch.float32,
+                           self.device, "state")
         native.check(self.h, self.lib.cp_set_state(self.h, _ptr(s), self._stream()), "cp_set_state")
 
     def episode_returns(self):

@@ -709,6 +709,13 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     if (cfg->initial_force_steps < 0 || cfg->settle_steps < 0)
         return fail(nullptr, "cp_create: negative step counts");
     if (cfg->phys.solver_iterations < 0) return fail(nullptr, "cp_create: negative solver_iterations");
+    // host-computed derived fields must agree with their sources (the kernels use both)
+    if (!(cfg->phys.dt > 0.0f) || std::fabs((double)cfg->phys.dt * (double)cfg->phys.inv_dt - 1.0) > 1e-6)
+        return fail(nullptr, "cp_create: phys.inv_dt must be 1 / phys.dt (recompute it when dt changes)");
+    if (std::fabs((double)cfg->tan_angle_threshold - std::tan((double)cfg->angle_threshold)) > 1e-6 ||
+        std::fabs((double)cfg->sin_angle_threshold - std::sin((double)cfg->angle_threshold)) > 1e-6)
+        return fail(nullptr, "cp_create: tan/sin_angle_threshold must be tan/sin(angle_threshold)");
+    if (!(cfg->phys.residual_threshold >= 0.0f)) return fail(nullptr, "cp_create: negative residual_threshold");
     if ((unsigned long long)cfg->num_envs * CP_STATE_FIELDS * 4ull >= (1ull << 32) ||
         (unsigned long long)cfg->num_envs * cfg->action_repeats * 14ull * 4ull >= (1ull << 32))
         return fail(nullptr, "cp_create: num_envs too large for one handle (SoA arrays must stay below 4 GiB)");

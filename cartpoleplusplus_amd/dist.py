@@ -1,10 +1,14 @@
 """Data-parallel sharding of independent envs across ranks (one process per GPU).
 
 Envs never interact, so a batch of N*B envs runs as N independent shards with no
-per-step communication.  Rank r owns global env ids [r*B, (r+1)*B): the id keys the
-Philox bump stream, so the sharded job reproduces the unsharded one exactly.  The
-only collective is the gather of per-env episode returns once per reporting window
-(RCCL over xGMI with backend "nccl"; gloo on CPU in tests).
+per-step communication.  Rank r owns global env ids [r*B, (r+1)*B).  The seed rule:
+every rank uses the SAME seed (the Philox key); the global env id is the Philox
+counter's env word, so rank r's envs draw exactly the bump pushes envs r*B.. of one
+unsharded N*B-env run draw, and a sharded job given the same per-env actions
+reproduces the unsharded one bit for bit (tests/test_dist.py on the oracle,
+tests/test_gpu_shard.py on the HIP path).  bench.py keys its synthetic actions by
+global env id as well.  The only collective is the gather of per-env episode returns
+once per reporting window (RCCL over xGMI with backend "nccl"; gloo on CPU in tests).
 """
 import torch
 import torch.distributed as dist

@@ -111,6 +111,8 @@ class ReplayMemory:
         x = x.to(self.device)
         if x.dtype not in (torch.float16, torch.float32):
             x = x.float()
+        if x.numel() != rows * self.state_dim:
+            raise ValueError(f"states: {x.numel()} values for {rows} rows x state_dim {self.state_dim}")
         x = x.reshape(rows, self.state_dim).contiguous()
         return x, (abi.CP_STATES_F16 if x.dtype == torch.float16 else abi.CP_STATES_F32)
 
@@ -220,8 +222,7 @@ class ReplayMemory:
         """Envs (all, or mask != 0) start an episode at states[j] (B, *state_shape)."""
         B = self.num_envs
         x, kind = self._states(states, B)
-        m = torch.ones(B, dtype=torch.uint8, device=self.device) if mask is None else \
-            torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
+        m = torch.ones(B, dtype=torch.uint8, device=self.device) if mask is None else self._rows_u8(mask, B, "mask")
         self._add(B, 0, None, None, abi.CP_ACTION_CONTINUOUS, None, None, m, x, None, kind)
 
     def add_steps(self, actions, reward, done, next_states, terminal_states=None, valid=None, restart=None):
@@ -232,16 +233,28 @@ class ReplayMemory:
         actions = actions.to(dev)
         if kind == abi.CP_ACTION_CONTINUOUS:
             actions = actions.float()
+        if actions.numel() != B * self.action_dim:
+            raise ValueError(f"actions: {actions.numel()} values for {B} rows x action_dim {self.action_dim}")
         actions = actions.reshape(B, self.action_dim).contiguous()
         x, skind = self._states(next_states, B)
         t = None
         if terminal_states is not None:
             t, tkind = self._states(terminal_states, B)
-            assert tkind == skind
-        u8 = lambda v: None if v is None else torch.as_tensor(v, device=dev).to(torch.uint8).contiguous()  # noqa: E731
-        valid = torch.ones(B, dtype=torch.uint8, device=dev) if valid is None else u8(valid)
-        self._add(B, 0, valid, actions, kind, reward.to(dev).float().contiguous(), u8(done), u8(restart), x, t,
-                  skind)
+            if tkind != skind:
+                raise ValueError("terminal_states and next_states must have the same dtype")
+        u8 = lambda v, name: None if v is None else self._rows_u8(v, B, name)  # noqa: E731
+        valid = torch.ones(B, dtype=torch.uint8, device=dev) if valid is None else u8(valid, "valid")
+        reward = torch.as_tensor(reward, device=dev).float().reshape(-1).contiguous()
+        if reward.numel() != B:
+            raise ValueError(f"reward: {reward.numel()} values for {B} rows")
+        self._add(B, 0, valid, actions, kind, reward, u8(done, "done"), u8(restart, "restart"), x, t, skind)
+
+    def _rows_u8(self, v, rows, name):
+        """(rows,) uint8 device mask; the C-ABI reads `rows` bytes through the pointer."""
+        t = torch.as_tensor(v, device=self.device).to(torch.uint8).reshape(-1).contiguous()
+        if t.numel() != rows:
+            raise ValueError(f"{name}: {t.numel()} values for {rows} rows")
+        return t
 
     # ----------------------------------------------- BatchedCartpole feed
     def _env_states(self, env):
@@ -255,13 +268,15 @@ class ReplayMemory:
 
     def after_reset(self, env, mask=None):
         """After env.reset(mask): those envs start new episodes."""
-        assert env.B == self.num_envs
+        if env.B != self.num_envs:
+            raise ValueError(f"env has {env.B} envs, the replay memory {self.num_envs} rows")
         self.begin_episodes(self._env_states(env)[0], mask)
 
     def after_step(self, env, actions):
         """After env.step(actions): one event per simulated env (the done-before envs of a
         non-autoreset env are skipped); autoreset envs also start their next episode."""
-        assert env.B == self.num_envs
+        if env.B != self.num_envs:
+            raise ValueError(f"env has {env.B} envs, the replay memory {self.num_envs} rows")
         native.check(env.h, self.lib.cp_get_stepped(env.h, _p(self._stepped), env._stream()), "cp_get_stepped")
         nxt, term = self._env_states(env)
         restart = env.done if env.cfg.autoreset else None

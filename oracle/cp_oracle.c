@@ -1019,7 +1019,7 @@ void orc_world_get_euler(const orc_world* w, int body, double out3[3]) {
 }
 
 /* -------------------------------------------------------------- env-level API */
-#define SF(e, f, i) ((e)->state[(size_t)(f) * (e)->B + (i)])
+#define SF(e, f, i) (((real*)(e)->state)[(size_t)(f) * (e)->B + (i)])
 
 static void env_load(const orc_envs* e, int i, sim_t* S) {
     for (int d = 0; d < CP_NUM_DYN; ++d) {
@@ -1039,26 +1039,26 @@ static void env_load(const orc_envs* e, int i, sim_t* S) {
 }
 static void env_store(orc_envs* e, int i, const sim_t* S) {
     for (int d = 0; d < CP_NUM_DYN; ++d) {
-        SF(e, CP_SF_BODY(d, 0), i) = (float)S->x[d].x;
-        SF(e, CP_SF_BODY(d, 1), i) = (float)S->x[d].y;
-        SF(e, CP_SF_BODY(d, 2), i) = (float)S->x[d].z;
-        for (int k = 0; k < 4; ++k) SF(e, CP_SF_BODY(d, 3 + k), i) = (float)S->q[d][k];
-        SF(e, CP_SF_BODY(d, 7), i) = (float)S->v[d].x;
-        SF(e, CP_SF_BODY(d, 8), i) = (float)S->v[d].y;
-        SF(e, CP_SF_BODY(d, 9), i) = (float)S->v[d].z;
-        SF(e, CP_SF_BODY(d, 10), i) = (float)S->w[d].x;
-        SF(e, CP_SF_BODY(d, 11), i) = (float)S->w[d].y;
-        SF(e, CP_SF_BODY(d, 12), i) = (float)S->w[d].z;
+        SF(e, CP_SF_BODY(d, 0), i) = S->x[d].x;
+        SF(e, CP_SF_BODY(d, 1), i) = S->x[d].y;
+        SF(e, CP_SF_BODY(d, 2), i) = S->x[d].z;
+        for (int k = 0; k < 4; ++k) SF(e, CP_SF_BODY(d, 3 + k), i) = S->q[d][k];
+        SF(e, CP_SF_BODY(d, 7), i) = S->v[d].x;
+        SF(e, CP_SF_BODY(d, 8), i) = S->v[d].y;
+        SF(e, CP_SF_BODY(d, 9), i) = S->v[d].z;
+        SF(e, CP_SF_BODY(d, 10), i) = S->w[d].x;
+        SF(e, CP_SF_BODY(d, 11), i) = S->w[d].y;
+        SF(e, CP_SF_BODY(d, 12), i) = S->w[d].z;
     }
     for (int c = 0; c < 2; ++c) {
-        SF(e, CP_SF_PENDING(c, 0), i) = (float)S->f[2 * c].x;
-        SF(e, CP_SF_PENDING(c, 1), i) = (float)S->f[2 * c].y;
-        SF(e, CP_SF_PENDING(c, 2), i) = (float)S->f[2 * c].z;
+        SF(e, CP_SF_PENDING(c, 0), i) = S->f[2 * c].x;
+        SF(e, CP_SF_PENDING(c, 1), i) = S->f[2 * c].y;
+        SF(e, CP_SF_PENDING(c, 2), i) = S->f[2 * c].z;
     }
     for (int p = 0; p < CP_NUM_ISLANDS; ++p)
         for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
             memcpy(&SF(e, CP_SF_WS_ID(p, j), i), &S->ws_id[p][j], 4);
-            for (int k = 0; k < 4; ++k) SF(e, CP_SF_WS_LAM(p, j, k), i) = (float)S->ws_lam[p][j][k];
+            for (int k = 0; k < 4; ++k) SF(e, CP_SF_WS_LAM(p, j, k), i) = S->ws_lam[p][j][k];
         }
 }
 static int32_t get_i(const orc_envs* e, int f, int i) {
@@ -1084,7 +1084,7 @@ int orc_envs_create(const cp_config* cfg, orc_envs** out) {
     e->B = cfg->num_envs;
     size_t B = (size_t)e->B;
     int R = cfg->action_repeats;
-    e->state = (float*)calloc((size_t)CP_STATE_FIELDS * B, sizeof(float));
+    e->state = calloc((size_t)CP_STATE_FIELDS * B, sizeof(real));
     e->term_obs = (float*)calloc((size_t)R * 14 * B, sizeof(float));
     e->bump_forces = (float*)calloc(B * (size_t)cfg->initial_force_steps * 4, sizeof(float));
     e->ret_acc = (float*)calloc(B, sizeof(float));
@@ -1115,11 +1115,11 @@ void orc_envs_destroy(orc_envs* e) {
 void orc_envs_set_bump_forces(orc_envs* e, const float* f) {
     memcpy(e->bump_forces, f, (size_t)e->B * e->cfg.initial_force_steps * 4 * sizeof(float));
 }
-void orc_envs_get_state(const orc_envs* e, float* out) {
-    memcpy(out, e->state, (size_t)CP_STATE_FIELDS * e->B * sizeof(float));
+void orc_envs_get_state(const orc_envs* e, void* out) {
+    memcpy(out, e->state, (size_t)CP_STATE_FIELDS * e->B * sizeof(real));
 }
-void orc_envs_set_state(orc_envs* e, const float* in) {
-    memcpy(e->state, in, (size_t)CP_STATE_FIELDS * e->B * sizeof(float));
+void orc_envs_set_state(orc_envs* e, const void* in) {
+    memcpy(e->state, in, (size_t)CP_STATE_FIELDS * e->B * sizeof(real));
 }
 
 /* bump force k (0..initial_force_steps-1) on cart c (0: cart, 1: cart2), LINK frame */

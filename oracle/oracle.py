@@ -45,10 +45,22 @@ _LIBS = {}
 
 
 def load(precision="f32"):
-    name = "libcp_oracle.so" if precision == "f32" else "libcp_oracle_f64.so"
-    if name in _LIBS:
-        return _LIBS[name]
-    path = os.environ.get("ORC_LIB_OVERRIDE") or os.path.join(BUILD, name)
+    """precision: "f32" (parity build), "f64", or "native" (fp32, -O3 -march=native: the
+    CPU-baseline build of bench.py, same results as "f32")."""
+    if precision == "native":
+        name = native_path()
+        if name in _LIBS:
+            return _LIBS[name]
+        path = name
+        if not os.path.exists(path):
+            out = subprocess.run(["make", "-C", HERE, "native", f"NATIVE_OUT={path}"], capture_output=True, text=True)
+            if out.returncode != 0:
+                raise RuntimeError("native oracle build failed:\n" + out.stdout + out.stderr)
+    else:
+        name = {"f32": "libcp_oracle.so", "f64": "libcp_oracle_f64.so"}[precision]
+        if name in _LIBS:
+            return _LIBS[name]
+        path = os.environ.get("ORC_LIB_OVERRIDE") or os.path.join(BUILD, name)
     if not os.path.exists(path):
         build()
     lib = C.CDLL(path)
@@ -85,6 +97,22 @@ def load(precision="f32"):
         f.restype, f.argtypes = res, args
     _LIBS[name] = lib
     return lib
+
+
+def native_path():
+    """Where the -march=native build for THIS host's CPU lives (keyed by the CPU model and
+    flags, so a tree copied to another machine rebuilds instead of running foreign code)."""
+    import hashlib
+    import platform
+    key = platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            lines = [ln for ln in f if ln.startswith(("model name", "flags"))][:2]
+        key += "".join(lines)
+    except OSError:
+        pass
+    tag = hashlib.sha1(key.encode()).hexdigest()[:12]
+    return os.path.join(BUILD, f"native_{tag}", "libcp_oracle_native.so")
 
 
 def default_config(**overrides):
@@ -184,13 +212,25 @@ class Envs:
         self.lib.orc_envs_set_lqr(self.h, _ptr(self._gains), int(bool(per_env)), _ptr(self.state8),
                                   float(done_pos), float(done_angle))
 
+    @property
+    def real(self):
+        """numpy dtype of the state (float32, or float64 for the fp64 build)."""
+        return np.float64 if self.lib.orc_sizeof_real() == 8 else np.float32
+
     def get_state(self):
-        s = np.empty((abi.CP_STATE_FIELDS, self.B), np.float32)
+        """State SoA (CP_STATE_FIELDS, B) in the build's real type; integer fields hold
+        int32 bits in their first 4 bytes (read them with abi.state_ints)."""
+        s = np.empty((abi.CP_STATE_FIELDS, self.B), self.real)
         self.lib.orc_envs_get_state(self.h, _ptr(s))
         return s
 
     def set_state(self, s):
-        s = np.ascontiguousarray(s, dtype=np.float32)
+        s = np.asarray(s)
+        if s.dtype != self.real:
+            raise ValueError(f"state dtype {s.dtype}, this oracle build keeps {np.dtype(self.real)}")
+        s = np.ascontiguousarray(s)
+        if s.shape != (abi.CP_STATE_FIELDS, self.B):
+            raise ValueError(f"state shape {s.shape}")
         self.lib.orc_envs_set_state(self.h, _ptr(s))
 
     def reset(self, mask=None, obs=None):

@@ -1,0 +1,69 @@
+"""Diagnostic: PGS sweep counts per solve under the model's stopping rule.
+
+Builds the ORC_STATS variant of the CPU oracle (test infrastructure) into /tmp, runs the bench
+workload (C3: random discrete actions, R = 3, autoreset) on B envs, and records every solve
+(one per env and substep: the two islands are one solver group).  Reports the sweep
+distribution, the rate of solves that reach the sweep cap, and what a 64-lane wave (32 envs)
+pays: the max over its envs, per substep.
+
+usage: python tools/sweep_stats.py [--envs 4096] [--warmup 60] [--steps 40] [--threshold 1e-7]
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--warmup", type=int, default=60)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--threshold", type=float, default=None)
+    args = ap.parse_args()
+    from row_classes import build_stats_oracle
+    os.environ["ORC_LIB_OVERRIDE"] = build_stats_oracle()
+    from cartpoleplusplus_amd import abi
+    from oracle import oracle as O
+
+    B, R = args.envs, 3
+    cfg = O.default_config(num_envs=B, action_repeats=R, initial_force=55.0, seed=1234, autoreset=1)
+    if args.threshold is not None:
+        cfg.phys.residual_threshold = args.threshold
+    env = O.Envs(abi.cp_config.from_buffer_copy(cfg))
+    lib = env.lib
+    lib.orc_stats_open.argtypes = [C.c_char_p]
+    env.reset()
+    rng = np.random.default_rng(1234)
+    for _ in range(args.warmup):
+        env.step(rng.integers(0, 5, (B, 2)).astype(np.int8))
+    path = "/tmp/sweep_stats.txt"
+    lib.orc_stats_open(path.encode())
+    for _ in range(args.steps):
+        env.step(rng.integers(0, 5, (B, 2)).astype(np.int8))
+    lib.orc_stats_open(None)
+    rows = np.loadtxt(path, dtype=np.int64)
+    # two lines per solve (island 0, island 1; same sweep count); env-major, then substep
+    its = rows[0::2, 11]
+    cap = cfg.phys.solver_iterations
+    per_env = its.reshape(B, -1)                    # (B, steps * R) solves
+    waves = per_env.reshape(B // 32, 32, -1).max(1)  # what each 64-lane wave pays
+    out = {"envs": B, "warmup_steps": args.warmup, "recorded_steps": args.steps,
+           "residual_threshold": cfg.phys.residual_threshold, "sweep_cap": cap,
+           "solves": int(its.size), "mean_sweeps": float(its.mean()), "median_sweeps": float(np.median(its)),
+           "p90_sweeps": float(np.percentile(its, 90)), "capped_fraction": float((its >= cap).mean()),
+           "wave_mean_sweeps": float(waves.mean()), "wave_capped_fraction": float((waves >= cap).mean()),
+           "no_rows_fraction": float((its == 0).mean()),
+           "histogram": {str(k): int(v) for k, v in zip(*np.unique(its, return_counts=True))}}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
