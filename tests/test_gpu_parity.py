@@ -163,9 +163,13 @@ def test_state_roundtrip_into_oracle(oracle_mod):
 
 
 def test_full_size_bench_config_subset_parity_and_properties(oracle_mod):
-    """B = 65,536, discrete, R = 3, autoreset (BASELINE config 3): a random subset of
-    envs is re-simulated on the oracle from the GPU state; the whole batch is checked
-    for finiteness, unit quaternions and run-to-run determinism."""
+    """B = 65,536, discrete, R = 3, autoreset (BASELINE config 3): the whole batch is checked
+    for finiteness, unit quaternions and run-to-run determinism; then every env's step
+    counter is set to 198 (cp_set_state), so the second step after that ends all 65,536
+    episodes at once (bullet_cartpole.py:255-257) and the burst runs through the step
+    kernel's ballot-compacted reset list and the throughput-shaped reset kernel.  Four
+    blocks of 128 envs (env ids keep the Philox bump streams) are re-simulated on the oracle
+    from the GPU state across the burst: obs, terminal obs, done, bit for bit."""
     B = 65536
     cfg = native.default_config(num_envs=B, action_repeats=3, initial_force=55.0, seed=1234, autoreset=1)
     g1 = BatchedCartpole(B, 0, config=abi.cp_config.from_buffer_copy(cfg))
@@ -181,20 +185,32 @@ def test_full_size_bench_config_subset_parity_and_properties(oracle_mod):
     assert torch.isfinite(o1).all()
     q = o1[..., 3:7].double()
     assert torch.allclose(q.norm(dim=-1), torch.ones_like(q[..., 0]), atol=1e-5)
-    # subset parity: oracle restarted from the GPU state of 512 envs
     st = _np(g1.get_state())
-    idx = np.sort(np.random.default_rng(0).choice(B, 512, replace=False))
-    sub = abi.cp_config.from_buffer_copy(cfg)
-    sub.num_envs = 512
-    orc = oracle_mod.Envs(sub)
-    orc.set_state(np.ascontiguousarray(st[:, idx]))
+    st.view(np.int32)[abi.CP_SF_STEPS] = 198
+    g1.set_state(torch.from_numpy(st).cuda())
+    blocks = [0, 20000, 40960, B - 128]
+    orcs = []
+    for lo in blocks:
+        sub = abi.cp_config.from_buffer_copy(cfg)
+        sub.num_envs, sub.env_id_offset = 128, lo
+        orc = oracle_mod.Envs(sub)
+        orc.set_state(np.ascontiguousarray(st[:, lo:lo + 128]))
+        orcs.append(orc)
     rng = np.random.default_rng(9)
-    for t in range(8):
+    for t in range(5):
         a = rng.integers(0, 5, (B, 2)).astype(np.int8)
         go, gr, gd = g1.step(torch.from_numpy(a).cuda())
-        oo, orw, od = orc.step(np.ascontiguousarray(a[idx]))
-        _assert_same(_np(go)[idx], oo, f"subset obs {t}")
-        _assert_same(_np(gd)[idx], od, f"subset done {t}")
+        go, gd, gt = _np(go), _np(gd), _np(g1.terminal_obs)
+        if t == 1:
+            assert gd.all(), "every episode ends at step 200"
+        for lo, orc in zip(blocks, orcs):
+            oo, orw, od, ot = orc.step(np.ascontiguousarray(a[lo:lo + 128]), terminal=True)
+            _assert_same(go[lo:lo + 128], oo, f"block {lo} obs {t}")
+            _assert_same(gd[lo:lo + 128], od, f"block {lo} done {t}")
+            if t == 1:
+                _assert_same(gt[lo:lo + 128], ot, f"block {lo} terminal obs")
+    eps = _np(g1.get_state()).view(np.int32)[abi.CP_SF_EPISODE]
+    assert (eps == 2).all()                                     # reset once, auto-reset once
 
 
 def test_gym_mirror_matches_oracle_and_reference_errors(oracle_mod):

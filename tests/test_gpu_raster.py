@@ -126,3 +126,25 @@ def test_gym_mirror_raw_pixels():
     assert 0.0 <= s.min() and s.max() <= 1.0
     s2, r, d, _ = env.step([1, 2])
     assert s2.shape == s.shape and r == 1.0 and not d
+
+
+def test_full_size_c5_properties_and_subset(oracle_mod):
+    """C5 at its full size (B = 65,536, 50 x 50 x 3, 1 camera, R = 3: 2.95 GB of float16
+    frames per step, the throughput-shaped step kernel and the one-block-per-env render
+    kernel): every pixel finite and in [0, 1]; the last repeat's frame of 48 envs spread
+    over the batch bit-exact against the oracle's ray caster."""
+    B = 65536
+    env = BatchedCartpole(B, 0, action_repeats=3, initial_force=55.0, seed=1234, autoreset=True)
+    env.enable_raster(True)
+    env.reset()
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    for _ in range(3):
+        env.step(torch.randint(0, 5, (B, 2), device="cuda", generator=gen, dtype=torch.int8))
+    px = env.pixels
+    assert px.shape == (B, 50, 50, 3, 1, 3) and px.dtype == torch.float16
+    assert bool(torch.isfinite(px).all()) and float(px.min()) >= 0.0 and float(px.max()) <= 1.0
+    idx = np.sort(np.random.default_rng(3).choice(B, 48, replace=False))
+    pix = px[torch.from_numpy(idx).cuda()].cpu().numpy()
+    st = env.get_state().cpu().numpy()[:, idx]
+    for k in range(len(idx)):
+        _check_env(oracle_mod, env, pix, st, k, 2)
