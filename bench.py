@@ -107,12 +107,13 @@ def make_actions(continuous, B, env_id_offset, steps, seed, dev):
 
 
 # ------------------------------------------------------------------- roofline
-def step_kernel_bytes(R, action_bytes):
-    """Algorithmic HBM bytes one env moves in one step-kernel launch."""
+def step_kernel_bytes(R, action_bytes, real_bytes=4):
+    """Algorithmic HBM bytes one env moves in one step-kernel launch; the
+    state SoA holds the handle's real type (4 B, or 8 B for the fp64 variant)."""
     state_read = 52 + 6 + 2            # 4 bodies x 13, 2 pending forces x 3, steps, done
     state_write = 52 + 6 + 1           # bodies, pending forces, steps
     warm_cache = 2 * (10 + 40)         # warm-start ids + impulses, read + write once per step
-    return 4 * (state_read + state_write + warm_cache) + action_bytes + 4 * 14 * R + 4 + 1 + 8
+    return real_bytes * (state_read + state_write + warm_cache) + action_bytes + 4 * 14 * R + 4 + 1 + 8
 
 
 def render_kernel_bytes(H, W, C, R):
@@ -303,8 +304,9 @@ def _pose_diffs(g, o):
 
 def parity_case(device, R, B, F, stream, steps, thr=None, seed=0, precision="f32"):
     """One SURVEY §8d parity run: B envs from reset (seed, F_init = F), 200 steps of one
-    continuous action stream, GPU (precision) vs oracle f32 and f64; per step the max
-    |dpos| and |dquat|."""
+    continuous action stream, GPU vs oracle; per step the max |dpos| and |dquat|.
+    precision "f32": the fp32 kernels vs the oracle's f32 and f64 builds; "f64": the fp64
+    kernel variant vs the oracle's f64 build."""
     import numpy as np
 
     from oracle import oracle as O
@@ -313,8 +315,11 @@ def parity_case(device, R, B, F, stream, steps, thr=None, seed=0, precision="f32
     cfg = O.default_config(num_envs=B, action_repeats=R, initial_force=float(F), seed=seed, autoreset=0)
     for k, v in over.items():
         setattr(cfg.phys, k, v)
+    if precision == "f64":
+        cfg.precision = abi.CP_PRECISION_F64
     gpu = BatchedCartpole(B, device.index, config=abi.cp_config.from_buffer_copy(cfg))
-    orc = {p: O.Envs(abi.cp_config.from_buffer_copy(cfg), precision=p) for p in ("f32", "f64")}
+    orc = {p: O.Envs(abi.cp_config.from_buffer_copy(cfg), precision=p)
+           for p in (("f32", "f64") if precision == "f32" else ("f64",))}
     g = gpu.reset().cpu().numpy()
     o = {p: e.reset() for p, e in orc.items()}
     rng = np.random.default_rng(seed)
@@ -383,8 +388,18 @@ def parity_check(device, R, B=128, steps=WINDOW):
                 log(f"  parity {variant} F={F} {stream}")
                 matrix[f"{variant}/F{F}/{stream}"] = parity_case(device, R, B, F, stream, steps, thr)
     worst32 = max(max(v["f32"]["max_dpos"], v["f32"]["max_dquat"]) for v in matrix.values())
+    # the fp64 kernel variant (cp_config.precision = F64) on the early-exit cases: the GPU
+    # computing the double-precision algorithm, against the oracle's fp64 build
+    f64 = {}
+    for F in (0, 55):
+        for stream in ("zero", "constant", "random"):
+            log(f"  parity fp64 kernel F={F} {stream}")
+            r = parity_case(device, R, B, F, stream, steps, None, precision="f64")["f64"]
+            f64[f"early_exit/F{F}/{stream}"] = {"max_dpos": r["max_dpos"], "max_dquat": r["max_dquat"]}
+    worst64 = max(max(v["max_dpos"], v["max_dquat"]) for v in f64.values())
     return {"envs_per_case": B, "steps": steps, "repeats": R, "actions": "continuous (B,2,2)",
             "bit_exact_vs_oracle_f32": worst32 == 0.0, "max_abs_diff_vs_oracle_f32": worst32,
+            "fp64_kernel_vs_oracle_f64": {"bit_exact": worst64 == 0.0, "max_abs_diff": worst64, "cases": f64},
             "c3_workload_vs_oracle_f32": parity_c3(device, R),
             "matrix": matrix, "vs_pybullet": None,
             "note": "pybullet is not installed (parity with it unpinned, SURVEY.md §8c); f64 = the oracle's "
@@ -400,7 +415,8 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="envs per GPU (default 65,536; 4,096 with --continuous)")
     ap.add_argument("--repeats", type=int, default=3)
     ap.add_argument("--continuous", action="store_true", help="C2: continuous (B,2,2) U[-1,1] actions")
-    ap.add_argument("--dtype", choices=("f32",), default="f32")
+    ap.add_argument("--dtype", choices=("f32", "f64"), default="f32",
+                    help="f64: the fp64 kernel variant (cp_config.precision; the parity mode, DESIGN.md §7)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the cpu_baseline and parity legs")
     ap.add_argument("--no-parity", action="store_true")
@@ -432,7 +448,7 @@ def main():
     spec = shard_spec(B, rank, world, seed=SEED)
     env = BatchedCartpole(B, local, action_repeats=R, steps_per_repeat=1, max_episode_len=WINDOW,
                           initial_force=55.0, autoreset=True, seed=spec["seed"], done_on_bounds=args.done_on_bounds,
-                          env_id_offset=spec["env_id_offset"],
+                          env_id_offset=spec["env_id_offset"], precision=args.dtype,
                           **({} if args.solver_iterations is None else {"solver_iterations": args.solver_iterations}))
     if args.raster:
         env.enable_raster(True, num_cameras=args.cameras)
@@ -470,9 +486,9 @@ def main():
     value = world * B * K / elapsed
     kind = "continuous" if args.continuous else "discrete"
     per_launch_s = tm["step_ms"] / max(1, tm["step_launches"]) / 1e3
-    bytes_launch = B * step_kernel_bytes(R, 16 if args.continuous else 2)
+    bytes_launch = B * step_kernel_bytes(R, 16 if args.continuous else 2, 8 if args.dtype == "f64" else 4)
     achieved = bytes_launch / per_launch_s / 1e9
-    kernel = f"cp_step_kernel<{kind}>"
+    kernel = f"cp_step_kernel<{kind}>" if args.dtype == "f32" else f"cp64::cp_step_kernel<{kind}>"
     traffic, traffic_src = pmc_traffic(kernel, B, R, kind)
     if args.raster:
         # C5: the render kernel writes 2.9 GB per step and is the dominant HBM consumer
@@ -507,7 +523,7 @@ def main():
         "data": "synthetic (hashed random actions keyed by global env id, Philox bump pushes; no pybullet, "
                 "see DESIGN.md)",
         "config": {"workload": wl, "name": name, "global_batch": world * B, "envs_per_gpu": B, "action_repeats": R,
-                   "steps_per_repeat": 1, "action_kind": kind, "step_kernel_shape": step_shape(B),
+                   "steps_per_repeat": 1, "action_kind": kind, "step_kernel_shape": "latency (fp64)" if args.dtype == "f64" else step_shape(B),
                    "parallelism": f"dp{world} (independent env shards, no per-step collective)",
                    "solver_iterations": env.cfg.phys.solver_iterations,
                    "residual_threshold": env.cfg.phys.residual_threshold},

@@ -5,7 +5,7 @@ library's entry points with these types.
 """
 import ctypes as C
 
-CP_ABI_VERSION = 1
+CP_ABI_VERSION = 2
 
 CP_BODY_GROUND, CP_BODY_CART, CP_BODY_POLE, CP_BODY_CART2, CP_BODY_POLE2 = range(5)
 CP_NUM_BODIES = 5
@@ -100,7 +100,12 @@ class cp_config(C.Structure):
         ("seed", C.c_uint64),
         ("env_id_offset", C.c_int64),
         ("phys", cp_physics),
+        ("precision", C.c_int32),
     ]
+
+
+CP_PRECISION_F32 = 0
+CP_PRECISION_F64 = 1
 
 
 class cp_raster_config(C.Structure):

@@ -43,7 +43,7 @@ class BatchedCartpole:
     def __init__(self, num_envs, device=0, *, action_repeats=2, steps_per_repeat=1, max_episode_len=200,
                  action_force=50.0, initial_force=200.0, random_theta=True, done_on_bounds=False,
                  autoreset=False, seed=0, env_id_offset=0, bump_mode="philox", discrete_actions=False,
-                 config=None, **phys):
+                 precision="f32", config=None, **phys):
         self.lib = native.load()
         if config is None:
             config = native.default_config(
@@ -53,6 +53,9 @@ class BatchedCartpole:
                 random_theta=int(bool(random_theta)), done_on_bounds=int(bool(done_on_bounds)),
                 autoreset=int(bool(autoreset)), seed=int(seed), env_id_offset=int(env_id_offset),
                 bump_mode=abi.CP_BUMP_HOST if bump_mode == "host" else abi.CP_BUMP_PHILOX)
+            if precision not in ("f32", "f64"):
+                raise ValueError(f"precision must be 'f32' or 'f64', got {precision!r}")
+            config.precision = abi.CP_PRECISION_F64 if precision == "f64" else abi.CP_PRECISION_F32
             for k, v in phys.items():
                 if not hasattr(config.phys, k):
                     raise ValueError(f"unknown physics parameter {k!r}")
@@ -61,6 +64,8 @@ class BatchedCartpole:
                 config.phys.inv_dt = 1.0 / float(phys["dt"])
         self.cfg = config
         self.B, self.R, self.S = config.num_envs, config.action_repeats, config.steps_per_repeat
+        # the state's real type (cp_config.precision); obs and all other outputs are float32
+        self.real = torch.float64 if config.precision == abi.CP_PRECISION_F64 else torch.float32
         self.discrete_actions = bool(discrete_actions)
         self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
         if self.device.type != "cuda":
@@ -169,13 +174,15 @@ class BatchedCartpole:
         native.check(self.h, self.lib.cp_set_bump_forces(self.h, _ptr(f), self._stream()), "cp_set_bump_forces")
 
     def get_state(self):
-        s = torch.empty((abi.CP_STATE_FIELDS, self.B), device=self.device, dtype=torch.float32)
+        s = torch.empty((abi.CP_STATE_FIELDS, self.B), device=self.device, dtype=self.real)
         native.check(self.h, self.lib.cp_get_state(self.h, _ptr(s), self._stream()), "cp_get_state")
         return s
 
     def set_state(self, s):
-        s = _device_buffer(torch.as_tensor(s, dtype=torch.float32), (abi.CP_STATE_FIELDS, self.B), torch.float32,
-                           self.device, "state")
+        s = torch.as_tensor(s)
+        if s.dtype != self.real:
+            raise ValueError(f"state: this handle keeps {self.real} state, got {s.dtype}")
+        s = _device_buffer(s, (abi.CP_STATE_FIELDS, self.B), self.real, self.device, "state")
         native.check(self.h, self.lib.cp_set_state(self.h, _ptr(s), self._stream()), "cp_set_state")
 
     def episode_returns(self):

@@ -15,15 +15,18 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = os.path.join(HERE, "csrc", "cp_kernels.hip")
-DEPS = [os.path.join(HERE, "csrc", f) for f in ("cp_kernels.hip", "cp_physics.h", "cp_math.h", "cp_raster.h", "cp_replay.h")] + [
+# two translation units, compiled in parallel and linked into one library: the fp32 env
+# kernels + raster / event / replay kernels + the C-ABI, and the fp64 env kernels
+SRCS = [os.path.join(HERE, "csrc", f) for f in ("cp_kernels.hip", "cp_kernels64.hip")]
+DEPS = SRCS + [os.path.join(HERE, "csrc", f) for f in ("cp_common.h", "cp_env.h", "cp_physics.h", "cp_math.h",
+                                                     "cp_raster.h", "cp_replay.h")] + [
     os.path.join(HERE, "..", "include", "cartpole_amd.h")]
 LIB = os.path.join(HERE, "libcartpole_hip.so")
 STAMPS_LIB = os.path.join(HERE, "libcartpole_hip_stamps.so")
 ARCH = os.environ.get("CP_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-fPIC", "-shared",
+FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-fPIC",
          "-Wno-unused-result",
          # LLVM's iterative ILP scheduler for gfx9: step kernel 0.634 -> 0.624 ms (r11);
          # scheduling never reorders a rounding, so the results stay bit-identical
@@ -41,12 +44,25 @@ def build(force=False, verbose=False, stamps=False):
     lib = STAMPS_LIB if stamps else LIB
     if not force and up_to_date(lib):
         return lib
-    cmd = [HIPCC] + FLAGS + (["-DCP_STAMPS"] if stamps else []) + ["-o", lib + ".tmp", SRC]
-    if verbose:
-        print(" ".join(cmd))
+    extra = ["-DCP_STAMPS"] if stamps else []
+    objs, procs = [], []
+    for src in SRCS:
+        obj = lib + "." + os.path.basename(src) + ".o"
+        cmd = [HIPCC] + FLAGS + extra + ["-c", "-o", obj, src]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)))
+        objs.append(obj)
+    for cmd, pr in procs:
+        out, _ = pr.communicate()
+        if pr.returncode != 0:
+            raise RuntimeError("hipcc failed:\n" + " ".join(cmd) + "\n" + out)
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib + ".tmp"] + objs
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
-        raise RuntimeError("hipcc failed:\n" + res.stdout + res.stderr)
+        raise RuntimeError("hipcc link failed:\n" + res.stdout + res.stderr)
+    for o in objs:
+        os.remove(o)
     os.replace(lib + ".tmp", lib)
     return lib
 

@@ -1,0 +1,500 @@
+// cp_env.h — the batched env's kernels over `real` (step, reset, init) and their host
+// launchers; included once per real type after cp_math.h and cp_physics.h (cp_common.h):
+// namespace cp (fp32, cp_kernels.hip) and cp64 (fp64, cp_kernels64.hip).
+//
+//   cp_step_kernel   R x S substeps fused in one launch; force applied after each
+//                    substep (bullet_cartpole.py:199-207); obs at each repeat end
+//                    (:237 -> :298-311); steps/done/reward (:239-260).  Finishing
+//                    envs are appended to a reset list by wave ballot compaction.
+//   cp_reset_kernel  spawn poses, 100 settle + 30 bump substeps (:313-346), over a
+//                    compacted list of env ids (dense waves, no idle lanes).
+//
+// Memory: per-env state is SoA real [CP_STATE_FIELDS][B] in HBM (coalesced per field);
+// inside a launch the env lives in VGPRs and its contact rows in a per-wave LDS pool
+// (fp32: 20 KiB per wave, 8 waves per CU = 160 KiB).  Outputs (obs, terminal obs,
+// readback, 8-states, raster poses) are float32 in both instantiations, as the reference's
+// np.float32 state array (bullet_cartpole.py:148).  DESIGN.md §4-5.
+#if !defined(CP_NS) || !defined(CP_REAL)
+#error "define CP_NS and CP_REAL before including cp_env.h (see cp_kernels.hip)"
+#endif
+
+namespace CP_NS {
+
+// occupancy target of the physics kernels (waves per SIMD); the register budget follows
+#ifndef CP_WAVES_PER_EU
+#define CP_WAVES_PER_EU 2
+#endif
+
+// fp64: only the 1-wave-per-SIMD (512 VGPR) kernel shape, with the slow-form rows (the fast
+// form's precomputed rows do not fit twice the registers)
+constexpr bool kF64 = sizeof(real) == 8;
+
+using Bufs = cpc::Bufs;
+using Lqr = cpc::Lqr;
+using SoaF = SoaT<float>;
+
+__constant__ float kDiscrete[CP_NUM_DISCRETE][2] = {{0.f, 0.f}, {-1.f, 0.f}, {1.f, 0.f}, {0.f, 1.f}, {0.f, -1.f}};
+
+// raster obs: the repeat-end pose of the 4 bodies (xyz, quat xyzw) for the render kernel
+CP_DEV void write_rposes(const Sim& S, float* dst) {
+#pragma unroll
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        float* o = dst + d * 7;
+        o[0] = (float)S.b[d].x.x; o[1] = (float)S.b[d].x.y; o[2] = (float)S.b[d].x.z;
+        o[3] = (float)S.b[d].q[0]; o[4] = (float)S.b[d].q[1]; o[5] = (float)S.b[d].q[2]; o[6] = (float)S.b[d].q[3];
+    }
+}
+
+// per-wave stamp accumulation into b.stamps (lane 0 writes; CP_STAMPS builds only)
+CP_DEV void flush_stamps(const Stamps& ST, uint64_t* dst, uint64_t total) {
+#ifdef CP_STAMPS
+    if ((threadIdx.x & (WAVE - 1)) == 0) {
+        atomicAdd((unsigned long long*)&dst[0], (unsigned long long)ST.narrow);
+        atomicAdd((unsigned long long*)&dst[1], (unsigned long long)ST.vel);
+        atomicAdd((unsigned long long*)&dst[2], (unsigned long long)ST.solve);
+        atomicAdd((unsigned long long*)&dst[3], (unsigned long long)ST.integ);
+        atomicAdd((unsigned long long*)&dst[4], (unsigned long long)ST.sweeps);
+        atomicAdd((unsigned long long*)&dst[5], (unsigned long long)ST.substeps);
+        atomicAdd((unsigned long long*)&dst[6], (unsigned long long)total);
+        atomicAdd((unsigned long long*)&dst[7], 1ull);
+        if (ST.bb) {  // narrowphase split into the spare slots 8-10
+            atomicAdd((unsigned long long*)&dst[8], (unsigned long long)ST.sel);
+            atomicAdd((unsigned long long*)&dst[9], (unsigned long long)ST.bb);
+            atomicAdd((unsigned long long*)&dst[10], (unsigned long long)ST.rows);
+        }
+    }
+#else
+    (void)ST; (void)dst; (void)total;
+#endif
+}
+
+CP_DEV void load_sim(Sim& S, const Soa& st, uint32_t o) {
+#pragma unroll
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        S.b[d].x = mk(st.ld(CP_SF_BODY(d, 0), o), st.ld(CP_SF_BODY(d, 1), o), st.ld(CP_SF_BODY(d, 2), o));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) S.b[d].q[k] = st.ld(CP_SF_BODY(d, 3 + k), o);
+        S.b[d].v = mk(st.ld(CP_SF_BODY(d, 7), o), st.ld(CP_SF_BODY(d, 8), o), st.ld(CP_SF_BODY(d, 9), o));
+        S.b[d].w = mk(st.ld(CP_SF_BODY(d, 10), o), st.ld(CP_SF_BODY(d, 11), o), st.ld(CP_SF_BODY(d, 12), o));
+    }
+    S.f0 = mk(st.ld(CP_SF_PENDING(0, 0), o), st.ld(CP_SF_PENDING(0, 1), o), st.ld(CP_SF_PENDING(0, 2), o));
+    S.f2 = mk(st.ld(CP_SF_PENDING(1, 0), o), st.ld(CP_SF_PENDING(1, 1), o), st.ld(CP_SF_PENDING(1, 2), o));
+}
+
+CP_DEV void store_sim(const Sim& S, const Soa& st, uint32_t o) {
+#pragma unroll
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        st.st(CP_SF_BODY(d, 0), o, S.b[d].x.x);
+        st.st(CP_SF_BODY(d, 1), o, S.b[d].x.y);
+        st.st(CP_SF_BODY(d, 2), o, S.b[d].x.z);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) st.st(CP_SF_BODY(d, 3 + k), o, S.b[d].q[k]);
+        st.st(CP_SF_BODY(d, 7), o, S.b[d].v.x);
+        st.st(CP_SF_BODY(d, 8), o, S.b[d].v.y);
+        st.st(CP_SF_BODY(d, 9), o, S.b[d].v.z);
+        st.st(CP_SF_BODY(d, 10), o, S.b[d].w.x);
+        st.st(CP_SF_BODY(d, 11), o, S.b[d].w.y);
+        st.st(CP_SF_BODY(d, 12), o, S.b[d].w.z);
+    }
+    st.st(CP_SF_PENDING(0, 0), o, S.f0.x);
+    st.st(CP_SF_PENDING(0, 1), o, S.f0.y);
+    st.st(CP_SF_PENDING(0, 2), o, S.f0.z);
+    st.st(CP_SF_PENDING(1, 0), o, S.f2.x);
+    st.st(CP_SF_PENDING(1, 1), o, S.f2.y);
+    st.st(CP_SF_PENDING(1, 2), o, S.f2.z);
+}
+
+CP_DEV int32_t ldi(const Soa& st, int f, uint32_t o) { return (int32_t)to_bits(st.ld(f, o)); }
+CP_DEV void sti(const Soa& st, int f, uint32_t o, int32_t v) { st.st(f, o, bits_to<real>((uint32_t)v)); }
+
+CP_DEV void write_obs_row(const Sim& S, float* dst) {
+    dst[0] = (float)S.b[0].x.x; dst[1] = (float)S.b[0].x.y; dst[2] = (float)S.b[0].x.z;
+    dst[3] = (float)S.b[0].q[0]; dst[4] = (float)S.b[0].q[1]; dst[5] = (float)S.b[0].q[2]; dst[6] = (float)S.b[0].q[3];
+    dst[7] = (float)S.b[1].x.x; dst[8] = (float)S.b[1].x.y; dst[9] = (float)S.b[1].x.z;
+    dst[10] = (float)S.b[1].q[0]; dst[11] = (float)S.b[1].q[1]; dst[12] = (float)S.b[1].q[2];
+    dst[13] = (float)S.b[1].q[3];
+}
+
+// 12-state pole readback (bullet_cartpole.py:212-229)
+template <int POLE, int VEL>
+CP_DEV void readback_pole(const Sim& S, float* dst) {
+    const Body& p = S.b[POLE];
+    const Body& vb = S.b[VEL];
+    V3 rpy = quat_euler(p.q[0], p.q[1], p.q[2], p.q[3]);
+    dst[0] = (float)p.x.x; dst[1] = (float)p.x.y; dst[2] = (float)p.x.z;
+    dst[3] = (float)rpy.x; dst[4] = (float)rpy.y; dst[5] = (float)rpy.z;
+    dst[6] = (float)vb.v.x; dst[7] = (float)vb.v.y; dst[8] = (float)vb.v.z;
+    dst[9] = (float)vb.w.x; dst[10] = (float)vb.w.y; dst[11] = (float)vb.w.z;
+}
+
+// ---- closed-loop LQR policy (random_action_agent.py:60-135)
+// pole 8-state of pair P (:121-135): x - x0, x', y, y', roll, roll', pitch, pitch'
+template <int P>
+CP_DEV void pole_state8(const Sim& S, real x0, real s[8]) {
+    const Body& p = S.b[2 * P + 1];
+    const V3 rpy = quat_euler(p.q[0], p.q[1], p.q[2], p.q[3]);
+    s[0] = p.x.x - x0; s[1] = p.v.x; s[2] = p.x.y; s[3] = p.v.y;
+    s[4] = rpy.x; s[5] = p.w.x; s[6] = rpy.y; s[7] = p.w.y;
+}
+
+// u = -K s (:92-95, lqr zero point 0), accumulated k = 0..7 with fma
+CP_DEV void lqr_u(const float* K, const real s[8], real& ux, real& uy) {
+    real ax = real(0.0), ay = real(0.0);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        ax = fma_(real(K[k]), s[k], ax);
+        ay = fma_(real(K[8 + k]), s[k], ay);
+    }
+    ux = -ax;
+    uy = -ay;
+}
+
+CP_DEV bool lqr_out_of_bounds(const real s[8], real pos, real ang) {
+    return abs_(s[0]) > pos || abs_(s[2]) > pos || abs_(s[4]) > ang || abs_(s[6]) > ang;
+}
+
+// 8-states of both pairs -> next forces; true if both pairs are out of bounds (:908)
+CP_DEV bool lqr_observe(const Sim& S, const cp_config& cfg, const Lqr& q, const float* K, real u[2][2],
+                        float* s8_out) {
+    real s[8];
+    pole_state8<0>(S, real(cfg.phys.spawn_pos[CP_BODY_POLE][0]), s);
+    if (s8_out)
+        for (int k = 0; k < 8; ++k) s8_out[k] = (float)s[k];
+    lqr_u(K, s, u[0][0], u[0][1]);
+    const bool out0 = lqr_out_of_bounds(s, real(q.done_pos), real(q.done_angle));
+    pole_state8<1>(S, real(cfg.phys.spawn_pos[CP_BODY_POLE2][0]), s);
+    if (s8_out)
+        for (int k = 0; k < 8; ++k) s8_out[k + 8] = (float)s[k];
+    lqr_u(K + 16, s, u[1][0], u[1][1]);
+    const bool out1 = lqr_out_of_bounds(s, real(q.done_pos), real(q.done_angle));
+    return q.done_pos > 0.0f && out0 && out1;
+}
+
+// commented-out bounds check of the reference (:243-253), on the pole pose
+CP_DEV bool bounds_exceeded(const Sim& S, const cp_config& cfg) {
+    const Body& p = S.b[1];
+    if (abs_(p.x.x) > real(cfg.pos_threshold) || abs_(p.x.y) > real(cfg.pos_threshold)) return true;
+    real qx = p.q[0], qy = p.q[1], qz = p.q[2], qw = p.q[3];
+    real Y = real(2.0) * fma_(qy, qz, qw * qx);
+    real X = ((qw * qw - qx * qx) - qy * qy) + qz * qz;
+    bool roll_out = (X > real(0.0)) ? (abs_(Y) > X * real(cfg.tan_angle_threshold)) : !(X == real(0.0) && Y == real(0.0));
+    real sarg = real(-2.0) * fma_(qx, qz, -(qw * qy));
+    bool pitch_out = abs_(sarg) > real(cfg.sin_angle_threshold);
+    return roll_out || pitch_out;
+}
+
+// Bump force k on cart C (LINK frame), bullet_cartpole.py:354-359
+CP_DEV void bump_force(const cp_config& cfg, const float* bumps, int i, int episode, int k, int c, real& fx,
+                       real& fy) {
+    if (cfg.bump_mode == CP_BUMP_HOST) {
+        const float* f = bumps + (((size_t)i * cfg.initial_force_steps + k) * 2 + c) * 2;
+        fx = f[0];
+        fy = f[1];
+        return;
+    }
+    const real F = cfg.initial_force;
+    if (!cfg.random_theta) {
+        fx = F;
+        fy = F * real(0.0);
+        return;
+    }
+    uint32_t idx = (uint32_t)(2 * k + c);
+    uint64_t gid = (uint64_t)(cfg.env_id_offset + i);
+    uint32_t w = philox_word(idx >> 2, (uint32_t)episode, (uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)cfg.seed,
+                             (uint32_t)(cfg.seed >> 32), (int)(idx & 3u));
+    real u = real(w >> 8) * real(5.9604644775390625e-08);
+    real s, co;
+    sincos_turns(u, s, co);
+    fx = F * co;
+    fy = F * s;
+}
+
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) cp_init_kernel(cp_config cfg, Bufs b) {
+    const int B = cfg.num_envs;
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    const Soa st = Soa::make(b.state, B, CP_STATE_FIELDS);
+    const uint32_t o = Soa::eoff(i);
+    for (int f = 0; f < CP_STATE_FIELDS; ++f) st.st(f, o, real(0.0));
+#pragma unroll
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) st.st(CP_SF_BODY(d, k), o, real(cfg.phys.spawn_pos[d + 1][k]));
+        st.st(CP_SF_BODY(d, 6), o, real(1.0));
+    }
+#pragma unroll
+    for (int p = 0; p < CP_NUM_ISLANDS; ++p)
+#pragma unroll
+        for (int j = 0; j < CP_ISLAND_PAIRS; ++j) sti(st, CP_SF_WS_ID(p, j), o, -1);
+    sti(st, CP_SF_DONE, o, 1);  // not reset yet: reference raises, batched API reports done
+    b.ret_acc[i] = 0.0f;
+    b.last_ret[i] = 0.0f;
+    b.last_len[i] = 0;
+    b.overflow[i] = 0;
+}
+
+// LAT = false: the throughput shape of the step kernel (2 waves per SIMD), for reset bursts
+// (fixed-length episodes end together).  LAT = true: one wave per SIMD with 512 registers and
+// fast-form rows, for the short lists of desynchronised episodes (bounds termination), where
+// the 130 serial substeps of one wave are the whole latency of the step.
+template <bool LAT>
+__global__ void __launch_bounds__(WAVE)
+__attribute__((amdgpu_waves_per_eu(LAT ? 1 : CP_WAVES_PER_EU, LAT ? 1 : CP_WAVES_PER_EU)))
+cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
+    __shared__ real lds_pool[POOL_FLOATS * WAVE];
+    const int B = cfg.num_envs;
+    const int t = blockIdx.x * WAVE + threadIdx.x;
+    if (t == 0 && b.count_next) *b.count_next = 0;  // the next cp_step's list starts empty
+    const int n = *b.count;
+    if ((t >> 1) >= n) return;  // lane pairs past the compacted list
+    const int isl = t & 1;
+    const bool lead = isl == 0;
+    const int i = b.list[t >> 1];
+    real* pool = lds_pool + threadIdx.x;
+    real* pool0 = lds_pool + (threadIdx.x & ~1u);
+    const Mem G = Mem::make(b.state, b.scratch, B, i, isl);
+    const Lane L = Lane::make(isl, cfg.phys);
+    Stamps ST;
+    Sim S;
+    load_sim(S, G.st, G.off);  // pending forces survive the reset (pybullet keeps them)
+    const int episode = ldi(G.st, CP_SF_EPISODE, G.off);
+#pragma unroll
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        S.b[d].x = mk(cfg.phys.spawn_pos[d + 1][0], cfg.phys.spawn_pos[d + 1][1], cfg.phys.spawn_pos[d + 1][2]);
+        S.b[d].q[0] = real(0.0); S.b[d].q[1] = real(0.0); S.b[d].q[2] = real(0.0); S.b[d].q[3] = real(1.0);
+        S.b[d].v = mk(real(0.0), real(0.0), real(0.0));
+        S.b[d].w = mk(real(0.0), real(0.0), real(0.0));
+    }
+#pragma unroll
+    for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {  // the lane's island's warm-start cache
+        G.sw(CP_SF_WS_ID(0, j), bits_to<real>(0xFFFFFFFFu));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) G.sl(CP_SF_WS_LAM(0, j, k), real(0.0));
+    }
+    int ov = 0;
+    const int nsub = cfg.settle_steps + cfg.initial_force_steps;
+    for (int s = 0; s < nsub; ++s) {
+        substep<LAT && !kF64>(S, cfg.phys, L, pool, pool0, ov, G, ST);
+        const int k = s - cfg.settle_steps;
+        if (k >= 0) {
+            real fx, fy;
+            bump_force(cfg, b.bumps, i, episode, k, 0, fx, fy);
+            apply_force_link<0>(S, fx, fy);
+            bump_force(cfg, b.bumps, i, episode, k, 1, fx, fy);
+            apply_force_link<1>(S, fx, fy);
+        }
+    }
+    ov += (int)partner_u((uint32_t)ov);
+    if (!lead) return;
+    store_sim(S, G.st, G.off);
+    b.overflow[i] += ov;
+    float row[14];
+    write_obs_row(S, row);
+    const int R = cfg.action_repeats;
+    if (b.rposes)  // every repeat slot shows the reset pose (bullet_cartpole.py:342-345)
+        for (int r = 0; r < R; ++r) write_rposes(S, b.rposes + ((size_t)i * R + r) * CP_NUM_DYN * 7);
+    float* o = obs_out + (size_t)i * R * 14;
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int f = 0; f < 14; ++f) o[r * 14 + f] = row[f];
+    sti(G.st, CP_SF_STEPS, G.off, 0);
+    sti(G.st, CP_SF_DONE, G.off, 0);
+    sti(G.st, CP_SF_EPISODE, G.off, episode + 1);
+    b.ret_acc[i] = 0.0f;
+}
+
+// LAT: the latency shape of cp_reset_kernel<true> (1 wave per SIMD, 512 registers, fast-form
+// rows) for batches whose waves all get a SIMD of their own (<= 32,768 envs)
+template <int KIND, bool LQR, bool LAT>
+__global__ void __launch_bounds__(WAVE)
+__attribute__((amdgpu_waves_per_eu(LAT ? 1 : CP_WAVES_PER_EU, LAT ? 1 : CP_WAVES_PER_EU)))
+cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float* reward_out, uint8_t* done_out,
+               float* term_out, float* readback, int rb_bug, Lqr lq) {
+    __shared__ real lds_pool[POOL_FLOATS * WAVE];
+    const int B = cfg.num_envs;
+    const int t = blockIdx.x * WAVE + threadIdx.x;
+    const int i = t >> 1, isl = t & 1;
+    const bool lead = isl == 0;  // lane 0 of the pair writes the env's outputs
+    const bool inb = i < B;
+    const int R = cfg.action_repeats, SR = cfg.steps_per_repeat;
+    real* pool = lds_pool + threadIdx.x;
+    real* pool0 = lds_pool + (threadIdx.x & ~1u);
+    bool want_reset = false;
+    bool render_me = false;  // simulated this step: its frames go to the render kernel
+    Stamps ST;
+    CP_STAMP(k0);
+    if (inb) {
+        const Mem G = Mem::make(b.state, b.scratch, B, i, isl);
+        const Lane L = Lane::make(isl, cfg.phys);
+        const SoaF term = SoaF::make(b.term_obs, B, R * 14);
+        const uint32_t toff = SoaF::eoff(i);
+        float* obs = obs_out + (size_t)i * R * 14;
+        const bool was_done = ldi(G.st, CP_SF_DONE, G.off) != 0;
+        if (lead) b.stepped[i] = was_done ? 0 : 1;
+        if (was_done) {  // step after done (bullet_cartpole.py:179-181)
+            if (lead) {
+                for (int f = 0; f < R * 14; ++f) obs[f] = term.ld(f, toff);
+                reward_out[i] = 0.0f;
+                done_out[i] = 1;
+            }
+        } else {
+            real a00, a01, a10, a11;
+            if constexpr (KIND == CP_ACTION_CONTINUOUS) {
+                const float4 a = reinterpret_cast<const float4*>(actions)[i];
+                a00 = a.x; a01 = a.y; a10 = a.z; a11 = a.w;
+            } else {
+                const char2 a = reinterpret_cast<const char2*>(actions)[i];
+                int k0 = a.x, k1 = a.y;
+                k0 = (k0 < 0 || k0 >= CP_NUM_DISCRETE) ? 0 : k0;
+                k1 = (k1 < 0 || k1 >= CP_NUM_DISCRETE) ? 0 : k1;
+                a00 = kDiscrete[k0][0]; a01 = kDiscrete[k0][1];
+                a10 = kDiscrete[k1][0]; a11 = kDiscrete[k1][1];
+            }
+            const real F = cfg.action_force;
+            const real f00 = a00 * F, f01 = a01 * F, f10 = a10 * F, f11 = a11 * F;
+            Sim S;
+            load_sim(S, G.st, G.off);
+            int ov = 0;
+            real u[2][2] = {{real(0.0), real(0.0)}, {real(0.0), real(0.0)}};  // LQR forces from the last observed state
+            bool lqr_done = false;
+            const float* K = nullptr;
+            if constexpr (LQR) {
+                K = lq.gains + (lq.per_env ? (size_t)i * 32 : 0);
+                lqr_observe(S, cfg, lq, K, u, nullptr);
+            }
+            for (int r = 0; r < R; ++r) {
+                for (int s = 0; s < SR; ++s) {
+                    substep<LAT && !kF64>(S, cfg.phys, L, pool, pool0, ov, G, ST);
+                    if constexpr (LQR) {  // disturbance + control (:897-901), control from the pre-step state
+                        apply_force_link<0>(S, f00 + u[0][0], f01 + u[0][1]);
+                        apply_force_link<1>(S, f10 + u[1][0], f11 + u[1][1]);
+                        float* s8 = (lq.state8 && lead) ? lq.state8 + (((size_t)i * R + r) * SR + s) * 16 : nullptr;
+                        lqr_done |= lqr_observe(S, cfg, lq, K, u, s8);
+                    } else {
+                        apply_force_link<0>(S, f00, f01);
+                        apply_force_link<1>(S, f10, f11);
+                    }
+                    if (readback && lead) {
+                        float* rb = readback + (size_t)i * 2 * R * SR * 12;
+                        readback_pole<1, 1>(S, rb + ((size_t)(0 * R + r) * SR + s) * 12);
+                        if (rb_bug) readback_pole<3, 1>(S, rb + ((size_t)(1 * R + r) * SR + s) * 12);
+                        else readback_pole<3, 3>(S, rb + ((size_t)(1 * R + r) * SR + s) * 12);
+                    }
+                }
+                if (lead) {
+                    float row[14];
+                    write_obs_row(S, row);
+#pragma unroll
+                    for (int f = 0; f < 14; ++f) obs[r * 14 + f] = row[f];
+                    if (b.rposes) write_rposes(S, b.rposes + ((size_t)i * R + r) * CP_NUM_DYN * 7);
+                }
+            }
+            render_me = lead && b.rposes != nullptr;
+            ov += (int)partner_u((uint32_t)ov);
+            if (ov && lead) b.overflow[i] += ov;
+            const int steps = ldi(G.st, CP_SF_STEPS, G.off) + 1;
+            bool done = steps >= cfg.max_episode_len;
+            if (cfg.done_on_bounds && bounds_exceeded(S, cfg)) done = true;
+            if (LQR && lqr_done) done = true;
+            if (lead) {
+                store_sim(S, G.st, G.off);
+                sti(G.st, CP_SF_STEPS, G.off, steps);
+                reward_out[i] = 1.0f;  // bullet_cartpole.py:260
+                done_out[i] = done ? 1 : 0;
+                const float ret = b.ret_acc[i] + 1.0f;
+                if (done) {
+                    b.last_ret[i] = ret;
+                    b.last_len[i] = steps;
+                    b.ret_acc[i] = 0.0f;
+                    for (int f = 0; f < R * 14; ++f) term.st(f, toff, obs[f]);
+                    if (term_out)
+                        for (int f = 0; f < R * 14; ++f) term_out[(size_t)i * R * 14 + f] = obs[f];
+                    sti(G.st, CP_SF_DONE, G.off, 1);
+                    want_reset = cfg.autoreset != 0;
+                } else {
+                    b.ret_acc[i] = ret;
+                }
+            }
+        }
+    }
+#ifdef CP_STAMPS
+    CP_STAMP(k1);
+    flush_stamps(ST, b.stamps, k1 - k0);
+#endif
+    if (cfg.autoreset) {
+        // wave ballot compaction of the finishing envs into the reset list
+        const uint64_t bal = __ballot(want_reset);
+        const int lane = threadIdx.x;  // want_reset is set on lead lanes only
+        const int n = __popcll(bal);
+        int base = 0;
+        if (lane == 0 && n) base = atomicAdd(b.count, n);
+        base = __shfl(base, 0);
+        if (want_reset) b.list[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
+    }
+    if (b.rposes) {
+        const uint64_t bal = __ballot(render_me);
+        const int lane = threadIdx.x & (WAVE - 1);
+        const int n = __popcll(bal);
+        int base = 0;
+        if (lane == 0 && n) base = atomicAdd(b.rcount, n);
+        base = __shfl(base, 0);
+        if (render_me) b.rlist[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
+    }
+}
+
+// ---------------------------------------------------------------- host launchers
+static inline unsigned env_grid(int n, int block) { return (unsigned)((n + block - 1) / block); }
+
+void launch_init(const cp_config& cfg, const Bufs& b, hipStream_t st) {
+    hipLaunchKernelGGL(cp_init_kernel, dim3(env_grid(cfg.num_envs, 256)), dim3(256), 0, st, cfg, b);
+}
+
+void launch_reset(bool lat, const cp_config& cfg, const Bufs& b, float* obs_out, hipStream_t st) {
+    const dim3 grid(env_grid(2 * cfg.num_envs, WAVE)), block(WAVE);  // two lanes per env
+    if constexpr (kF64) {
+        (void)lat;
+        hipLaunchKernelGGL(cp_reset_kernel<true>, grid, block, 0, st, cfg, b, obs_out);
+    } else {
+        if (lat) hipLaunchKernelGGL(cp_reset_kernel<true>, grid, block, 0, st, cfg, b, obs_out);
+        else hipLaunchKernelGGL(cp_reset_kernel<false>, grid, block, 0, st, cfg, b, obs_out);
+    }
+}
+
+template <int K, bool Q>
+static void launch_step_t(bool lat, const cp_config& cfg, const Bufs& b, const void* actions, float* obs_out,
+                          float* reward_out, uint8_t* done_out, float* term_out, float* readback, int rb_bug,
+                          const Lqr& lq, hipStream_t st) {
+    const dim3 grid(env_grid(2 * cfg.num_envs, WAVE)), block(WAVE);  // two lanes per env
+    if constexpr (kF64) {
+        (void)lat;
+        hipLaunchKernelGGL((cp_step_kernel<K, Q, true>), grid, block, 0, st, cfg, b, actions, obs_out, reward_out,
+                           done_out, term_out, readback, rb_bug, lq);
+    } else {
+        if (lat)
+            hipLaunchKernelGGL((cp_step_kernel<K, Q, true>), grid, block, 0, st, cfg, b, actions, obs_out, reward_out,
+                               done_out, term_out, readback, rb_bug, lq);
+        else
+            hipLaunchKernelGGL((cp_step_kernel<K, Q, false>), grid, block, 0, st, cfg, b, actions, obs_out, reward_out,
+                               done_out, term_out, readback, rb_bug, lq);
+    }
+}
+
+void launch_step(bool lat, int kind, const cp_config& cfg, const Bufs& b, const void* actions, float* obs_out,
+                 float* reward_out, uint8_t* done_out, float* term_out, float* readback, int rb_bug, const Lqr& lq,
+                 hipStream_t st) {
+    const bool q = lq.gains != nullptr;
+    if (kind == CP_ACTION_CONTINUOUS) {
+        if (q) launch_step_t<CP_ACTION_CONTINUOUS, true>(lat, cfg, b, actions, obs_out, reward_out, done_out, term_out,
+                                                         readback, rb_bug, lq, st);
+        else launch_step_t<CP_ACTION_CONTINUOUS, false>(lat, cfg, b, actions, obs_out, reward_out, done_out, term_out,
+                                                        readback, rb_bug, lq, st);
+    } else {
+        if (q) launch_step_t<CP_ACTION_DISCRETE, true>(lat, cfg, b, actions, obs_out, reward_out, done_out, term_out,
+                                                       readback, rb_bug, lq, st);
+        else launch_step_t<CP_ACTION_DISCRETE, false>(lat, cfg, b, actions, obs_out, reward_out, done_out, term_out,
+                                                      readback, rb_bug, lq, st);
+    }
+}
+
+}  // namespace CP_NS

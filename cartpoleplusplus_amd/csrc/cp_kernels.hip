@@ -1,19 +1,12 @@
-// cp_kernels.hip — batched cartpole++ env on MI355X (gfx950): kernels + C-ABI.
+// cp_kernels.hip — batched cartpole++ env on MI355X (gfx950): the fp32 kernels + C-ABI.
 //
 // Replaces bullet_cartpole.py's hot path (BulletCartpole.step/reset and the
 // pybullet calls behind them) for B independent envs, two lanes per env (lane
-// 2e+p owns contact island p; cp_physics.h).
-//
-//   cp_step_kernel   R x S substeps fused in one launch; force applied after each
-//                    substep (bullet_cartpole.py:199-207); obs at each repeat end
-//                    (:237 -> :298-311); steps/done/reward (:239-260).  Finishing
-//                    envs are appended to a reset list by wave ballot compaction.
-//   cp_reset_kernel  spawn poses, 100 settle + 30 bump substeps (:313-346), over a
-//                    compacted list of env ids (dense waves, no idle lanes).
-//
-// Memory: per-env state is SoA float32 [CP_STATE_FIELDS][B] in HBM (coalesced
-// per field); inside a launch the env lives in VGPRs and its contact rows in a
-// 20 KiB-per-wave LDS pool (8 waves per CU = 160 KiB).  DESIGN.md §Kernels.
+// 2e+p owns contact island p; cp_physics.h).  The env kernels (cp_env.h) are written
+// over `real` and instantiated here for fp32 (namespace cp, the product path) and in
+// cp_kernels64.hip for fp64 (namespace cp64, the parity variant, cp_config.precision).
+// This file also holds the fp32-only kernels (reset-mask compaction, raster obs, event
+// log records, replay memory) and every C-ABI entry point (include/cartpole_amd.h).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -26,248 +19,20 @@
 #include <vector>
 
 #include "../../include/cartpole_amd.h"
+#include "cp_common.h"
+
+#define CP_NS cp
+#define CP_REAL float
+#include "cp_math.h"
 #include "cp_physics.h"
+#include "cp_env.h"
+#undef CP_NS
+#undef CP_REAL
+
 #include "cp_raster.h"
 #include "cp_replay.h"
 
 namespace cp {
-
-// occupancy target of the physics kernels (waves per SIMD); the register budget follows
-#ifndef CP_WAVES_PER_EU
-#define CP_WAVES_PER_EU 2
-#endif
-#define CP_PHYS_ATTR __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(CP_WAVES_PER_EU, CP_WAVES_PER_EU)))
-
-__constant__ float kDiscrete[CP_NUM_DISCRETE][2] = {{0.f, 0.f}, {-1.f, 0.f}, {1.f, 0.f}, {0.f, 1.f}, {0.f, -1.f}};
-
-struct Bufs {
-    float* state;      // [CP_STATE_FIELDS][B]
-    float* term_obs;   // [R*14][B]
-    float* bumps;      // [B][ifs][2][2]
-    float* ret_acc;    // [B]
-    float* last_ret;   // [B]
-    int32_t* last_len; // [B]
-    int32_t* overflow; // [B]
-    int32_t* list;     // [B] reset list
-    int32_t* count;    // reset list length (one of the handle's two counters, by step parity)
-    int32_t* count_next;  // the other counter: zeroed by the reset kernel for the next call
-    float* scratch;    // [4*CP_ISLAND_PAIRS][2B] manifold headers of the current substep, per lane
-    uint64_t* stamps;  // [waves][8] diagnostic phase cycles (CP_STAMPS builds only)
-    float* rposes;     // [B][R][4][7] repeat-end poses for the raster obs (NULL: raster off)
-    float4* rtable;    // [C][H*W] (d, t_ground) then [C][H*W] uint8 ground class (cp_raster_table_kernel)
-    int32_t* rlist;    // [B] envs to render after the step kernel
-    int32_t* rcount;   // [1]
-    uint8_t* stepped;  // [B] 1 = simulated by the last cp_step (event log: done-before envs are not logged)
-};
-
-// raster obs: the repeat-end pose of the 4 bodies (xyz, quat xyzw) for the render kernel
-CP_DEV void write_rposes(const Sim& S, float* dst) {
-#pragma unroll
-    for (int d = 0; d < CP_NUM_DYN; ++d) {
-        float* o = dst + d * 7;
-        o[0] = S.b[d].x.x; o[1] = S.b[d].x.y; o[2] = S.b[d].x.z;
-        o[3] = S.b[d].q[0]; o[4] = S.b[d].q[1]; o[5] = S.b[d].q[2]; o[6] = S.b[d].q[3];
-    }
-}
-
-// per-wave stamp accumulation into b.stamps (lane 0 writes; CP_STAMPS builds only)
-CP_DEV void flush_stamps(const Stamps& ST, uint64_t* dst, uint64_t total) {
-#ifdef CP_STAMPS
-    if ((threadIdx.x & (WAVE - 1)) == 0) {
-        atomicAdd((unsigned long long*)&dst[0], (unsigned long long)ST.narrow);
-        atomicAdd((unsigned long long*)&dst[1], (unsigned long long)ST.vel);
-        atomicAdd((unsigned long long*)&dst[2], (unsigned long long)ST.solve);
-        atomicAdd((unsigned long long*)&dst[3], (unsigned long long)ST.integ);
-        atomicAdd((unsigned long long*)&dst[4], (unsigned long long)ST.sweeps);
-        atomicAdd((unsigned long long*)&dst[5], (unsigned long long)ST.substeps);
-        atomicAdd((unsigned long long*)&dst[6], (unsigned long long)total);
-        atomicAdd((unsigned long long*)&dst[7], 1ull);
-        if (ST.bb) {  // narrowphase split into the spare slots 8-10
-            atomicAdd((unsigned long long*)&dst[8], (unsigned long long)ST.sel);
-            atomicAdd((unsigned long long*)&dst[9], (unsigned long long)ST.bb);
-            atomicAdd((unsigned long long*)&dst[10], (unsigned long long)ST.rows);
-        }
-    }
-#else
-    (void)ST; (void)dst; (void)total;
-#endif
-}
-
-
-CP_DEV uint32_t boff(int i) { return (uint32_t)i * 4u; }
-
-CP_DEV void load_sim(Sim& S, const Soa& st, uint32_t o) {
-#pragma unroll
-    for (int d = 0; d < CP_NUM_DYN; ++d) {
-        S.b[d].x = mk(st.ld(CP_SF_BODY(d, 0), o), st.ld(CP_SF_BODY(d, 1), o), st.ld(CP_SF_BODY(d, 2), o));
-#pragma unroll
-        for (int k = 0; k < 4; ++k) S.b[d].q[k] = st.ld(CP_SF_BODY(d, 3 + k), o);
-        S.b[d].v = mk(st.ld(CP_SF_BODY(d, 7), o), st.ld(CP_SF_BODY(d, 8), o), st.ld(CP_SF_BODY(d, 9), o));
-        S.b[d].w = mk(st.ld(CP_SF_BODY(d, 10), o), st.ld(CP_SF_BODY(d, 11), o), st.ld(CP_SF_BODY(d, 12), o));
-    }
-    S.f0 = mk(st.ld(CP_SF_PENDING(0, 0), o), st.ld(CP_SF_PENDING(0, 1), o), st.ld(CP_SF_PENDING(0, 2), o));
-    S.f2 = mk(st.ld(CP_SF_PENDING(1, 0), o), st.ld(CP_SF_PENDING(1, 1), o), st.ld(CP_SF_PENDING(1, 2), o));
-}
-
-CP_DEV void store_sim(const Sim& S, const Soa& st, uint32_t o) {
-#pragma unroll
-    for (int d = 0; d < CP_NUM_DYN; ++d) {
-        st.st(CP_SF_BODY(d, 0), o, S.b[d].x.x);
-        st.st(CP_SF_BODY(d, 1), o, S.b[d].x.y);
-        st.st(CP_SF_BODY(d, 2), o, S.b[d].x.z);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) st.st(CP_SF_BODY(d, 3 + k), o, S.b[d].q[k]);
-        st.st(CP_SF_BODY(d, 7), o, S.b[d].v.x);
-        st.st(CP_SF_BODY(d, 8), o, S.b[d].v.y);
-        st.st(CP_SF_BODY(d, 9), o, S.b[d].v.z);
-        st.st(CP_SF_BODY(d, 10), o, S.b[d].w.x);
-        st.st(CP_SF_BODY(d, 11), o, S.b[d].w.y);
-        st.st(CP_SF_BODY(d, 12), o, S.b[d].w.z);
-    }
-    st.st(CP_SF_PENDING(0, 0), o, S.f0.x);
-    st.st(CP_SF_PENDING(0, 1), o, S.f0.y);
-    st.st(CP_SF_PENDING(0, 2), o, S.f0.z);
-    st.st(CP_SF_PENDING(1, 0), o, S.f2.x);
-    st.st(CP_SF_PENDING(1, 1), o, S.f2.y);
-    st.st(CP_SF_PENDING(1, 2), o, S.f2.z);
-}
-
-CP_DEV int32_t ldi(const Soa& st, int f, uint32_t o) { return __float_as_int(st.ld(f, o)); }
-CP_DEV void sti(const Soa& st, int f, uint32_t o, int32_t v) { st.st(f, o, __int_as_float(v)); }
-
-CP_DEV void write_obs_row(const Sim& S, float* dst) {
-    dst[0] = S.b[0].x.x; dst[1] = S.b[0].x.y; dst[2] = S.b[0].x.z;
-    dst[3] = S.b[0].q[0]; dst[4] = S.b[0].q[1]; dst[5] = S.b[0].q[2]; dst[6] = S.b[0].q[3];
-    dst[7] = S.b[1].x.x; dst[8] = S.b[1].x.y; dst[9] = S.b[1].x.z;
-    dst[10] = S.b[1].q[0]; dst[11] = S.b[1].q[1]; dst[12] = S.b[1].q[2]; dst[13] = S.b[1].q[3];
-}
-
-// 12-state pole readback (bullet_cartpole.py:212-229)
-template <int POLE, int VEL>
-CP_DEV void readback_pole(const Sim& S, float* dst) {
-    const Body& p = S.b[POLE];
-    const Body& vb = S.b[VEL];
-    V3 rpy = quat_euler(p.q[0], p.q[1], p.q[2], p.q[3]);
-    dst[0] = p.x.x; dst[1] = p.x.y; dst[2] = p.x.z;
-    dst[3] = rpy.x; dst[4] = rpy.y; dst[5] = rpy.z;
-    dst[6] = vb.v.x; dst[7] = vb.v.y; dst[8] = vb.v.z;
-    dst[9] = vb.w.x; dst[10] = vb.w.y; dst[11] = vb.w.z;
-}
-
-// ---- closed-loop LQR policy (random_action_agent.py:60-135)
-struct Lqr {
-    const float* gains;  // [B or 1][2 pairs][2 (fx, fy)][8]
-    int per_env;
-    float* state8;       // [B][2][R][S][8] or null
-    float done_pos;      // _check_done thresholds (:108-119); <= 0: no bounds termination
-    float done_angle;
-};
-
-// pole 8-state of pair P (:121-135): x - x0, x', y, y', roll, roll', pitch, pitch'
-template <int P>
-CP_DEV void pole_state8(const Sim& S, float x0, float s[8]) {
-    const Body& p = S.b[2 * P + 1];
-    const V3 rpy = quat_euler(p.q[0], p.q[1], p.q[2], p.q[3]);
-    s[0] = p.x.x - x0; s[1] = p.v.x; s[2] = p.x.y; s[3] = p.v.y;
-    s[4] = rpy.x; s[5] = p.w.x; s[6] = rpy.y; s[7] = p.w.y;
-}
-
-// u = -K s (:92-95, lqr zero point 0), accumulated k = 0..7 with fma
-CP_DEV void lqr_u(const float* K, const float s[8], float& ux, float& uy) {
-    float ax = 0.0f, ay = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        ax = fmaf_(K[k], s[k], ax);
-        ay = fmaf_(K[8 + k], s[k], ay);
-    }
-    ux = -ax;
-    uy = -ay;
-}
-
-CP_DEV bool lqr_out_of_bounds(const float s[8], float pos, float ang) {
-    return fabsf(s[0]) > pos || fabsf(s[2]) > pos || fabsf(s[4]) > ang || fabsf(s[6]) > ang;
-}
-
-// 8-states of both pairs -> next forces; true if both pairs are out of bounds (:908)
-CP_DEV bool lqr_observe(const Sim& S, const cp_config& cfg, const Lqr& q, const float* K, float u[2][2],
-                        float* s8_out) {
-    float s[8];
-    pole_state8<0>(S, cfg.phys.spawn_pos[CP_BODY_POLE][0], s);
-    if (s8_out)
-        for (int k = 0; k < 8; ++k) s8_out[k] = s[k];
-    lqr_u(K, s, u[0][0], u[0][1]);
-    const bool out0 = lqr_out_of_bounds(s, q.done_pos, q.done_angle);
-    pole_state8<1>(S, cfg.phys.spawn_pos[CP_BODY_POLE2][0], s);
-    if (s8_out)
-        for (int k = 0; k < 8; ++k) s8_out[k + 8] = s[k];
-    lqr_u(K + 16, s, u[1][0], u[1][1]);
-    const bool out1 = lqr_out_of_bounds(s, q.done_pos, q.done_angle);
-    return q.done_pos > 0.0f && out0 && out1;
-}
-
-// commented-out bounds check of the reference (:243-253), on the pole pose
-CP_DEV bool bounds_exceeded(const Sim& S, const cp_config& cfg) {
-    const Body& p = S.b[1];
-    if (fabsf(p.x.x) > cfg.pos_threshold || fabsf(p.x.y) > cfg.pos_threshold) return true;
-    float qx = p.q[0], qy = p.q[1], qz = p.q[2], qw = p.q[3];
-    float Y = 2.0f * fmaf_(qy, qz, qw * qx);
-    float X = ((qw * qw - qx * qx) - qy * qy) + qz * qz;
-    bool roll_out = (X > 0.0f) ? (fabsf(Y) > X * cfg.tan_angle_threshold) : !(X == 0.0f && Y == 0.0f);
-    float sarg = -2.0f * fmaf_(qx, qz, -(qw * qy));
-    bool pitch_out = fabsf(sarg) > cfg.sin_angle_threshold;
-    return roll_out || pitch_out;
-}
-
-// Bump force k on cart C (LINK frame), bullet_cartpole.py:354-359
-CP_DEV void bump_force(const cp_config& cfg, const float* bumps, int i, int episode, int k, int c, float& fx,
-                       float& fy) {
-    if (cfg.bump_mode == CP_BUMP_HOST) {
-        const float* f = bumps + (((size_t)i * cfg.initial_force_steps + k) * 2 + c) * 2;
-        fx = f[0];
-        fy = f[1];
-        return;
-    }
-    const float F = cfg.initial_force;
-    if (!cfg.random_theta) {
-        fx = F;
-        fy = F * 0.0f;
-        return;
-    }
-    uint32_t idx = (uint32_t)(2 * k + c);
-    uint64_t gid = (uint64_t)(cfg.env_id_offset + i);
-    uint32_t w = philox_word(idx >> 2, (uint32_t)episode, (uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)cfg.seed,
-                             (uint32_t)(cfg.seed >> 32), (int)(idx & 3u));
-    float u = (float)(w >> 8) * 5.9604644775390625e-08f;
-    float s, co;
-    sincos_turns(u, s, co);
-    fx = F * co;
-    fy = F * s;
-}
-
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) cp_init_kernel(cp_config cfg, Bufs b) {
-    const int B = cfg.num_envs;
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= B) return;
-    const Soa st = Soa::make(b.state, B, CP_STATE_FIELDS);
-    const uint32_t o = boff(i);
-    for (int f = 0; f < CP_STATE_FIELDS; ++f) st.st(f, o, 0.0f);
-#pragma unroll
-    for (int d = 0; d < CP_NUM_DYN; ++d) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) st.st(CP_SF_BODY(d, k), o, cfg.phys.spawn_pos[d + 1][k]);
-        st.st(CP_SF_BODY(d, 6), o, 1.0f);
-    }
-#pragma unroll
-    for (int p = 0; p < CP_NUM_ISLANDS; ++p)
-#pragma unroll
-        for (int j = 0; j < CP_ISLAND_PAIRS; ++j) sti(st, CP_SF_WS_ID(p, j), o, -1);
-    sti(st, CP_SF_DONE, o, 1);  // not reset yet: reference raises, batched API reports done
-    b.ret_acc[i] = 0.0f;
-    b.last_ret[i] = 0.0f;
-    b.last_len[i] = 0;
-    b.overflow[i] = 0;
-}
 
 // env_mask -> compacted list (wave ballot + one atomic per wave)
 __global__ void __launch_bounds__(256) cp_mask_to_list_kernel(int B, const uint8_t* mask, int32_t* list,
@@ -281,214 +46,6 @@ __global__ void __launch_bounds__(256) cp_mask_to_list_kernel(int B, const uint8
     if (lane == 0 && n) base = atomicAdd(count, n);
     base = __shfl(base, 0);
     if (want) list[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
-}
-
-// LAT = false: the throughput shape of the step kernel (2 waves per SIMD), for reset bursts
-// (fixed-length episodes end together).  LAT = true: one wave per SIMD with 512 registers and
-// fast-form rows, for the short lists of desynchronised episodes (bounds termination), where
-// the 130 serial substeps of one wave are the whole latency of the step.
-template <bool LAT>
-__global__ void __launch_bounds__(WAVE)
-__attribute__((amdgpu_waves_per_eu(LAT ? 1 : CP_WAVES_PER_EU, LAT ? 1 : CP_WAVES_PER_EU)))
-cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
-    __shared__ float lds_pool[POOL_FLOATS * WAVE];
-    const int B = cfg.num_envs;
-    const int t = blockIdx.x * WAVE + threadIdx.x;
-    if (t == 0 && b.count_next) *b.count_next = 0;  // the next cp_step's list starts empty
-    const int n = *b.count;
-    if ((t >> 1) >= n) return;  // lane pairs past the compacted list
-    const int isl = t & 1;
-    const bool lead = isl == 0;
-    const int i = b.list[t >> 1];
-    float* pool = lds_pool + threadIdx.x;
-    float* pool0 = lds_pool + (threadIdx.x & ~1u);
-    const Mem G = Mem::make(b.state, b.scratch, B, i, isl);
-    const Lane L = Lane::make(isl, cfg.phys);
-    Stamps ST;
-    Sim S;
-    load_sim(S, G.st, G.off);  // pending forces survive the reset (pybullet keeps them)
-    const int episode = ldi(G.st, CP_SF_EPISODE, G.off);
-#pragma unroll
-    for (int d = 0; d < CP_NUM_DYN; ++d) {
-        S.b[d].x = mk(cfg.phys.spawn_pos[d + 1][0], cfg.phys.spawn_pos[d + 1][1], cfg.phys.spawn_pos[d + 1][2]);
-        S.b[d].q[0] = 0.0f; S.b[d].q[1] = 0.0f; S.b[d].q[2] = 0.0f; S.b[d].q[3] = 1.0f;
-        S.b[d].v = mk(0.0f, 0.0f, 0.0f);
-        S.b[d].w = mk(0.0f, 0.0f, 0.0f);
-    }
-#pragma unroll
-    for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {  // the lane's island's warm-start cache
-        G.sw(CP_SF_WS_ID(0, j), __int_as_float(-1));
-#pragma unroll
-        for (int k = 0; k < 4; ++k) G.sl(CP_SF_WS_LAM(0, j, k), 0.0f);
-    }
-    int ov = 0;
-    const int nsub = cfg.settle_steps + cfg.initial_force_steps;
-    for (int s = 0; s < nsub; ++s) {
-        substep<LAT>(S, cfg.phys, L, pool, pool0, ov, G, ST);
-        const int k = s - cfg.settle_steps;
-        if (k >= 0) {
-            float fx, fy;
-            bump_force(cfg, b.bumps, i, episode, k, 0, fx, fy);
-            apply_force_link<0>(S, fx, fy);
-            bump_force(cfg, b.bumps, i, episode, k, 1, fx, fy);
-            apply_force_link<1>(S, fx, fy);
-        }
-    }
-    ov += (int)partner_u((uint32_t)ov);
-    if (!lead) return;
-    store_sim(S, G.st, G.off);
-    b.overflow[i] += ov;
-    float row[14];
-    write_obs_row(S, row);
-    const int R = cfg.action_repeats;
-    if (b.rposes)  // every repeat slot shows the reset pose (bullet_cartpole.py:342-345)
-        for (int r = 0; r < R; ++r) write_rposes(S, b.rposes + ((size_t)i * R + r) * CP_NUM_DYN * 7);
-    float* o = obs_out + (size_t)i * R * 14;
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-        for (int f = 0; f < 14; ++f) o[r * 14 + f] = row[f];
-    sti(G.st, CP_SF_STEPS, G.off, 0);
-    sti(G.st, CP_SF_DONE, G.off, 0);
-    sti(G.st, CP_SF_EPISODE, G.off, episode + 1);
-    b.ret_acc[i] = 0.0f;
-}
-
-// LAT: the latency shape of cp_reset_kernel<true> (1 wave per SIMD, 512 registers, fast-form
-// rows) for batches whose waves all get a SIMD of their own (<= 32,768 envs)
-template <int KIND, bool LQR, bool LAT>
-__global__ void __launch_bounds__(WAVE)
-__attribute__((amdgpu_waves_per_eu(LAT ? 1 : CP_WAVES_PER_EU, LAT ? 1 : CP_WAVES_PER_EU)))
-cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float* reward_out, uint8_t* done_out,
-               float* term_out, float* readback, int rb_bug, Lqr lq) {
-    __shared__ float lds_pool[POOL_FLOATS * WAVE];
-    const int B = cfg.num_envs;
-    const int t = blockIdx.x * WAVE + threadIdx.x;
-    const int i = t >> 1, isl = t & 1;
-    const bool lead = isl == 0;  // lane 0 of the pair writes the env's outputs
-    const bool inb = i < B;
-    const int R = cfg.action_repeats, SR = cfg.steps_per_repeat;
-    float* pool = lds_pool + threadIdx.x;
-    float* pool0 = lds_pool + (threadIdx.x & ~1u);
-    bool want_reset = false;
-    bool render_me = false;  // simulated this step: its frames go to the render kernel
-    Stamps ST;
-    CP_STAMP(k0);
-    if (inb) {
-        const Mem G = Mem::make(b.state, b.scratch, B, i, isl);
-        const Lane L = Lane::make(isl, cfg.phys);
-        const Soa term = Soa::make(b.term_obs, B, R * 14);
-        float* obs = obs_out + (size_t)i * R * 14;
-        const bool was_done = ldi(G.st, CP_SF_DONE, G.off) != 0;
-        if (lead) b.stepped[i] = was_done ? 0 : 1;
-        if (was_done) {  // step after done (bullet_cartpole.py:179-181)
-            if (lead) {
-                for (int f = 0; f < R * 14; ++f) obs[f] = term.ld(f, G.off);
-                reward_out[i] = 0.0f;
-                done_out[i] = 1;
-            }
-        } else {
-            float a00, a01, a10, a11;
-            if constexpr (KIND == CP_ACTION_CONTINUOUS) {
-                const float4 a = reinterpret_cast<const float4*>(actions)[i];
-                a00 = a.x; a01 = a.y; a10 = a.z; a11 = a.w;
-            } else {
-                const char2 a = reinterpret_cast<const char2*>(actions)[i];
-                int k0 = a.x, k1 = a.y;
-                k0 = (k0 < 0 || k0 >= CP_NUM_DISCRETE) ? 0 : k0;
-                k1 = (k1 < 0 || k1 >= CP_NUM_DISCRETE) ? 0 : k1;
-                a00 = kDiscrete[k0][0]; a01 = kDiscrete[k0][1];
-                a10 = kDiscrete[k1][0]; a11 = kDiscrete[k1][1];
-            }
-            const float F = cfg.action_force;
-            const float f00 = a00 * F, f01 = a01 * F, f10 = a10 * F, f11 = a11 * F;
-            Sim S;
-            load_sim(S, G.st, G.off);
-            int ov = 0;
-            float u[2][2] = {{0.0f, 0.0f}, {0.0f, 0.0f}};  // LQR forces from the last observed state
-            bool lqr_done = false;
-            const float* K = nullptr;
-            if constexpr (LQR) {
-                K = lq.gains + (lq.per_env ? (size_t)i * 32 : 0);
-                lqr_observe(S, cfg, lq, K, u, nullptr);
-            }
-            for (int r = 0; r < R; ++r) {
-                for (int s = 0; s < SR; ++s) {
-                    substep<LAT>(S, cfg.phys, L, pool, pool0, ov, G, ST);
-                    if constexpr (LQR) {  // disturbance + control (:897-901), control from the pre-step state
-                        apply_force_link<0>(S, f00 + u[0][0], f01 + u[0][1]);
-                        apply_force_link<1>(S, f10 + u[1][0], f11 + u[1][1]);
-                        float* s8 = (lq.state8 && lead) ? lq.state8 + (((size_t)i * R + r) * SR + s) * 16 : nullptr;
-                        lqr_done |= lqr_observe(S, cfg, lq, K, u, s8);
-                    } else {
-                        apply_force_link<0>(S, f00, f01);
-                        apply_force_link<1>(S, f10, f11);
-                    }
-                    if (readback && lead) {
-                        float* rb = readback + (size_t)i * 2 * R * SR * 12;
-                        readback_pole<1, 1>(S, rb + ((size_t)(0 * R + r) * SR + s) * 12);
-                        if (rb_bug) readback_pole<3, 1>(S, rb + ((size_t)(1 * R + r) * SR + s) * 12);
-                        else readback_pole<3, 3>(S, rb + ((size_t)(1 * R + r) * SR + s) * 12);
-                    }
-                }
-                if (lead) {
-                    float row[14];
-                    write_obs_row(S, row);
-#pragma unroll
-                    for (int f = 0; f < 14; ++f) obs[r * 14 + f] = row[f];
-                    if (b.rposes) write_rposes(S, b.rposes + ((size_t)i * R + r) * CP_NUM_DYN * 7);
-                }
-            }
-            render_me = lead && b.rposes != nullptr;
-            ov += (int)partner_u((uint32_t)ov);
-            if (ov && lead) b.overflow[i] += ov;
-            const int steps = ldi(G.st, CP_SF_STEPS, G.off) + 1;
-            bool done = steps >= cfg.max_episode_len;
-            if (cfg.done_on_bounds && bounds_exceeded(S, cfg)) done = true;
-            if (LQR && lqr_done) done = true;
-            if (lead) {
-                store_sim(S, G.st, G.off);
-                sti(G.st, CP_SF_STEPS, G.off, steps);
-                reward_out[i] = 1.0f;  // bullet_cartpole.py:260
-                done_out[i] = done ? 1 : 0;
-                const float ret = b.ret_acc[i] + 1.0f;
-                if (done) {
-                    b.last_ret[i] = ret;
-                    b.last_len[i] = steps;
-                    b.ret_acc[i] = 0.0f;
-                    for (int f = 0; f < R * 14; ++f) term.st(f, G.off, obs[f]);
-                    if (term_out)
-                        for (int f = 0; f < R * 14; ++f) term_out[(size_t)i * R * 14 + f] = obs[f];
-                    sti(G.st, CP_SF_DONE, G.off, 1);
-                    want_reset = cfg.autoreset != 0;
-                } else {
-                    b.ret_acc[i] = ret;
-                }
-            }
-        }
-    }
-#ifdef CP_STAMPS
-    CP_STAMP(k1);
-    flush_stamps(ST, b.stamps, k1 - k0);
-#endif
-    if (cfg.autoreset) {
-        // wave ballot compaction of the finishing envs into the reset list
-        const uint64_t bal = __ballot(want_reset);
-        const int lane = threadIdx.x;  // want_reset is set on lead lanes only
-        const int n = __popcll(bal);
-        int base = 0;
-        if (lane == 0 && n) base = atomicAdd(b.count, n);
-        base = __shfl(base, 0);
-        if (want_reset) b.list[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
-    }
-    if (b.rposes) {
-        const uint64_t bal = __ballot(render_me);
-        const int lane = threadIdx.x & (WAVE - 1);
-        const int n = __popcll(bal);
-        int base = 0;
-        if (lane == 0 && n) base = atomicAdd(b.rcount, n);
-        base = __shfl(base, 0);
-        if (render_me) b.rlist[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -585,10 +142,11 @@ struct cp_timing {
 struct cp_handle {
     cp_config cfg;
     int device;
-    cp::Bufs b;
+    cpc::Bufs b;
+    int f64;           // cfg.precision == CP_PRECISION_F64: real = double (namespace cp64)
     float* readback;
     int readback_bug;
-    cp::Lqr lqr;
+    cpc::Lqr lqr;
     cp_timing timing;
     cp_raster_config raster;
     uint16_t* pixels;  // raster obs output (NULL: raster off)
@@ -716,7 +274,9 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
         std::fabs((double)cfg->sin_angle_threshold - std::sin((double)cfg->angle_threshold)) > 1e-6)
         return fail(nullptr, "cp_create: tan/sin_angle_threshold must be tan/sin(angle_threshold)");
     if (!(cfg->phys.residual_threshold >= 0.0f)) return fail(nullptr, "cp_create: negative residual_threshold");
-    if ((unsigned long long)cfg->num_envs * CP_STATE_FIELDS * 4ull >= (1ull << 32) ||
+    if (cfg->precision != CP_PRECISION_F32 && cfg->precision != CP_PRECISION_F64)
+        return fail(nullptr, "cp_create: precision must be CP_PRECISION_F32 or CP_PRECISION_F64");
+    if ((unsigned long long)cfg->num_envs * CP_STATE_FIELDS * (cfg->precision == CP_PRECISION_F64 ? 8ull : 4ull) >= (1ull << 32) ||
         (unsigned long long)cfg->num_envs * cfg->action_repeats * 14ull * 4ull >= (1ull << 32))
         return fail(nullptr, "cp_create: num_envs too large for one handle (SoA arrays must stay below 4 GiB)");
     cp_handle* h = new (std::nothrow) cp_handle();
@@ -725,7 +285,8 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     h->device = device;
     h->readback = nullptr;
     h->readback_bug = 1;
-    h->lqr = cp::Lqr{nullptr, 0, nullptr, 0.0f, 0.0f};
+    h->lqr = cpc::Lqr{nullptr, 0, nullptr, 0.0f, 0.0f};
+    h->f64 = cfg->precision == CP_PRECISION_F64;
     h->pixels = nullptr;
     choose_reset_shape(h);
     cp_default_raster_config(&h->raster);
@@ -742,7 +303,8 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
 #define CP_ALLOC(ptr, bytes)                                   \
     e = hipMalloc((void**)&(ptr), (bytes));                    \
     if (e != hipSuccess) return fail_free(e, "hipMalloc " #ptr);
-    CP_ALLOC(h->b.state, (size_t)CP_STATE_FIELDS * B * sizeof(float));
+    const size_t rb = h->f64 ? sizeof(double) : sizeof(float);  // bytes of the handle's real type
+    CP_ALLOC(h->b.state, (size_t)CP_STATE_FIELDS * B * rb);
     CP_ALLOC(h->b.term_obs, (size_t)R * 14 * B * sizeof(float));
     CP_ALLOC(h->b.bumps, B * (size_t)(cfg->initial_force_steps > 0 ? cfg->initial_force_steps : 1) * 4 * sizeof(float));
     CP_ALLOC(h->b.ret_acc, B * sizeof(float));
@@ -751,7 +313,7 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     CP_ALLOC(h->b.overflow, B * sizeof(int32_t));
     CP_ALLOC(h->b.list, B * sizeof(int32_t));
     CP_ALLOC(h->count2, 2 * sizeof(int32_t));
-    CP_ALLOC(h->b.scratch, (size_t)4 * CP_ISLAND_PAIRS * 2 * B * sizeof(float));
+    CP_ALLOC(h->b.scratch, (size_t)4 * CP_ISLAND_PAIRS * 2 * B * rb);
     CP_ALLOC(h->b.stamps, 16 * sizeof(uint64_t));
     CP_ALLOC(h->b.stepped, B * sizeof(uint8_t));
 #undef CP_ALLOC
@@ -767,7 +329,8 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     if (e != hipSuccess) return fail_free(e, "hipMemset");
     e = hipMemset(h->b.bumps, 0, B * (size_t)(cfg->initial_force_steps > 0 ? cfg->initial_force_steps : 1) * 4 * sizeof(float));
     if (e != hipSuccess) return fail_free(e, "hipMemset");
-    hipLaunchKernelGGL(cp::cp_init_kernel, dim3(grid_for((int)B, 256)), dim3(256), 0, 0, h->cfg, h->b);
+    if (h->f64) cp64::launch_init(h->cfg, h->b, 0);
+    else cp::launch_init(h->cfg, h->b, 0);
     e = hipGetLastError();
     if (e != hipSuccess) return fail_free(e, "cp_init_kernel");
     e = hipDeviceSynchronize();
@@ -849,12 +412,8 @@ static int launch_reset_from_list(cp_handle* h, float* obs_out, hipStream_t st, 
     const int B = h->cfg.num_envs;
     hipEvent_t* ev = timing_slot(h, 1);
     if (ev) CP_TRY(h, hipEventRecord(ev[0], st));
-    if (h->reset_lat)
-        hipLaunchKernelGGL(cp::cp_reset_kernel<true>, dim3(grid_for(2 * B, cp::WAVE)), dim3(cp::WAVE), 0, st, h->cfg,
-                           h->b, obs_out);
-    else
-        hipLaunchKernelGGL(cp::cp_reset_kernel<false>, dim3(grid_for(2 * B, cp::WAVE)), dim3(cp::WAVE), 0, st, h->cfg,
-                           h->b, obs_out);
+    if (h->f64) cp64::launch_reset(true, h->cfg, h->b, obs_out, st);
+    else cp::launch_reset(h->reset_lat != 0, h->cfg, h->b, obs_out, st);
     if (check(h, hipGetLastError(), "cp_reset_kernel")) return -1;
     if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
     if (render && h->pixels) return launch_render(h, h->b.list, h->b.count, st);
@@ -884,29 +443,14 @@ int cp_step(cp_handle* h, const void* actions, int action_kind, float* obs_out, 
     CP_TRY(h, hipSetDevice(h->device));
     if (h->cfg.autoreset) use_counter(h);  // zeroed by the previous call's reset launch
     if (h->pixels) CP_TRY(h, hipMemsetAsync(h->b.rcount, 0, sizeof(int32_t), st));
-    dim3 grid(grid_for(2 * B, cp::WAVE)), block(cp::WAVE);  // two lanes per env
     hipEvent_t* ev = timing_slot(h, 0);
     if (ev) CP_TRY(h, hipEventRecord(ev[0], st));
-    const bool lqr = h->lqr.gains != nullptr;
-#define CP_LAUNCH_STEP(K, Q)                                                                                    \
-    do {                                                                                                        \
-        if (h->step_lat)                                                                                        \
-            hipLaunchKernelGGL((cp::cp_step_kernel<K, Q, true>), grid, block, 0, st, h->cfg, h->b, actions,     \
-                               obs_out, reward_out, done_out, terminal_obs_out, h->readback, h->readback_bug,    \
-                               h->lqr);                                                                         \
-        else                                                                                                    \
-            hipLaunchKernelGGL((cp::cp_step_kernel<K, Q, false>), grid, block, 0, st, h->cfg, h->b, actions,    \
-                               obs_out, reward_out, done_out, terminal_obs_out, h->readback, h->readback_bug,    \
-                               h->lqr);                                                                         \
-    } while (0)
-    if (action_kind == CP_ACTION_CONTINUOUS) {
-        if (lqr) CP_LAUNCH_STEP(CP_ACTION_CONTINUOUS, true);
-        else CP_LAUNCH_STEP(CP_ACTION_CONTINUOUS, false);
-    } else {
-        if (lqr) CP_LAUNCH_STEP(CP_ACTION_DISCRETE, true);
-        else CP_LAUNCH_STEP(CP_ACTION_DISCRETE, false);
-    }
-#undef CP_LAUNCH_STEP
+    if (h->f64)
+        cp64::launch_step(true, action_kind, h->cfg, h->b, actions, obs_out, reward_out, done_out, terminal_obs_out,
+                          h->readback, h->readback_bug, h->lqr, st);
+    else
+        cp::launch_step(h->step_lat != 0, action_kind, h->cfg, h->b, actions, obs_out, reward_out, done_out,
+                        terminal_obs_out, h->readback, h->readback_bug, h->lqr, st);
     CP_TRY(h, hipGetLastError());
     if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
     // autoreset envs were simulated this step, so they are in the render list; the reset
@@ -948,7 +492,8 @@ int cp_get_state(cp_handle* h, float* state_out, void* stream) {
     if (!h || !state_out) return fail(h, "cp_get_state: null argument");
     CP_TRY(h, hipSetDevice(h->device));
     size_t n = (size_t)CP_STATE_FIELDS * h->cfg.num_envs;
-    CP_TRY(h, hipMemcpyAsync(state_out, h->b.state, n * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    CP_TRY(h, hipMemcpyAsync(state_out, h->b.state, n * (h->f64 ? sizeof(double) : sizeof(float)), hipMemcpyDeviceToDevice,
+                             (hipStream_t)stream));
     return 0;
 }
 
@@ -956,7 +501,8 @@ int cp_set_state(cp_handle* h, const float* state_in, void* stream) {
     if (!h || !state_in) return fail(h, "cp_set_state: null argument");
     CP_TRY(h, hipSetDevice(h->device));
     size_t n = (size_t)CP_STATE_FIELDS * h->cfg.num_envs;
-    CP_TRY(h, hipMemcpyAsync(h->b.state, state_in, n * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    CP_TRY(h, hipMemcpyAsync(h->b.state, state_in, n * (h->f64 ? sizeof(double) : sizeof(float)), hipMemcpyDeviceToDevice,
+                             (hipStream_t)stream));
     return 0;
 }
 

@@ -10,13 +10,15 @@
 // env with a cross-island contact is solved by both lanes redundantly in the
 // global order.  The algorithm is DESIGN.md §Physics model; the CPU
 // oracle (oracle/cp_oracle.c) states the same arithmetic, operation for operation.
-#pragma once
-#include "../../include/cartpole_amd.h"
-#include "cp_math.h"
+// Written over `real`; included after cp_math.h once per real type (cp_common.h).
+#if !defined(CP_NS) || !defined(CP_REAL)
+#error "define CP_NS and CP_REAL before including cp_physics.h (see cp_kernels.hip)"
+#endif
+#include "cp_common.h"
 
 #include <type_traits>
 
-namespace cp {
+namespace CP_NS {
 
 // Diagnostic phase stamps (built only with -DCP_STAMPS; see cp_debug_stamps).
 // Wave-uniform cycle counters from s_memtime, accumulated per wave.
@@ -42,8 +44,8 @@ constexpr int NPF = 6;
 constexpr int FF_L1 = 0, FF_L2 = 1, FF_IE1 = 2, FF_IE2 = 3;
 constexpr int POOL_FLOATS = NPF * MAXP + 4 * MAXF;  // 80 floats per lane = 20 KiB per wave
 
-CP_DEV float& pool_n(float* pool, int field, int slot) { return pool[(field * MAXP + slot) * WAVE]; }
-CP_DEV float& pool_f(float* pool, int field, int slot) { return pool[(NPF * MAXP + field * MAXF + slot) * WAVE]; }
+CP_DEV real& pool_n(real* pool, int field, int slot) { return pool[(field * MAXP + slot) * WAVE]; }
+CP_DEV real& pool_f(real* pool, int field, int slot) { return pool[(NPF * MAXP + field * MAXF + slot) * WAVE]; }
 
 // body pairs (a < b), Bullet-like order over the loadURDF ids
 __host__ __device__ constexpr int pair_a(int p) {
@@ -55,7 +57,7 @@ __host__ __device__ constexpr int pair_b(int p) {
 
 struct Body {
     V3 x, v, w;
-    float q[4];
+    real q[4];
 };
 
 // Per-env simulation state held in registers for the duration of a kernel.
@@ -65,72 +67,51 @@ struct Sim {
 };
 
 // Per-env global memory touched once per substep (cold data kept out of VGPRs):
-// the warm-start cache lives in the state SoA, the manifold headers of the
-// current substep are staged in a [4*CP_NUM_PAIRS][B] scratch.
-// SoA field access through a buffer resource: the field base is a wave-uniform
-// SGPR soffset (f * B * 4) and the env is a 32-bit VGPR voffset (i * 4), so each
-// env keeps one offset register instead of a 64-bit address per field (the flat
-// form made the compiler hoist and spill ~100 of them).  Limits one SoA array to
-// 4 GiB: B * fields * 4 < 2^32 (checked at cp_create).
-struct Soa {
-    __amdgpu_buffer_rsrc_t r;
-    uint32_t fstride;  // B * 4 bytes
-    CP_DEV static Soa make(float* base, int B, int fields) {
-        Soa s;
-        s.r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)((uint32_t)B * 4u * (uint32_t)fields), 0x00020000);
-        s.fstride = (uint32_t)B * 4u;
-        return s;
-    }
-    CP_DEV float ld(int f, uint32_t off) const {
-        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, (int)((uint32_t)f * fstride), 0));
-    }
-    CP_DEV void st(int f, uint32_t off, float v) const {
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)off, (int)((uint32_t)f * fstride), 0);
-    }
-};
+// the warm-start cache lives in the state SoA (SoaT: buffer-resource access, cp_common.h).
+using Soa = SoaT<real>;
 struct Mem {
     Soa st;           // state SoA [CP_STATE_FIELDS][B]
     Soa scr;          // scratch SoA [4*CP_ISLAND_PAIRS][2B], one column per lane
-    uint32_t off;     // env index * 4
+    uint32_t off;     // env index * sizeof(real)
     uint32_t woff;    // off + island * CP_ISLAND_PAIRS fields  (warm-start ids of the lane's island)
     uint32_t loff;    // off + island * 4*CP_ISLAND_PAIRS fields (warm-start impulses)
-    uint32_t xoff;    // (2 * env + island) * 4
-    CP_DEV static Mem make(float* state, float* scratch, int B, int env, int isl) {
+    uint32_t xoff;    // (2 * env + island) * sizeof(real)
+    CP_DEV static Mem make(void* state, void* scratch, int B, int env, int isl) {
         Mem m;
         m.st = Soa::make(state, B, CP_STATE_FIELDS);
         m.scr = Soa::make(scratch, 2 * B, 4 * CP_ISLAND_PAIRS);
-        m.off = (uint32_t)env * 4u;
+        m.off = Soa::eoff(env);
         m.woff = m.off + (uint32_t)(isl * CP_ISLAND_PAIRS) * m.st.fstride;
         m.loff = m.off + (uint32_t)(isl * 4 * CP_ISLAND_PAIRS) * m.st.fstride;
-        m.xoff = (uint32_t)(2 * env + isl) * 4u;
+        m.xoff = Soa::eoff(2 * env + isl);
         return m;
     }
-    CP_DEV float ls(int f) const { return st.ld(f, off); }
-    CP_DEV void ss(int f, float v) const { st.st(f, off, v); }
-    CP_DEV float lw(int f) const { return st.ld(f, woff); }
-    CP_DEV void sw(int f, float v) const { st.st(f, woff, v); }
-    CP_DEV float ll(int f) const { return st.ld(f, loff); }
-    CP_DEV void sl(int f, float v) const { st.st(f, loff, v); }
-    CP_DEV float lx(int f) const { return scr.ld(f, xoff); }
-    CP_DEV void sx(int f, float v) const { scr.st(f, xoff, v); }
+    CP_DEV real ls(int f) const { return st.ld(f, off); }
+    CP_DEV void ss(int f, real v) const { st.st(f, off, v); }
+    CP_DEV real lw(int f) const { return st.ld(f, woff); }
+    CP_DEV void sw(int f, real v) const { st.st(f, woff, v); }
+    CP_DEV real ll(int f) const { return st.ld(f, loff); }
+    CP_DEV void sl(int f, real v) const { st.st(f, loff, v); }
+    CP_DEV real lx(int f) const { return scr.ld(f, xoff); }
+    CP_DEV void sx(int f, real v) const { scr.st(f, xoff, v); }
 };
 
 struct Box {
     V3 c;
     Axes ax;
-    float h0, h1, h2;
+    real h0, h1, h2;
 };
 
 // component-wise selects (a struct-valued ?: lets the compiler build the operands in scratch)
-CP_DEV float sel3(float a, float b, float c, int i) { return i == 0 ? a : (i == 1 ? b : c); }
+CP_DEV real sel3(real a, real b, real c, int i) { return i == 0 ? a : (i == 1 ? b : c); }
 CP_DEV V3 sel3v(V3 a, V3 b, V3 c, int i) { return mk(sel3(a.x, b.x, c.x, i), sel3(a.y, b.y, c.y, i), sel3(a.z, b.z, c.z, i)); }
 CP_DEV V3 selv(bool t, V3 a, V3 b) { return mk(t ? a.x : b.x, t ? a.y : b.y, t ? a.z : b.z); }
 CP_DEV V3 axis_of(const Axes& A, int i) { return sel3v(A.a0, A.a1, A.a2, i); }
-CP_DEV float h_of(const Box& B, int i) { return i == 0 ? B.h0 : (i == 1 ? B.h1 : B.h2); }
+CP_DEV real h_of(const Box& B, int i) { return i == 0 ? B.h0 : (i == 1 ? B.h1 : B.h2); }
 
 // contact point candidate (reference-face coordinates u, v and separation n)
 struct Out4 {
-    float u[4] = {0, 0, 0, 0}, v[4] = {0, 0, 0, 0}, n[4] = {0, 0, 0, 0};
+    real u[4] = {0, 0, 0, 0}, v[4] = {0, 0, 0, 0}, n[4] = {0, 0, 0, 0};
     int id[4] = {0, 0, 0, 0};
     int m = 0;
 };
@@ -138,10 +119,10 @@ struct Out4 {
 // Face-contact geometry in reference-face coordinates (u, v along the face, n
 // along its normal): incident-face centre c, half edges e1, e2, vertices P[4].
 struct FaceGeom {
-    float hu, hv, margin;
-    float cu, cv, cn, e1u, e1v, e1n, e2u, e2v, e2n;
-    float Pu[4], Pv[4], Pn[4];
-    float idet;
+    real hu, hv, margin;
+    real cu, cv, cn, e1u, e1v, e1n, e2u, e2v, e2n;
+    real Pu[4], Pv[4], Pn[4];
+    real idet;
     bool all_in;  // all four incident vertices inside the reference rectangle: C1 only
 };
 
@@ -149,38 +130,38 @@ struct FaceGeom {
 // and whether it is kept.  Same arithmetic as the oracle's candidate loops; the
 // candidates are re-evaluated per pass instead of stored (72 registers saved).
 template <int K>
-CP_DEV bool cand(const FaceGeom& G, float& u, float& v, float& n) {
+CP_DEV bool cand(const FaceGeom& G, real& u, real& v, real& n) {
     if constexpr (K < 4) {
         u = G.Pu[K]; v = G.Pv[K]; n = G.Pn[K];
-        return fabsf(G.Pu[K]) <= G.hu && fabsf(G.Pv[K]) <= G.hv && G.Pn[K] <= G.margin;
+        return abs_(G.Pu[K]) <= G.hu && abs_(G.Pv[K]) <= G.hv && G.Pn[K] <= G.margin;
     } else if constexpr (K < 8) {
         constexpr int c = K - 4;
-        const float X = (c == 0 || c == 3) ? G.hu : -G.hu;
-        const float Y = (c < 2) ? G.hv : -G.hv;
-        const float ru = X - G.cu, rv = Y - G.cv;
-        const float al = fmaf_(ru, G.e2v, -(rv * G.e2u)) * G.idet;
-        const float be = fmaf_(G.e1u, rv, -(G.e1v * ru)) * G.idet;
-        const float dn = fmaf_(be, G.e2n, fmaf_(al, G.e1n, G.cn));
+        const real X = (c == 0 || c == 3) ? G.hu : -G.hu;
+        const real Y = (c < 2) ? G.hv : -G.hv;
+        const real ru = X - G.cu, rv = Y - G.cv;
+        const real al = fma_(ru, G.e2v, -(rv * G.e2u)) * G.idet;
+        const real be = fma_(G.e1u, rv, -(G.e1v * ru)) * G.idet;
+        const real dn = fma_(be, G.e2n, fma_(al, G.e1n, G.cn));
         u = X; v = Y; n = dn;
-        return !G.all_in && fabsf(al) < 1.0f && fabsf(be) < 1.0f && dn <= G.margin;
+        return !G.all_in && abs_(al) < real(1.0) && abs_(be) < real(1.0) && dn <= G.margin;
     } else {
         constexpr int k = (K - 8) / 4, sd = (K - 8) % 4, k1 = (k + 1) & 3;
-        const float lim = (sd & 1) ? ((sd < 2) ? -G.hu : -G.hv) : ((sd < 2) ? G.hu : G.hv);
-        const float pc = (sd < 2) ? G.Pu[k] : G.Pv[k], qc = (sd < 2) ? G.Pu[k1] : G.Pv[k1];
-        const float dp = pc - lim, dq = qc - lim;
-        const bool cross_ = (dp < 0.0f && dq > 0.0f) || (dp > 0.0f && dq < 0.0f);
-        const float t = dp / (dp - dq);
+        const real lim = (sd & 1) ? ((sd < 2) ? -G.hu : -G.hv) : ((sd < 2) ? G.hu : G.hv);
+        const real pc = (sd < 2) ? G.Pu[k] : G.Pv[k], qc = (sd < 2) ? G.Pu[k1] : G.Pv[k1];
+        const real dp = pc - lim, dq = qc - lim;
+        const bool cross_ = (dp < real(0.0) && dq > real(0.0)) || (dp > real(0.0) && dq < real(0.0));
+        const real t = dp / (dp - dq);
         bool inr;
         if constexpr (sd < 2) {
             u = lim;
-            v = fmaf_(G.Pv[k1] - G.Pv[k], t, G.Pv[k]);
-            inr = fabsf(v) <= G.hv;
+            v = fma_(G.Pv[k1] - G.Pv[k], t, G.Pv[k]);
+            inr = abs_(v) <= G.hv;
         } else {
             v = lim;
-            u = fmaf_(G.Pu[k1] - G.Pu[k], t, G.Pu[k]);
-            inr = fabsf(u) <= G.hu;
+            u = fma_(G.Pu[k1] - G.Pu[k], t, G.Pu[k]);
+            inr = abs_(u) <= G.hu;
         }
-        n = fmaf_(G.Pn[k1] - G.Pn[k], t, G.Pn[k]);
+        n = fma_(G.Pn[k1] - G.Pn[k], t, G.Pn[k]);
         return !G.all_in && cross_ && inr && n <= G.margin;
     }
 }
@@ -189,7 +170,7 @@ CP_DEV bool cand(const FaceGeom& G, float& u, float& v, float& n) {
 template <int K = 0, typename Fn>
 CP_DEV void for_cands(const FaceGeom& G, Fn&& fn) {
     if constexpr (K < 24) {
-        float u, v, n;
+        real u, v, n;
         const bool ok = cand<K>(G, u, v, n);
         fn(K, ok, u, v, n);
         for_cands<K + 1>(G, fn);
@@ -197,7 +178,7 @@ CP_DEV void for_cands(const FaceGeom& G, Fn&& fn) {
 }
 
 // Face contact (oracle: face_contact).  Fills up to 4 selected candidates.
-CP_DEV void face_contact(const Box& R, int ri, V3 nr, const Box& I, float margin, V3& fc, V3& u, V3& v,
+CP_DEV void face_contact(const Box& R, int ri, V3 nr, const Box& I, real margin, V3& fc, V3& u, V3& v,
                          Out4& out) {
     int r1 = ri == 2 ? 0 : ri + 1, r2 = ri == 0 ? 2 : ri - 1;
     fc = madd(R.c, nr, h_of(R, ri));
@@ -207,13 +188,13 @@ CP_DEV void face_contact(const Box& R, int ri, V3 nr, const Box& I, float margin
     G.margin = margin;
     G.hu = h_of(R, r1);
     G.hv = h_of(R, r2);
-    float e0 = dot(nr, I.ax.a0), e1d = dot(nr, I.ax.a1), e2d = dot(nr, I.ax.a2);
+    real e0 = dot(nr, I.ax.a0), e1d = dot(nr, I.ax.a1), e2d = dot(nr, I.ax.a2);
     int j = 0;
-    float best = fabsf(e0);
-    if (fabsf(e1d) > best) { j = 1; best = fabsf(e1d); }
-    if (fabsf(e2d) > best) { j = 2; }
-    float ej = sel3(e0, e1d, e2d, j);
-    float isg = (ej > 0.0f) ? -1.0f : 1.0f;
+    real best = abs_(e0);
+    if (abs_(e1d) > best) { j = 1; best = abs_(e1d); }
+    if (abs_(e2d) > best) { j = 2; }
+    real ej = sel3(e0, e1d, e2d, j);
+    real isg = (ej > real(0.0)) ? -real(1.0) : real(1.0);
     V3 ic = madd(I.c, axis_of(I.ax, j), isg * h_of(I, j));
     int j1 = j == 2 ? 0 : j + 1, j2 = j == 0 ? 2 : j - 1;
     V3 E1 = scl(axis_of(I.ax, j1), h_of(I, j1));
@@ -228,18 +209,18 @@ CP_DEV void face_contact(const Box& R, int ri, V3 nr, const Box& I, float margin
     G.Pu[3] = (G.cu + G.e1u) - G.e2u; G.Pv[3] = (G.cv + G.e1v) - G.e2v; G.Pn[3] = (G.cn + G.e1n) - G.e2n;
     int inside = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) inside += (fabsf(G.Pu[k]) <= G.hu && fabsf(G.Pv[k]) <= G.hv) ? 1 : 0;
+    for (int k = 0; k < 4; ++k) inside += (abs_(G.Pu[k]) <= G.hu && abs_(G.Pv[k]) <= G.hv) ? 1 : 0;
     G.all_in = inside == 4;
-    G.idet = 0.0f;
+    G.idet = real(0.0);
     if (!G.all_in) {
-        float det = fmaf_(G.e1u, G.e2v, -(G.e1v * G.e2u));
-        G.idet = 1.0f / det;
+        real det = fma_(G.e1u, G.e2v, -(G.e1v * G.e2u));
+        G.idet = real(1.0) / det;
     }
     // pass 1: valid set and the deepest candidate (first minimum in canonical order)
     uint32_t valid = 0;
     int i0 = -1;
-    float bn = 0.0f, u0 = 0.0f, v0 = 0.0f;
-    for_cands(G, [&](int k, bool ok, float cu_, float cv_, float cn_) {
+    real bn = real(0.0), u0 = real(0.0), v0 = real(0.0);
+    for_cands(G, [&](int k, bool ok, real cu_, real cv_, real cn_) {
         if (ok) {
             valid |= 1u << k;
             if (i0 < 0 || cn_ < bn) { i0 = k; bn = cn_; u0 = cu_; v0 = cv_; }
@@ -249,33 +230,33 @@ CP_DEV void face_contact(const Box& R, int ri, V3 nr, const Box& I, float margin
     if (__builtin_popcount(valid) > 4) {
         // deepest; farthest from it; max / min signed area  (oracle: same rule)
         int i1 = -1;
-        float bd = 0.0f, u1 = 0.0f, v1 = 0.0f;
-        for_cands(G, [&](int k, bool ok, float cu_, float cv_, float) {
+        real bd = real(0.0), u1 = real(0.0), v1 = real(0.0);
+        for_cands(G, [&](int k, bool ok, real cu_, real cv_, real) {
             if (!ok || k == i0) return;
-            float du = cu_ - u0, dv = cv_ - v0;
-            float d2 = fmaf_(du, du, dv * dv);
+            real du = cu_ - u0, dv = cv_ - v0;
+            real d2 = fma_(du, du, dv * dv);
             if (i1 < 0 || d2 > bd) { i1 = k; bd = d2; u1 = cu_; v1 = cv_; }
         });
-        const float ex = u1 - u0, ey = v1 - v0;
+        const real ex = u1 - u0, ey = v1 - v0;
         int i2 = -1;
-        float ba = 0.0f;
-        for_cands(G, [&](int k, bool ok, float cu_, float cv_, float) {
+        real ba = real(0.0);
+        for_cands(G, [&](int k, bool ok, real cu_, real cv_, real) {
             if (!ok || k == i0 || k == i1) return;
-            float ar = fmaf_(ex, cv_ - v0, -(ey * (cu_ - u0)));
+            real ar = fma_(ex, cv_ - v0, -(ey * (cu_ - u0)));
             if (i2 < 0 || ar > ba) { i2 = k; ba = ar; }
         });
         int i3 = -1;
-        float bb = 0.0f;
-        for_cands(G, [&](int k, bool ok, float cu_, float cv_, float) {
+        real bb = real(0.0);
+        for_cands(G, [&](int k, bool ok, real cu_, real cv_, real) {
             if (!ok || k == i0 || k == i1 || k == i2) return;
-            float ar = fmaf_(ex, cv_ - v0, -(ey * (cu_ - u0)));
+            real ar = fma_(ex, cv_ - v0, -(ey * (cu_ - u0)));
             if (i3 < 0 || ar < bb) { i3 = k; bb = ar; }
         });
         sel = (1u << i0) | (1u << i1) | (1u << i2) | (1u << i3);
     }
     // emit the selected candidates in canonical order
     out.m = 0;
-    for_cands(G, [&](int k, bool, float cu_, float cv_, float cn_) {
+    for_cands(G, [&](int k, bool, real cu_, real cv_, real cn_) {
         if ((sel >> k) & 1u) {
             const int m = out.m;
 #pragma unroll
@@ -297,45 +278,45 @@ struct Contact {
     V3 n;          // from A to B
     int m;         // points
     V3 p[4];       // world contact points (midway between the surfaces)
-    float d[4];    // signed separation (negative = penetration)
+    real d[4];    // signed separation (negative = penetration)
     int id[4];     // feature ids (warm-start keys)
 };
 
 // Box-box narrowphase (oracle: box_box).  Normal from A to B.
-CP_DEV void box_box(const Box& A, const Box& B, float margin, float edge_bias, Contact& C) {
+CP_DEV void box_box(const Box& A, const Box& B, real margin, real edge_bias, Contact& C) {
     C.m = 0;
     V3 d = sub(B.c, A.c);
     V3 Aax[3] = {A.ax.a0, A.ax.a1, A.ax.a2};
     V3 Bax[3] = {B.ax.a0, B.ax.a1, B.ax.a2};
-    float Ah[3] = {A.h0, A.h1, A.h2}, Bh[3] = {B.h0, B.h1, B.h2};
-    float Cm[3][3], AC[3][3], da[3], db[3];
+    real Ah[3] = {A.h0, A.h1, A.h2}, Bh[3] = {B.h0, B.h1, B.h2};
+    real Cm[3][3], AC[3][3], da[3], db[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
             Cm[i][j] = dot(Aax[i], Bax[j]);
-            AC[i][j] = fabsf(Cm[i][j]);
+            AC[i][j] = abs_(Cm[i][j]);
         }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         da[i] = dot(d, Aax[i]);
         db[i] = dot(d, Bax[i]);
     }
-    float best = 0.0f;
+    real best = real(0.0);
     int kind = 0, bi = 0, bj = 0;
-    V3 bax = mk(0.0f, 0.0f, 0.0f);
+    V3 bax = mk(real(0.0), real(0.0), real(0.0));
     bool sep = false;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-        float pr = fmaf_(Bh[0], AC[i][0], fmaf_(Bh[1], AC[i][1], Bh[2] * AC[i][2]));
-        float s = fabsf(da[i]) - (Ah[i] + pr);
+        real pr = fma_(Bh[0], AC[i][0], fma_(Bh[1], AC[i][1], Bh[2] * AC[i][2]));
+        real s = abs_(da[i]) - (Ah[i] + pr);
         sep = sep || (s > margin);
         if (i == 0 || s > best) { best = s; kind = 0; bi = i; }
     }
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-        float pr = fmaf_(Ah[0], AC[0][j], fmaf_(Ah[1], AC[1][j], Ah[2] * AC[2][j]));
-        float s = fabsf(db[j]) - (Bh[j] + pr);
+        real pr = fma_(Ah[0], AC[0][j], fma_(Ah[1], AC[1][j], Ah[2] * AC[2][j]));
+        real s = abs_(db[j]) - (Bh[j] + pr);
         sep = sep || (s > margin);
         if (s > best) { best = s; kind = 1; bj = j; }
     }
@@ -345,13 +326,13 @@ CP_DEV void box_box(const Box& A, const Box& B, float margin, float edge_bias, C
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
             V3 ax = cross(Aax[i], Bax[j]);
-            float L2 = dot(ax, ax);
-            if (L2 < 1e-6f) continue;
-            float L = sqrtf(L2);
+            real L2 = dot(ax, ax);
+            if (L2 < real(1e-6)) continue;
+            real L = sqrt_(L2);
             const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
-            float ra = fmaf_(Ah[i1], AC[i2][j], Ah[i2] * AC[i1][j]);
-            float rb = fmaf_(Bh[j1], AC[i][j2], Bh[j2] * AC[i][j1]);
-            float num = fabsf(dot(d, ax)) - (ra + rb);   // separation * L
+            real ra = fma_(Ah[i1], AC[i2][j], Ah[i2] * AC[i1][j]);
+            real rb = fma_(Bh[j1], AC[i][j2], Bh[j2] * AC[i][j1]);
+            real num = abs_(dot(d, ax)) - (ra + rb);   // separation * L
             sep = sep || (num > margin * L);
             if (num > (best + edge_bias) * L) { best = num / L; kind = 2; bi = i; bj = j; bax = ax; }
         }
@@ -361,8 +342,8 @@ CP_DEV void box_box(const Box& A, const Box& B, float margin, float edge_bias, C
         // face of A (kind 0) or face of B (kind 1) is the reference face
         const bool fa = kind == 0;
         int ri = fa ? bi : bj;
-        float sg = fa ? ((sel3(da[0], da[1], da[2], bi) >= 0.0f) ? 1.0f : -1.0f)
-                      : ((sel3(db[0], db[1], db[2], bj) >= 0.0f) ? -1.0f : 1.0f);
+        real sg = fa ? ((sel3(da[0], da[1], da[2], bi) >= real(0.0)) ? real(1.0) : -real(1.0))
+                      : ((sel3(db[0], db[1], db[2], bj) >= real(0.0)) ? -real(1.0) : real(1.0));
         Box R, I;
         R.c = selv(fa, A.c, B.c);
         R.ax.a0 = selv(fa, A.ax.a0, B.ax.a0);
@@ -383,54 +364,54 @@ CP_DEV void box_box(const Box& A, const Box& B, float margin, float edge_bias, C
         C.m = o.m;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            C.p[k] = madd(madd(madd(fc, u, o.u[k]), v, o.v[k]), nr, o.n[k] * 0.5f);
+            C.p[k] = madd(madd(madd(fc, u, o.u[k]), v, o.v[k]), nr, o.n[k] * real(0.5));
             C.d[k] = o.n[k];
             C.id[k] = o.id[k] + code;
         }
         return;
     }
     // edge-edge
-    float L = sqrtf(dot(bax, bax));
+    real L = sqrt_(dot(bax, bax));
     V3 w = mk(bax.x / L, bax.y / L, bax.z / L);
-    w = selv(dot(w, d) < 0.0f, neg(w), w);
+    w = selv(dot(w, d) < real(0.0), neg(w), w);
     C.n = w;
     V3 pa = A.c, pb = B.c;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        float sg = (dot(Aax[k], w) > 0.0f) ? 1.0f : -1.0f;
+        real sg = (dot(Aax[k], w) > real(0.0)) ? real(1.0) : -real(1.0);
         if (k != bi) pa = madd(pa, Aax[k], sg * Ah[k]);
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        float sg = (dot(Bax[k], w) > 0.0f) ? -1.0f : 1.0f;
+        real sg = (dot(Bax[k], w) > real(0.0)) ? -real(1.0) : real(1.0);
         if (k != bj) pb = madd(pb, Bax[k], sg * Bh[k]);
     }
     V3 ua = axis_of(A.ax, bi), ub = axis_of(B.ax, bj);
     V3 r = sub(pb, pa);
-    float c = dot(ua, ub), ar = dot(ua, r), br = dot(ub, r);
-    float den = fmaf_(-c, c, 1.0f);
-    float s = fmaf_(-c, br, ar) / den;
-    float t = fmaf_(c, ar, -br) / den;
-    float ha = sel3(A.h0, A.h1, A.h2, bi), hb = sel3(B.h0, B.h1, B.h2, bj);
+    real c = dot(ua, ub), ar = dot(ua, r), br = dot(ub, r);
+    real den = fma_(-c, c, real(1.0));
+    real s = fma_(-c, br, ar) / den;
+    real t = fma_(c, ar, -br) / den;
+    real ha = sel3(A.h0, A.h1, A.h2, bi), hb = sel3(B.h0, B.h1, B.h2, bj);
     s = s > ha ? ha : (s < -ha ? -ha : s);
     t = t > hb ? hb : (t < -hb ? -hb : t);
     V3 qa = madd(pa, ua, s), qb = madd(pb, ub, t);
     C.m = 1;
-    C.p[0] = scl(add(qa, qb), 0.5f);
+    C.p[0] = scl(add(qa, qb), real(0.5));
     C.d[0] = best;
     C.id[0] = 6 * 32 + 3 * bi + bj;
 }
 
 CP_DEV void plane_space(V3 n, V3& t1, V3& t2) {
-    if (fabsf(n.z) > (float)0.7071067811865476) {
-        float a = fmaf_(n.y, n.y, n.z * n.z);
-        float k = 1.0f / sqrtf(a);
-        t1 = mk(0.0f, -(n.z * k), n.y * k);
+    if (abs_(n.z) > (real)0.7071067811865476) {
+        real a = fma_(n.y, n.y, n.z * n.z);
+        real k = real(1.0) / sqrt_(a);
+        t1 = mk(real(0.0), -(n.z * k), n.y * k);
         t2 = mk(a * k, -(n.x * t1.z), n.x * t1.y);
     } else {
-        float a = fmaf_(n.x, n.x, n.y * n.y);
-        float k = 1.0f / sqrtf(a);
-        t1 = mk(-(n.y * k), n.x * k, 0.0f);
+        real a = fma_(n.x, n.x, n.y * n.y);
+        real k = real(1.0) / sqrt_(a);
+        t1 = mk(-(n.y * k), n.x * k, real(0.0));
         t2 = mk(-(n.z * t1.y), n.z * t1.x, a * k);
     }
 }
@@ -440,10 +421,6 @@ CP_DEV void plane_space(V3 n, V3& t1, V3& t2) {
 // p: island 0 = ground, cart, pole (pairs 0 1 4) plus the
 // cross pairs 5 6; island 1 = ground, cart2, pole2 (pairs 2 3 9) plus 7 8.  Both
 // lanes keep the whole env state; they exchange results through DPP swaps.
-CP_DEV float partner(float x) {
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
-}
-CP_DEV uint32_t partner_u(uint32_t x) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false); }
 CP_DEV V3 partner(V3 v) { return mk(partner(v.x), partner(v.y), partner(v.z)); }
 
 // global pair of island `isl`'s local pair j (oracle: ISLAND_PAIR)
@@ -456,9 +433,9 @@ __host__ __device__ constexpr int local_of(int p) {
 // Per-lane constants of the lane's island (lane-varying copies of cp_physics fields).
 struct Lane {
     int isl;
-    float im1, im2;      // inverse masses of the island's cart, pole
-    float ii1[3], ii2[3];  // their body-frame inverse inertias
-    float mu0, mu1, mu2; // friction products of local pairs 0..2
+    real im1, im2;      // inverse masses of the island's cart, pole
+    real ii1[3], ii2[3];  // their body-frame inverse inertias
+    real mu0, mu1, mu2; // friction products of local pairs 0..2
     CP_DEV static Lane make(int isl, const cp_physics& P) {
         Lane L;
         L.isl = isl;
@@ -468,7 +445,7 @@ struct Lane {
             L.ii1[k] = isl ? P.inv_inertia[3][k] : P.inv_inertia[1][k];
             L.ii2[k] = isl ? P.inv_inertia[4][k] : P.inv_inertia[2][k];
         }
-        const float fc = isl ? P.friction[3] : P.friction[1], fq = isl ? P.friction[4] : P.friction[2];
+        const real fc = isl ? P.friction[3] : P.friction[1], fq = isl ? P.friction[4] : P.friction[2];
         L.mu0 = P.friction[0] * fc;
         L.mu1 = P.friction[0] * fq;
         L.mu2 = fc * fq;
@@ -496,7 +473,7 @@ struct Dyn {
 };
 struct Isl {
     Dyn d1, d2;
-    float im1, im2;
+    real im1, im2;
 };
 template <int K>
 CP_DEV Dyn& dyn(Isl& I) {
@@ -504,13 +481,13 @@ CP_DEV Dyn& dyn(Isl& I) {
     else return I.d2;
 }
 template <int K>
-CP_DEV float dyn_im(const Isl& I) {
+CP_DEV real dyn_im(const Isl& I) {
     if constexpr (K == 1) return I.im1;
     else return I.im2;
 }
 
 template <int A, int B>
-CP_DEV void isl_impulse(Isl& I, V3 rb, V3 t, float lam) {
+CP_DEV void isl_impulse(Isl& I, V3 rb, V3 t, real lam) {
     Dyn& b = dyn<B>(I);
     V3 rbt = cross(rb, t);
     V3 ib = symv(b.M, rbt);
@@ -527,13 +504,13 @@ CP_DEV void isl_impulse(Isl& I, V3 rb, V3 t, float lam) {
 }
 
 template <int A, int B, bool FRICTION>
-CP_DEV bool isl_row(Isl& I, V3 rb, V3 t, float inv_eff, float target, float& lam, float bound, float tol) {
+CP_DEV bool isl_row(Isl& I, V3 rb, V3 t, real inv_eff, real target, real& lam, real bound, real tol) {
     Dyn& b = dyn<B>(I);
-    const float imb = dyn_im<B>(I);
+    const real imb = dyn_im<B>(I);
     V3 rbt = cross(rb, t);
     V3 ib = symv(b.M, rbt);
-    float vn;
-    V3 ia = mk(0.0f, 0.0f, 0.0f);
+    real vn;
+    V3 ia = mk(real(0.0), real(0.0), real(0.0));
     if constexpr (A == 0) {
         vn = dot(t, b.v) + dot(b.w, rbt);
     } else {
@@ -543,24 +520,24 @@ CP_DEV bool isl_row(Isl& I, V3 rb, V3 t, float inv_eff, float target, float& lam
         ia = symv(a.M, rat);
         vn = (dot(t, sub(b.v, a.v)) + dot(b.w, rbt)) - dot(a.w, rat);
     }
-    float e = target - vn;
-    float dl = e * inv_eff;
-    float l0 = lam + dl;
-    float ln;
-    if constexpr (!FRICTION) ln = l0 > 0.0f ? l0 : 0.0f;
-    else ln = bound > 0.0f ? __builtin_amdgcn_fmed3f(l0, -bound, bound) : lam;  // see isl_row_ez
+    real e = target - vn;
+    real dl = e * inv_eff;
+    real l0 = lam + dl;
+    real ln;
+    if constexpr (!FRICTION) ln = l0 > real(0.0) ? l0 : real(0.0);
+    else ln = bound > real(0.0) ? clamp_sym(l0, bound) : lam;  // see isl_row_ez
     dl = ln - lam;
     lam = ln;
-    float sb = dl * imb;
+    real sb = dl * imb;
     b.v = madd(b.v, t, sb);
     b.w = madd(b.w, ib, dl);
     if constexpr (A != 0) {
         Dyn& a = dyn<A>(I);
-        float sa = dl * dyn_im<A>(I);
+        real sa = dl * dyn_im<A>(I);
         a.v = madd(a.v, neg(t), sa);
         a.w = madd(a.w, neg(ia), dl);
     }
-    return fabsf(dl) > tol * inv_eff;  // Bullet residual test (oracle: solve_row)
+    return abs_(dl) > tol * inv_eff;  // Bullet residual test (oracle: solve_row)
 }
 
 // isl_row<0, B> for a ground manifold whose normal is exactly +z (the static ground's top
@@ -571,52 +548,52 @@ CP_DEV bool isl_row(Isl& I, V3 rb, V3 t, float inv_eff, float target, float& lam
 // exact zero result can differ).  KIND 0: t = n, 1: t = t1, 2: t = t2.  Same values as
 // isl_row, about 60 % of its VALU work (no r x t, 6 of the 9 products of M (r x t)).
 template <int B, int KIND, bool FRICTION>
-CP_DEV bool isl_row_ez(Isl& I, V3 rb, float inv_eff, float target, float& lam, float bound, float tol) {
+CP_DEV bool isl_row_ez(Isl& I, V3 rb, real inv_eff, real target, real& lam, real bound, real tol) {
     Dyn& b = dyn<B>(I);
-    const float imb = dyn_im<B>(I);
+    const real imb = dyn_im<B>(I);
     const Sym& M = b.M;
     V3 ib;
-    float vn;
+    real vn;
     if constexpr (KIND == 0) {         // r x n = (rb.y, -rb.x, 0)
-        const float px = rb.y, py = -rb.x;
-        ib = mk(fmaf_(M.m0, px, M.m1 * py), fmaf_(M.m1, px, M.m3 * py), fmaf_(M.m2, px, M.m4 * py));
-        vn = b.v.z + fmaf_(b.w.x, px, b.w.y * py);
+        const real px = rb.y, py = -rb.x;
+        ib = mk(fma_(M.m0, px, M.m1 * py), fma_(M.m1, px, M.m3 * py), fma_(M.m2, px, M.m4 * py));
+        vn = b.v.z + fma_(b.w.x, px, b.w.y * py);
     } else if constexpr (KIND == 1) {  // r x t1 = (rb.z, 0, -rb.x)
-        const float px = rb.z, pz = -rb.x;
-        ib = mk(fmaf_(M.m0, px, M.m2 * pz), fmaf_(M.m1, px, M.m4 * pz), fmaf_(M.m2, px, M.m5 * pz));
-        vn = -b.v.y + fmaf_(b.w.x, px, b.w.z * pz);
+        const real px = rb.z, pz = -rb.x;
+        ib = mk(fma_(M.m0, px, M.m2 * pz), fma_(M.m1, px, M.m4 * pz), fma_(M.m2, px, M.m5 * pz));
+        vn = -b.v.y + fma_(b.w.x, px, b.w.z * pz);
     } else {                           // r x t2 = (0, rb.z, -rb.y)
-        const float py = rb.z, pz = -rb.y;
-        ib = mk(fmaf_(M.m1, py, M.m2 * pz), fmaf_(M.m3, py, M.m4 * pz), fmaf_(M.m4, py, M.m5 * pz));
-        vn = b.v.x + fmaf_(b.w.y, py, b.w.z * pz);
+        const real py = rb.z, pz = -rb.y;
+        ib = mk(fma_(M.m1, py, M.m2 * pz), fma_(M.m3, py, M.m4 * pz), fma_(M.m4, py, M.m5 * pz));
+        vn = b.v.x + fma_(b.w.y, py, b.w.z * pz);
     }
-    float e = target - vn;
-    float dl = e * inv_eff;
-    float l0 = lam + dl;
-    float ln;
+    real e = target - vn;
+    real dl = e * inv_eff;
+    real l0 = lam + dl;
+    real ln;
     // friction rows: Bullet skips the row while the normal impulse is not > 0 (lambda stays,
     // dl = 0, no residual); else the clamp as one v_med3_f32 (bound > 0): the same value as
     // the oracle's compare chain for every non-NaN l0, one dependent instruction instead of
     // three
-    if constexpr (!FRICTION) ln = l0 > 0.0f ? l0 : 0.0f;
-    else ln = bound > 0.0f ? __builtin_amdgcn_fmed3f(l0, -bound, bound) : lam;
+    if constexpr (!FRICTION) ln = l0 > real(0.0) ? l0 : real(0.0);
+    else ln = bound > real(0.0) ? clamp_sym(l0, bound) : lam;
     dl = ln - lam;
     lam = ln;
-    float sb = dl * imb;
+    real sb = dl * imb;
     if constexpr (KIND == 0) b.v.z = b.v.z + sb;
     else if constexpr (KIND == 1) b.v.y = b.v.y - sb;
     else b.v.x = b.v.x + sb;
     b.w = madd(b.w, ib, dl);
-    return fabsf(dl) > tol * inv_eff;  // Bullet residual test (oracle: solve_row)
+    return abs_(dl) > tol * inv_eff;  // Bullet residual test (oracle: solve_row)
 }
-CP_DEV bool is_plus_z(V3 n) { return n.x == 0.0f && n.y == 0.0f && n.z == 1.0f; }
+CP_DEV bool is_plus_z(V3 n) { return n.x == real(0.0) && n.y == real(0.0) && n.z == real(1.0); }
 
 // local pair j (0..2) of the island: (ground, cart), (ground, pole), (cart, pole)
 template <int J> constexpr int loc_a() { return J == 2 ? 1 : 0; }
 template <int J> constexpr int loc_b() { return J == 0 ? 1 : 2; }
 
 template <int J>
-CP_DEV void isl_warmstart(Isl& I, const Step& T, float* pool) {
+CP_DEV void isl_warmstart(Isl& I, const Step& T, real* pool) {
     const uint32_t pk = T.pk[J];
     const int cnt = pk_cnt(pk), base = pk_base(pk);
     for (int k = 0; k < cnt; ++k) {
@@ -627,21 +604,21 @@ CP_DEV void isl_warmstart(Isl& I, const Step& T, float* pool) {
 }
 
 template <int J>
-CP_DEV void isl_normal_rows(Isl& I, const Step& T, float* pool, float tol, bool& bad) {
+CP_DEV void isl_normal_rows(Isl& I, const Step& T, real* pool, real tol, bool& bad) {
     const uint32_t pk = T.pk[J];
     const int cnt = pk_cnt(pk), base = pk_base(pk);
     for (int k = 0; k < cnt; ++k) {
         const int s = base + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
-        float lam = pool_n(pool, F_LAM, s);
+        real lam = pool_n(pool, F_LAM, s);
         bad |= isl_row<loc_a<J>(), loc_b<J>(), false>(I, rb, T.n[J], pool_n(pool, F_IE, s),
-                                                      pool_n(pool, F_TG, s), lam, 0.0f, tol);
+                                                      pool_n(pool, F_TG, s), lam, real(0.0), tol);
         pool_n(pool, F_LAM, s) = lam;
     }
 }
 
 template <int J, bool HOISTED = false>
-CP_DEV void isl_friction_rows(Isl& I, const Step& T, float mu, float* pool, float tol, bool& bad, V3 ht1 = V3{},
+CP_DEV void isl_friction_rows(Isl& I, const Step& T, real mu, real* pool, real tol, bool& bad, V3 ht1 = V3{},
                               V3 ht2 = V3{}) {
     const uint32_t pk = T.pk[J];
     const int fcnt = pk_fcnt(pk);
@@ -660,10 +637,10 @@ CP_DEV void isl_friction_rows(Isl& I, const Step& T, float mu, float* pool, floa
     for (int k = 0; k < fcnt; ++k) {
         const int s = base + k, fs = fbase + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
-        float bound = mu * pool_n(pool, F_LAM, s);
-        float l1 = pool_f(pool, FF_L1, fs), l2 = pool_f(pool, FF_L2, fs);
-        bad |= isl_row<loc_a<J>(), loc_b<J>(), true>(I, rb, t1, pool_f(pool, FF_IE1, fs), 0.0f, l1, bound, tol);
-        bad |= isl_row<loc_a<J>(), loc_b<J>(), true>(I, rb, t2, pool_f(pool, FF_IE2, fs), 0.0f, l2, bound, tol);
+        real bound = mu * pool_n(pool, F_LAM, s);
+        real l1 = pool_f(pool, FF_L1, fs), l2 = pool_f(pool, FF_L2, fs);
+        bad |= isl_row<loc_a<J>(), loc_b<J>(), true>(I, rb, t1, pool_f(pool, FF_IE1, fs), real(0.0), l1, bound, tol);
+        bad |= isl_row<loc_a<J>(), loc_b<J>(), true>(I, rb, t2, pool_f(pool, FF_IE2, fs), real(0.0), l2, bound, tol);
         pool_f(pool, FF_L1, fs) = l1;
         pool_f(pool, FF_L2, fs) = l2;
     }
@@ -675,20 +652,20 @@ CP_DEV void isl_friction_rows(Isl& I, const Step& T, float mu, float* pool, floa
 // The rows of ground pair J (0 or 1) when every lane of the wave with rows on it has a +z
 // normal (wave-uniform choice in sweeps()): the same sweep with isl_row_ez.
 template <int J>
-CP_DEV void isl_normal_rows_ez(Isl& I, const Step& T, float* pool, float tol, bool& bad) {
+CP_DEV void isl_normal_rows_ez(Isl& I, const Step& T, real* pool, real tol, bool& bad) {
     static_assert(loc_a<J>() == 0, "ground pairs only");
     const uint32_t pk = T.pk[J];
     const int cnt = pk_cnt(pk), base = pk_base(pk);
     CP_EZ_LOOP(k, cnt) {
         const int s = base + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
-        float lam = pool_n(pool, F_LAM, s);
-        bad |= isl_row_ez<loc_b<J>(), 0, false>(I, rb, pool_n(pool, F_IE, s), pool_n(pool, F_TG, s), lam, 0.0f, tol);
+        real lam = pool_n(pool, F_LAM, s);
+        bad |= isl_row_ez<loc_b<J>(), 0, false>(I, rb, pool_n(pool, F_IE, s), pool_n(pool, F_TG, s), lam, real(0.0), tol);
         pool_n(pool, F_LAM, s) = lam;
     }
 }
 template <int J>
-CP_DEV void isl_friction_rows_ez(Isl& I, const Step& T, float mu, float* pool, float tol, bool& bad) {
+CP_DEV void isl_friction_rows_ez(Isl& I, const Step& T, real mu, real* pool, real tol, bool& bad) {
     static_assert(loc_a<J>() == 0, "ground pairs only");
     const uint32_t pk = T.pk[J];
     const int fcnt = pk_fcnt(pk);
@@ -697,10 +674,10 @@ CP_DEV void isl_friction_rows_ez(Isl& I, const Step& T, float mu, float* pool, f
     CP_EZ_LOOP(k, fcnt) {
         const int s = base + k, fs = fbase + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
-        float bound = mu * pool_n(pool, F_LAM, s);
-        float l1 = pool_f(pool, FF_L1, fs), l2 = pool_f(pool, FF_L2, fs);
-        bad |= isl_row_ez<loc_b<J>(), 1, true>(I, rb, pool_f(pool, FF_IE1, fs), 0.0f, l1, bound, tol);
-        bad |= isl_row_ez<loc_b<J>(), 2, true>(I, rb, pool_f(pool, FF_IE2, fs), 0.0f, l2, bound, tol);
+        real bound = mu * pool_n(pool, F_LAM, s);
+        real l1 = pool_f(pool, FF_L1, fs), l2 = pool_f(pool, FF_L2, fs);
+        bad |= isl_row_ez<loc_b<J>(), 1, true>(I, rb, pool_f(pool, FF_IE1, fs), real(0.0), l1, bound, tol);
+        bad |= isl_row_ez<loc_b<J>(), 2, true>(I, rb, pool_f(pool, FF_IE2, fs), real(0.0), l2, bound, tol);
         pool_f(pool, FF_L1, fs) = l1;
         pool_f(pool, FF_L2, fs) = l2;
     }
@@ -729,7 +706,7 @@ CP_DEV Hdr pair_hdr(const Step& T, bool second) {
 
 // impulse lam along t at rb (oracle: apply_impulse); A == 0 is the static ground
 template <int A, int B>
-CP_DEV void apply_impulse(Sim& S, const Step& T, const cp_physics& P, V3 rb, V3 t, float lam) {
+CP_DEV void apply_impulse(Sim& S, const Step& T, const cp_physics& P, V3 rb, V3 t, real lam) {
     V3 rbt = cross(rb, t);
     V3 ib = symv(T.M[B - 1], rbt);
     S.b[B - 1].v = madd(S.b[B - 1].v, t, lam * P.inv_mass[B]);
@@ -745,13 +722,13 @@ CP_DEV void apply_impulse(Sim& S, const Step& T, const cp_physics& P, V3 rb, V3 
 
 // One PGS row (oracle: solve_row).  Returns |e * dlambda|.
 template <int A, int B, bool FRICTION>
-CP_DEV bool solve_row(Sim& S, const Step& T, const cp_physics& P, V3 rb, V3 t, float inv_eff, float target,
-                      float& lam, float bound, float tol) {
-    float imb = P.inv_mass[B];
+CP_DEV bool solve_row(Sim& S, const Step& T, const cp_physics& P, V3 rb, V3 t, real inv_eff, real target,
+                      real& lam, real bound, real tol) {
+    real imb = P.inv_mass[B];
     V3 rbt = cross(rb, t);
     V3 ib = symv(T.M[B - 1], rbt);
-    float vn;
-    V3 ia = mk(0.0f, 0.0f, 0.0f);
+    real vn;
+    V3 ia = mk(real(0.0), real(0.0), real(0.0));
     if constexpr (A == 0) {
         vn = dot(t, S.b[B - 1].v) + dot(S.b[B - 1].w, rbt);
     } else {
@@ -760,29 +737,29 @@ CP_DEV bool solve_row(Sim& S, const Step& T, const cp_physics& P, V3 rb, V3 t, f
         ia = symv(T.M[A - 1], rat);
         vn = (dot(t, sub(S.b[B - 1].v, S.b[A - 1].v)) + dot(S.b[B - 1].w, rbt)) - dot(S.b[A - 1].w, rat);
     }
-    float e = target - vn;
-    float dl = e * inv_eff;
-    float l0 = lam + dl;
-    float ln;
-    if constexpr (!FRICTION) ln = l0 > 0.0f ? l0 : 0.0f;
-    else ln = bound > 0.0f ? __builtin_amdgcn_fmed3f(l0, -bound, bound) : lam;  // see isl_row_ez
+    real e = target - vn;
+    real dl = e * inv_eff;
+    real l0 = lam + dl;
+    real ln;
+    if constexpr (!FRICTION) ln = l0 > real(0.0) ? l0 : real(0.0);
+    else ln = bound > real(0.0) ? clamp_sym(l0, bound) : lam;  // see isl_row_ez
     dl = ln - lam;
     lam = ln;
-    float sb = dl * imb;
+    real sb = dl * imb;
     S.b[B - 1].v = madd(S.b[B - 1].v, t, sb);
     S.b[B - 1].w = madd(S.b[B - 1].w, ib, dl);
     if constexpr (A != 0) {
-        float sa = dl * P.inv_mass[A];
+        real sa = dl * P.inv_mass[A];
         S.b[A - 1].v = madd(S.b[A - 1].v, neg(t), sa);
         S.b[A - 1].w = madd(S.b[A - 1].w, neg(ia), dl);
     }
-    return fabsf(dl) > tol * inv_eff;  // Bullet residual test (oracle: solve_row)
+    return abs_(dl) > tol * inv_eff;  // Bullet residual test (oracle: solve_row)
 }
 
 template <int PAIR>
-CP_DEV void pair_warmstart(Sim& S, const Step& T, bool second, const cp_physics& P, float* pool0) {
+CP_DEV void pair_warmstart(Sim& S, const Step& T, bool second, const cp_physics& P, real* pool0) {
     constexpr int A = pair_a(PAIR), B = pair_b(PAIR);
-    float* pool = pool0 + island_of(PAIR);
+    real* pool = pool0 + island_of(PAIR);
     const Hdr H = pair_hdr<PAIR>(T, second);
     const uint32_t pk = H.pk;
     const int cnt = pk_cnt(pk), base = pk_base(pk);
@@ -794,34 +771,34 @@ CP_DEV void pair_warmstart(Sim& S, const Step& T, bool second, const cp_physics&
 }
 
 template <int PAIR>
-CP_DEV void pair_normal_rows(Sim& S, const Step& T, bool second, const cp_physics& P, float* pool0,
-                             float tol, bool& bad) {
+CP_DEV void pair_normal_rows(Sim& S, const Step& T, bool second, const cp_physics& P, real* pool0,
+                             real tol, bool& bad) {
     constexpr int A = pair_a(PAIR), B = pair_b(PAIR);
-    float* pool = pool0 + island_of(PAIR);
+    real* pool = pool0 + island_of(PAIR);
     const Hdr H = pair_hdr<PAIR>(T, second);
     const uint32_t pk = H.pk;
     const int cnt = pk_cnt(pk), base = pk_base(pk);
     for (int k = 0; k < cnt; ++k) {
         const int s = base + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
-        float lam = pool_n(pool, F_LAM, s);
+        real lam = pool_n(pool, F_LAM, s);
         bad |= solve_row<A, B, false>(S, T, P, rb, H.n, pool_n(pool, F_IE, s), pool_n(pool, F_TG, s),
-                                      lam, 0.0f, tol);
+                                      lam, real(0.0), tol);
         pool_n(pool, F_LAM, s) = lam;
     }
 }
 
 template <int PAIR>
-CP_DEV void pair_friction_rows(Sim& S, const Step& T, bool second, const cp_physics& P, float* pool0,
-                               float tol, bool& bad) {
+CP_DEV void pair_friction_rows(Sim& S, const Step& T, bool second, const cp_physics& P, real* pool0,
+                               real tol, bool& bad) {
     constexpr int A = pair_a(PAIR), B = pair_b(PAIR);
-    float* pool = pool0 + island_of(PAIR);
+    real* pool = pool0 + island_of(PAIR);
     const Hdr H = pair_hdr<PAIR>(T, second);
     const uint32_t pk = H.pk;
     const int fcnt = pk_fcnt(pk);
     if (fcnt == 0) return;
     const int base = pk_base(pk), fbase = pk_fbase(pk);
-    const float mu = P.friction[A] * P.friction[B];
+    const real mu = real(P.friction[A]) * real(P.friction[B]);  // oracle: (real) * (real)
     V3 n = H.n;
     asm volatile("" : "+v"(n.x), "+v"(n.y), "+v"(n.z));
     V3 t1, t2;
@@ -829,10 +806,10 @@ CP_DEV void pair_friction_rows(Sim& S, const Step& T, bool second, const cp_phys
     for (int k = 0; k < fcnt; ++k) {
         const int s = base + k, fs = fbase + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
-        float bound = mu * pool_n(pool, F_LAM, s);
-        float l1 = pool_f(pool, FF_L1, fs), l2 = pool_f(pool, FF_L2, fs);
-        bad |= solve_row<A, B, true>(S, T, P, rb, t1, pool_f(pool, FF_IE1, fs), 0.0f, l1, bound, tol);
-        bad |= solve_row<A, B, true>(S, T, P, rb, t2, pool_f(pool, FF_IE2, fs), 0.0f, l2, bound, tol);
+        real bound = mu * pool_n(pool, F_LAM, s);
+        real l1 = pool_f(pool, FF_L1, fs), l2 = pool_f(pool, FF_L2, fs);
+        bad |= solve_row<A, B, true>(S, T, P, rb, t1, pool_f(pool, FF_IE1, fs), real(0.0), l1, bound, tol);
+        bad |= solve_row<A, B, true>(S, T, P, rb, t2, pool_f(pool, FF_IE2, fs), real(0.0), l2, bound, tol);
         pool_f(pool, FF_L1, fs) = l1;
         pool_f(pool, FF_L2, fs) = l2;
     }
@@ -844,10 +821,10 @@ CP_DEV V3 sel5v(int g, V3 z, V3 a, V3 b, V3 c, V3 d) {
               g == 1 ? a.y : g == 2 ? b.y : g == 3 ? c.y : g == 4 ? d.y : z.y,
               g == 1 ? a.z : g == 2 ? b.z : g == 3 ? c.z : g == 4 ? d.z : z.z);
 }
-CP_DEV float sel5(int g, float z, float a, float b, float c, float d) {
+CP_DEV real sel5(int g, real z, real a, real b, real c, real d) {
     return g == 1 ? a : g == 2 ? b : g == 3 ? c : g == 4 ? d : z;
 }
-CP_DEV float sel5p(int g, const float* v) { return sel5(g, v[0], v[1], v[2], v[3], v[4]); }
+CP_DEV real sel5p(int g, const float* v) { return sel5(g, real(v[0]), real(v[1]), real(v[2]), real(v[3]), real(v[4])); }
 // Box of body g (lane-varying) with its world inverse inertia, from the pose in S:
 // the axes are rebuilt from the quaternion here rather than kept live through the
 // narrowphase (same arithmetic as the per-body quat_axes / world_inv_inertia).
@@ -859,11 +836,11 @@ CP_DEV Box box_sel(int g, const Sim& S, const cp_physics& P) {
                 P.half_extents[4][1]);
     b.h2 = sel5(g, P.half_extents[0][2], P.half_extents[1][2], P.half_extents[2][2], P.half_extents[3][2],
                 P.half_extents[4][2]);
-    b.c = sel5v(g, mk(0.0f, 0.0f, 0.0f), S.b[0].x, S.b[1].x, S.b[2].x, S.b[3].x);
-    const float qx = sel5(g, 0.0f, S.b[0].q[0], S.b[1].q[0], S.b[2].q[0], S.b[3].q[0]);
-    const float qy = sel5(g, 0.0f, S.b[0].q[1], S.b[1].q[1], S.b[2].q[1], S.b[3].q[1]);
-    const float qz = sel5(g, 0.0f, S.b[0].q[2], S.b[1].q[2], S.b[2].q[2], S.b[3].q[2]);
-    const float qw = sel5(g, 1.0f, S.b[0].q[3], S.b[1].q[3], S.b[2].q[3], S.b[3].q[3]);
+    b.c = sel5v(g, mk(real(0.0), real(0.0), real(0.0)), S.b[0].x, S.b[1].x, S.b[2].x, S.b[3].x);
+    const real qx = sel5(g, real(0.0), S.b[0].q[0], S.b[1].q[0], S.b[2].q[0], S.b[3].q[0]);
+    const real qy = sel5(g, real(0.0), S.b[0].q[1], S.b[1].q[1], S.b[2].q[1], S.b[3].q[1]);
+    const real qz = sel5(g, real(0.0), S.b[0].q[2], S.b[1].q[2], S.b[2].q[2], S.b[3].q[2]);
+    const real qw = sel5(g, real(1.0), S.b[0].q[3], S.b[1].q[3], S.b[2].q[3], S.b[3].q[3]);
     b.ax = quat_axes(qx, qy, qz, qw);  // identity, exactly, for the ground
     return b;
 }
@@ -879,19 +856,19 @@ CP_DEV Sym inertia_sel(int g, const Box& b, const cp_physics& P) {
 // Broadphase: true when a face axis of A already separates the pair by more than
 // the margin (bounding radius of B as its projection, plus 1e-3 m of slack for
 // rounding), i.e. when box_box would return no contact from its face-axis test.
-CP_DEV bool face_separated(const Box& A, const Box& B, float margin) {
+CP_DEV bool face_separated(const Box& A, const Box& B, real margin) {
     const V3 d = sub(B.c, A.c);
-    const float rb = sqrtf(fmaf_(B.h0, B.h0, fmaf_(B.h1, B.h1, B.h2 * B.h2)));
-    const float lim = (margin + 1e-3f) + rb;
-    return (fabsf(dot(d, A.ax.a0)) - A.h0 > lim) || (fabsf(dot(d, A.ax.a1)) - A.h1 > lim) ||
-           (fabsf(dot(d, A.ax.a2)) - A.h2 > lim);
+    const real rb = sqrt_(fma_(B.h0, B.h0, fma_(B.h1, B.h1, B.h2 * B.h2)));
+    const real lim = (margin + real(1e-3)) + rb;
+    return (abs_(dot(d, A.ax.a0)) - A.h0 > lim) || (abs_(dot(d, A.ax.a1)) - A.h1 > lim) ||
+           (abs_(dot(d, A.ax.a2)) - A.h2 > lim);
 }
 CP_DEV V3 pos_of(int g, const Sim& S) {
-    return sel5v(g, mk(0.0f, 0.0f, 0.0f), S.b[0].x, S.b[1].x, S.b[2].x, S.b[3].x);
+    return sel5v(g, mk(real(0.0), real(0.0), real(0.0)), S.b[0].x, S.b[1].x, S.b[2].x, S.b[3].x);
 }
 
 // row setup for direction t with pair bodies selected at run time (narrowphase)
-CP_DEV float row_k_dyn(int a, float ima, float imb, V3 xa, V3 xb, const Sym& Ma, const Sym& Mb, V3 rb, V3 t) {
+CP_DEV real row_k_dyn(int a, real ima, real imb, V3 xa, V3 xb, const Sym& Ma, const Sym& Mb, V3 rb, V3 t) {
     V3 rbt = cross(rb, t);
     V3 ib = symv(Mb, rbt);
     if (a == 0) return imb + dot(rbt, ib);
@@ -964,7 +941,7 @@ CP_DEV void cross_back(Isl& I, const Sim& S, bool second) {
 struct Ctx {
     Step T;          // own island's manifold headers (+ whole-env M for the cross rows)
     Isl I;           // own island's bodies
-    float mu0, mu1, mu2;
+    real mu0, mu1, mu2;
     int used, tot;   // rows of the own island, of the env
     bool merged, active;
 };
@@ -974,9 +951,9 @@ struct Ctx {
 // view.  Both lanes of an env stop together, after the first sweep in which no row of
 // the env (island 0, island 1, cross) has a squared residual above the threshold:
 // Bullet solves the two islands as one group (oracle: substep, step 4).
-CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, float* pool, float* pool0, bool second, int it0, int it1,
+CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0, bool second, int it0, int it1,
                    Stamps& ST) {
-    const float tol = sqrtf(P.residual_threshold);
+    const real tol = sqrt_(real(P.residual_threshold));  // oracle: SQRT((real)threshold)
     // the ground-pole pair's tangent basis (with the URDF frictions the only island pair with
     // friction rows: the carts' friction is 0), once per substep instead of once per sweep:
     // step kernel 0.772 -> 0.753 ms
@@ -1045,15 +1022,15 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, float* pool, float* pool
 // pairs 0 or 2 (the default friction table: a cart's friction is 0).
 struct GRow {
     V3 rbt, ib;
-    float ie, tg, lam;
+    real ie, tg, lam;
 };
 struct CRow {
     V3 rbt, ib, rat, ia;
-    float ie, tg, lam;
+    real ie, tg, lam;
 };
 struct FRow {
     V3 rbt1, ib1, rbt2, ib2;
-    float ie1, ie2, l1, l2;
+    real ie1, ie2, l1, l2;
 };
 struct FastIsl {
     GRow g0[4], g1[4];  // local pair 0 (ground, cart), 1 (ground, pole)
@@ -1065,7 +1042,7 @@ struct FastIsl {
 CP_DEV bool fast_ok(const Ctx& c) { return pk_fcnt(c.T.pk[0]) == 0 && pk_fcnt(c.T.pk[2]) == 0; }
 
 template <int J>
-CP_DEV void fast_ground_rows(GRow* R, const Ctx& c, float* pool) {
+CP_DEV void fast_ground_rows(GRow* R, const Ctx& c, real* pool) {
     const uint32_t pk = c.T.pk[J];
     const int cnt = pk_cnt(pk), base = pk_base(pk);
     const Sym& M = J == 0 ? c.I.d1.M : c.I.d2.M;
@@ -1083,7 +1060,7 @@ CP_DEV void fast_ground_rows(GRow* R, const Ctx& c, float* pool) {
     }
 }
 
-CP_DEV void fast_build(FastIsl& F, const Ctx& c, float* pool) {
+CP_DEV void fast_build(FastIsl& F, const Ctx& c, real* pool) {
     fast_ground_rows<0>(F.g0, c, pool);
     fast_ground_rows<1>(F.g1, c, pool);
     {
@@ -1133,45 +1110,45 @@ CP_DEV void fast_build(FastIsl& F, const Ctx& c, float* pool) {
 // one ground row (A = static ground) on body b: isl_row<0, B, FRICTION> with r x t
 // and M (r x t) precomputed
 template <bool FRICTION>
-CP_DEV bool fast_grow(Dyn& b, float imb, V3 t, V3 rbt, V3 ib, float inv_eff, float target, float& lam,
-                      float bound, float tol) {
-    const float vn = dot(t, b.v) + dot(b.w, rbt);
-    const float e = target - vn;
-    float dl = e * inv_eff;
-    const float l0 = lam + dl;
-    float ln;
-    if constexpr (!FRICTION) ln = l0 > 0.0f ? l0 : 0.0f;
-    else ln = bound > 0.0f ? __builtin_amdgcn_fmed3f(l0, -bound, bound) : lam;  // see isl_row_ez
+CP_DEV bool fast_grow(Dyn& b, real imb, V3 t, V3 rbt, V3 ib, real inv_eff, real target, real& lam,
+                      real bound, real tol) {
+    const real vn = dot(t, b.v) + dot(b.w, rbt);
+    const real e = target - vn;
+    real dl = e * inv_eff;
+    const real l0 = lam + dl;
+    real ln;
+    if constexpr (!FRICTION) ln = l0 > real(0.0) ? l0 : real(0.0);
+    else ln = bound > real(0.0) ? clamp_sym(l0, bound) : lam;  // see isl_row_ez
     dl = ln - lam;
     lam = ln;
-    const float sb = dl * imb;
+    const real sb = dl * imb;
     b.v = madd(b.v, t, sb);
     b.w = madd(b.w, ib, dl);
-    return fabsf(dl) > tol * inv_eff;  // Bullet residual test (oracle: solve_row)
+    return abs_(dl) > tol * inv_eff;  // Bullet residual test (oracle: solve_row)
 }
 
 // one cart-pole normal row: isl_row<1, 2, false> with both bodies' terms precomputed
-CP_DEV bool fast_crow(Isl& I, V3 t, const CRow& R, float& lam, float tol) {
-    const float vn = (dot(t, sub(I.d2.v, I.d1.v)) + dot(I.d2.w, R.rbt)) - dot(I.d1.w, R.rat);
-    const float e = R.tg - vn;
-    float dl = e * R.ie;
-    const float l0 = lam + dl;
-    const float ln = l0 > 0.0f ? l0 : 0.0f;
+CP_DEV bool fast_crow(Isl& I, V3 t, const CRow& R, real& lam, real tol) {
+    const real vn = (dot(t, sub(I.d2.v, I.d1.v)) + dot(I.d2.w, R.rbt)) - dot(I.d1.w, R.rat);
+    const real e = R.tg - vn;
+    real dl = e * R.ie;
+    const real l0 = lam + dl;
+    const real ln = l0 > real(0.0) ? l0 : real(0.0);
     dl = ln - lam;
     lam = ln;
-    const float sb = dl * I.im2;
+    const real sb = dl * I.im2;
     I.d2.v = madd(I.d2.v, t, sb);
     I.d2.w = madd(I.d2.w, R.ib, dl);
-    const float sa = dl * I.im1;
+    const real sa = dl * I.im1;
     I.d1.v = madd(I.d1.v, neg(t), sa);
     I.d1.w = madd(I.d1.w, neg(R.ia), dl);
-    return fabsf(dl) > tol * R.ie;  // Bullet residual test (oracle: solve_row)
+    return abs_(dl) > tol * R.ie;  // Bullet residual test (oracle: solve_row)
 }
 
 // sweeps() with the island rows in fast form (same row order, same stopping rule)
-CP_DEV void sweeps_fast(Ctx& c, FastIsl& F, Sim& S, const cp_physics& P, float* pool, float* pool0, bool second,
+CP_DEV void sweeps_fast(Ctx& c, FastIsl& F, Sim& S, const cp_physics& P, real* pool, real* pool0, bool second,
                         int it0, int it1, Stamps& ST) {
-    const float tol = sqrtf(P.residual_threshold);
+    const real tol = sqrt_(real(P.residual_threshold));  // oracle: SQRT((real)threshold)
     const int cnt0 = pk_cnt(c.T.pk[0]), cnt1 = pk_cnt(c.T.pk[1]), cnt2 = pk_cnt(c.T.pk[2]);
     const int fc1 = pk_fcnt(c.T.pk[1]);
     const V3 n0 = c.T.n[0], n1 = c.T.n[1], n2 = c.T.n[2];
@@ -1185,11 +1162,11 @@ CP_DEV void sweeps_fast(Ctx& c, FastIsl& F, Sim& S, const cp_physics& P, float* 
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 if (k < cnt0) bad |= fast_grow<false>(c.I.d1, c.I.im1, n0, F.g0[k].rbt, F.g0[k].ib, F.g0[k].ie,
-                                                      F.g0[k].tg, F.g0[k].lam, 0.0f, tol);
+                                                      F.g0[k].tg, F.g0[k].lam, real(0.0), tol);
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 if (k < cnt1) bad |= fast_grow<false>(c.I.d2, c.I.im2, n1, F.g1[k].rbt, F.g1[k].ib, F.g1[k].ie,
-                                                      F.g1[k].tg, F.g1[k].lam, 0.0f, tol);
+                                                      F.g1[k].tg, F.g1[k].lam, real(0.0), tol);
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 if (k < cnt2) bad |= fast_crow(c.I, n2, F.c2[k], F.c2[k].lam, tol);
@@ -1207,10 +1184,10 @@ CP_DEV void sweeps_fast(Ctx& c, FastIsl& F, Sim& S, const cp_physics& P, float* 
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 if (k < fc1) {
-                    const float bound = c.mu1 * F.g1[k].lam;
-                    bad |= fast_grow<true>(c.I.d2, c.I.im2, F.t1, F.f1[k].rbt1, F.f1[k].ib1, F.f1[k].ie1, 0.0f,
+                    const real bound = c.mu1 * F.g1[k].lam;
+                    bad |= fast_grow<true>(c.I.d2, c.I.im2, F.t1, F.f1[k].rbt1, F.f1[k].ib1, F.f1[k].ie1, real(0.0),
                                            F.f1[k].l1, bound, tol);
-                    bad |= fast_grow<true>(c.I.d2, c.I.im2, F.t2, F.f1[k].rbt2, F.f1[k].ib2, F.f1[k].ie2, 0.0f,
+                    bad |= fast_grow<true>(c.I.d2, c.I.im2, F.t2, F.f1[k].rbt2, F.f1[k].ib2, F.f1[k].ie2, real(0.0),
                                            F.f1[k].l2, bound, tol);
                 }
             }
@@ -1230,7 +1207,7 @@ CP_DEV void sweeps_fast(Ctx& c, FastIsl& F, Sim& S, const cp_physics& P, float* 
 
 // the island rows' impulses back into the pool (substep_finish refreshes the
 // warm-start cache from it)
-CP_DEV void fast_store(const FastIsl& F, const Ctx& c, float* pool) {
+CP_DEV void fast_store(const FastIsl& F, const Ctx& c, real* pool) {
     const int cnt0 = pk_cnt(c.T.pk[0]), cnt1 = pk_cnt(c.T.pk[1]), cnt2 = pk_cnt(c.T.pk[2]);
     const int b0 = pk_base(c.T.pk[0]), b1 = pk_base(c.T.pk[1]), b2 = pk_base(c.T.pk[2]);
 #pragma unroll
@@ -1245,7 +1222,7 @@ CP_DEV void fast_store(const FastIsl& F, const Ctx& c, float* pool) {
 // lane of the wave has friction rows on local pairs 0 / 2 (wave-uniform choice; the
 // fast form needs the register budget of the 1-wave-per-SIMD latency kernels).
 template <bool FAST>
-CP_DEV void solve_range(Ctx& c, Sim& S, const cp_physics& P, float* pool, float* pool0, bool second, int it0, int it1,
+CP_DEV void solve_range(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0, bool second, int it0, int it1,
                         Stamps& ST) {
 #ifndef CP_NO_FAST_ROWS
     if constexpr (FAST) {
@@ -1272,10 +1249,10 @@ CP_DEV void island_view(const Sim& S, const Lane& L, Ctx& c) {
     I.d2.x = selv(second, S.b[3].x, S.b[1].x);
     I.d2.v = selv(second, S.b[3].v, S.b[1].v);
     I.d2.w = selv(second, S.b[3].w, S.b[1].w);
-    const float cq0 = second ? S.b[2].q[0] : S.b[0].q[0], cq1 = second ? S.b[2].q[1] : S.b[0].q[1];
-    const float cq2 = second ? S.b[2].q[2] : S.b[0].q[2], cq3 = second ? S.b[2].q[3] : S.b[0].q[3];
-    const float pq0 = second ? S.b[3].q[0] : S.b[1].q[0], pq1 = second ? S.b[3].q[1] : S.b[1].q[1];
-    const float pq2 = second ? S.b[3].q[2] : S.b[1].q[2], pq3 = second ? S.b[3].q[3] : S.b[1].q[3];
+    const real cq0 = second ? S.b[2].q[0] : S.b[0].q[0], cq1 = second ? S.b[2].q[1] : S.b[0].q[1];
+    const real cq2 = second ? S.b[2].q[2] : S.b[0].q[2], cq3 = second ? S.b[2].q[3] : S.b[0].q[3];
+    const real pq0 = second ? S.b[3].q[0] : S.b[1].q[0], pq1 = second ? S.b[3].q[1] : S.b[1].q[1];
+    const real pq2 = second ? S.b[3].q[2] : S.b[1].q[2], pq3 = second ? S.b[3].q[3] : S.b[1].q[3];
     I.d1.M = world_inv_inertia(quat_axes(cq0, cq1, cq2, cq3), L.ii1[0], L.ii1[1], L.ii1[2]);
     I.d2.M = world_inv_inertia(quat_axes(pq0, pq1, pq2, pq3), L.ii2[0], L.ii2[1], L.ii2[2]);
     I.im1 = L.im1;
@@ -1289,9 +1266,9 @@ CP_DEV void island_view(const Sim& S, const Lane& L, Ctx& c) {
 // row setup of the lane's island, unconstrained velocity update of the whole env,
 // the island view and the warm start.  A lane with live == false (done env, padding)
 // makes no contacts and writes nothing.
-CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, float* pool, float* pool0, int& overflow,
+CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool, real* pool0, int& overflow,
                          const Mem& G, Stamps& ST, bool live, Ctx& c) {
-    const float dt = P.dt, inv_dt = P.inv_dt;
+    const real dt = P.dt, inv_dt = P.inv_dt;
     CP_STAMP(t0);
     Step& T = c.T;
     // 2. narrowphase + row setup of the lane's island: wave-uniform loop over its 5
@@ -1305,13 +1282,13 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, float* pool
         const int a = GROUND ? 0 : pair_a(g), b = pair_b(g);
         CP_STAMP(n0);
         // warm-start cache of the pair, loaded first: its latency overlaps the narrowphase
-        const uint32_t oid = __float_as_uint(G.lw(CP_SF_WS_ID(0, j)));
-        const float ol0 = G.ll(CP_SF_WS_LAM(0, j, 0)), ol1 = G.ll(CP_SF_WS_LAM(0, j, 1));
-        const float ol2 = G.ll(CP_SF_WS_LAM(0, j, 2)), ol3 = G.ll(CP_SF_WS_LAM(0, j, 3));
+        const uint32_t oid = to_bits(G.lw(CP_SF_WS_ID(0, j)));
+        const real ol0 = G.ll(CP_SF_WS_LAM(0, j, 0)), ol1 = G.ll(CP_SF_WS_LAM(0, j, 1));
+        const real ol2 = G.ll(CP_SF_WS_LAM(0, j, 2)), ol3 = G.ll(CP_SF_WS_LAM(0, j, 3));
         Box A;
         if constexpr (GROUND) {
-            A.c = mk(0.0f, 0.0f, 0.0f);
-            A.ax = quat_axes(0.0f, 0.0f, 0.0f, 1.0f);
+            A.c = mk(real(0.0), real(0.0), real(0.0));
+            A.ax = quat_axes(real(0.0), real(0.0), real(0.0), real(1.0));
             A.h0 = P.half_extents[0][0];
             A.h1 = P.half_extents[0][1];
             A.h2 = P.half_extents[0][2];
@@ -1321,7 +1298,7 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, float* pool
         const Box Bx = box_sel(b, S, P);
         Contact C;
         C.m = 0;
-        C.n = mk(0.0f, 0.0f, 1.0f);
+        C.n = mk(real(0.0), real(0.0), real(1.0));
         CP_STAMP(n1);
         if (live && !face_separated(A, Bx, P.contact_margin)) box_box(A, Bx, P.contact_margin, P.edge_bias, C);
         CP_STAMP(n2);
@@ -1331,12 +1308,12 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, float* pool
         int m = 0, fm = 0;
         uint32_t nid = 0xFFFFFFFFu;
         if (__ballot(C.m > 0) != 0ull) {  // row setup, skipped when no lane of the wave has a contact
-        const float mu = sel5p(a, P.friction) * sel5p(b, P.friction);
-        const float ima = sel5p(a, P.inv_mass), imb = sel5p(b, P.inv_mass);
+        const real mu = sel5p(a, P.friction) * sel5p(b, P.friction);
+        const real ima = sel5p(a, P.inv_mass), imb = sel5p(b, P.inv_mass);
         const V3 xa = A.c, xb = Bx.c;
         const Sym Ma = inertia_sel(a, A, P), Mb = inertia_sel(b, Bx, P);
-        V3 t1 = mk(0.0f, 0.0f, 0.0f), t2 = t1;
-        if (mu > 0.0f) plane_space(C.n, t1, t2);
+        V3 t1 = mk(real(0.0), real(0.0), real(0.0)), t2 = t1;
+        if (mu > real(0.0)) plane_space(C.n, t1, t2);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             if (k < C.m) {
@@ -1345,11 +1322,11 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, float* pool
                 } else {
                     const int s = base + m;
                     V3 rb = sub(C.p[k], xb);
-                    float K = row_k_dyn(a, ima, imb, xa, xb, Ma, Mb, rb, C.n);
-                    float dist = C.d[k];
-                    float tg = dist > 0.0f ? -(dist * inv_dt) : -((P.erp * dist) * inv_dt);
+                    real K = row_k_dyn(a, ima, imb, xa, xb, Ma, Mb, rb, C.n);
+                    real dist = C.d[k];
+                    real tg = dist > real(0.0) ? -(dist * inv_dt) : -((P.erp * dist) * inv_dt);
                     const int id = C.id[k];
-                    float l0 = 0.0f;
+                    real l0 = real(0.0);
                     if ((int)(oid & 0xFFu) == id) l0 = ol0;
                     else if ((int)((oid >> 8) & 0xFFu) == id) l0 = ol1;
                     else if ((int)((oid >> 16) & 0xFFu) == id) l0 = ol2;
@@ -1357,19 +1334,19 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, float* pool
                     pool_n(pool, F_RBX, s) = rb.x;
                     pool_n(pool, F_RBY, s) = rb.y;
                     pool_n(pool, F_RBZ, s) = rb.z;
-                    pool_n(pool, F_IE, s) = 1.0f / K;
+                    pool_n(pool, F_IE, s) = real(1.0) / K;
                     pool_n(pool, F_TG, s) = tg;
                     pool_n(pool, F_LAM, s) = P.warmstart * l0;
                     nid = (nid & ~(0xFFu << (8 * m))) | ((uint32_t)id << (8 * m));
-                    if (mu > 0.0f) {
+                    if (mu > real(0.0)) {
                         if (fbase + fm >= MAXF) {
                             overflow += 1;
                         } else {
                             const int fs = fbase + fm;
-                            pool_f(pool, FF_IE1, fs) = 1.0f / row_k_dyn(a, ima, imb, xa, xb, Ma, Mb, rb, t1);
-                            pool_f(pool, FF_IE2, fs) = 1.0f / row_k_dyn(a, ima, imb, xa, xb, Ma, Mb, rb, t2);
-                            pool_f(pool, FF_L1, fs) = 0.0f;
-                            pool_f(pool, FF_L2, fs) = 0.0f;
+                            pool_f(pool, FF_IE1, fs) = real(1.0) / row_k_dyn(a, ima, imb, xa, xb, Ma, Mb, rb, t1);
+                            pool_f(pool, FF_IE2, fs) = real(1.0) / row_k_dyn(a, ima, imb, xa, xb, Ma, Mb, rb, t2);
+                            pool_f(pool, FF_L1, fs) = real(0.0);
+                            pool_f(pool, FF_L2, fs) = real(0.0);
                             fm += 1;
                         }
                     }
@@ -1387,7 +1364,7 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, float* pool
         G.sx(4 * j + 0, C.n.x);
         G.sx(4 * j + 1, C.n.y);
         G.sx(4 * j + 2, C.n.z);
-        G.sx(4 * j + 3, __uint_as_float(pk));
+        G.sx(4 * j + 3, bits_to<real>(pk));
 #else
         // the pair's manifold header into registers: j is wave-uniform, so this is a
         // scalar switch, not a dynamically indexed register array
@@ -1399,7 +1376,7 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, float* pool
             default: T.n[4] = C.n; T.pk[4] = pk; break;
         }
 #endif
-        if (live) G.sw(CP_SF_WS_ID(0, j), __uint_as_float(nid));
+        if (live) G.sw(CP_SF_WS_ID(0, j), bits_to<real>(nid));
     };
 #ifdef CP_NO_GROUND_PEEL
 #pragma unroll 1
@@ -1414,37 +1391,37 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, float* pool
 #pragma unroll
     for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
         T.n[j] = mk(G.lx(4 * j + 0), G.lx(4 * j + 1), G.lx(4 * j + 2));
-        T.pk[j] = __float_as_uint(G.lx(4 * j + 3));
+        T.pk[j] = to_bits(G.lx(4 * j + 3));
     }
 #endif
     CP_STAMP(t1);
     CP_ACC(narrow, t0, t1);
     // 3. unconstrained velocity update (both lanes, whole env)
-    const float kl = P.lin_damping, ka = P.ang_damping;
+    const real kl = P.lin_damping, ka = P.ang_damping;
 #pragma unroll
     for (int d = 0; d < CP_NUM_DYN; ++d) {
         const int g = d + 1;
-        const float im = P.inv_mass[g];
+        const real im = P.inv_mass[g];
         const Axes ax = quat_axes(S.b[d].q[0], S.b[d].q[1], S.b[d].q[2], S.b[d].q[3]);
         V3 v = S.b[d].v, w = S.b[d].w;
-        V3 F = (d == 0) ? S.f0 : ((d == 2) ? S.f2 : mk(0.0f, 0.0f, 0.0f));
-        float vlen = sqrtf(dot(v, v));
-        float dv = fmaf_(kl, vlen, kl);
-        V3 acc = mk(fmaf_(-v.x, dv, fmaf_(F.x, im, P.gravity[0])), fmaf_(-v.y, dv, fmaf_(F.y, im, P.gravity[1])),
-                    fmaf_(-v.z, dv, fmaf_(F.z, im, P.gravity[2])));
+        V3 F = (d == 0) ? S.f0 : ((d == 2) ? S.f2 : mk(real(0.0), real(0.0), real(0.0)));
+        real vlen = sqrt_(dot(v, v));
+        real dv = fma_(kl, vlen, kl);
+        V3 acc = mk(fma_(-v.x, dv, fma_(F.x, im, real(P.gravity[0]))), fma_(-v.y, dv, fma_(F.y, im, real(P.gravity[1]))),
+                    fma_(-v.z, dv, fma_(F.z, im, real(P.gravity[2]))));
         V3 wl = rot_t(ax, w);
         V3 Iwl = mk(P.inertia[g][0] * wl.x, P.inertia[g][1] * wl.y, P.inertia[g][2] * wl.z);
         V3 gl = cross(wl, Iwl);
         V3 al = mk(-(P.inv_inertia[g][0] * gl.x), -(P.inv_inertia[g][1] * gl.y), -(P.inv_inertia[g][2] * gl.z));
         V3 aw = rot(ax, al);
-        float wlen = sqrtf(dot(w, w));
-        float dw = fmaf_(ka, wlen, ka);
-        V3 accw = mk(fmaf_(-w.x, dw, aw.x), fmaf_(-w.y, dw, aw.y), fmaf_(-w.z, dw, aw.z));
+        real wlen = sqrt_(dot(w, w));
+        real dw = fma_(ka, wlen, ka);
+        V3 accw = mk(fma_(-w.x, dw, aw.x), fma_(-w.y, dw, aw.y), fma_(-w.z, dw, aw.z));
         S.b[d].v = madd(v, acc, dt);
         S.b[d].w = madd(w, accw, dt);
     }
-    S.f0 = mk(0.0f, 0.0f, 0.0f);  // 6. external forces are consumed by the step
-    S.f2 = mk(0.0f, 0.0f, 0.0f);
+    S.f0 = mk(real(0.0), real(0.0), real(0.0));  // 6. external forces are consumed by the step
+    S.f2 = mk(real(0.0), real(0.0), real(0.0));
     // 4. solve setup.  No cross-island contact: each lane solves its own island
     //    (oracle: independent islands); otherwise the env is "merged" and its cross
     //    rows run on both lanes.  (DPP reads the partner lane's register: evaluate it
@@ -1479,9 +1456,9 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, float* pool
 // Phase 3: whole-env velocities from the two lanes' islands (both lanes of every
 // env active), the warm-start cache refresh and the integration (DESIGN.md
 // §Physics model 5b-7).
-CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx& c, float* pool, const Mem& G,
+CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx& c, real* pool, const Mem& G,
                            Stamps& ST, bool live) {
-    const float dt = P.dt, inv_dt = P.inv_dt;
+    const real dt = P.dt, inv_dt = P.inv_dt;
     const bool second = L.isl != 0;
     CP_STAMP(t3);
     {
@@ -1503,32 +1480,32 @@ CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx
             const int cnt = pk_cnt(c.T.pk[j]), base = pk_base(c.T.pk[j]);
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                G.sl(CP_SF_WS_LAM(0, j, k), (k < cnt) ? pool_n(pool, F_LAM, base + k) : 0.0f);
+                G.sl(CP_SF_WS_LAM(0, j, k), (k < cnt) ? pool_n(pool, F_LAM, base + k) : real(0.0));
         }
     }
     // 5. integrate positions and orientations (both lanes, whole env)
-    const float hdt = 0.5f * dt;
-    const float c3 = ((dt * dt) * dt) * (float)0.020833333333;
-    const float maxang = P.max_angular_step;
+    const real hdt = real(0.5) * dt;
+    const real c3 = ((dt * dt) * dt) * (real)0.020833333333;
+    const real maxang = P.max_angular_step;
 #pragma unroll
     for (int d = 0; d < CP_NUM_DYN; ++d) {
         V3 v = S.b[d].v, w = S.b[d].w;
         S.b[d].x = madd(S.b[d].x, v, dt);
-        float ang = sqrtf(dot(w, w));
+        real ang = sqrt_(dot(w, w));
         if (ang * dt > maxang) ang = maxang * inv_dt;
-        float half = hdt * ang;
-        float sn, cs, s;
+        real half = hdt * ang;
+        real sn, cs, s;
         sincos_small(half, sn, cs);
-        if (ang < 0.001f) s = fmaf_(-c3, ang * ang, hdt);
+        if (ang < real(0.001)) s = fma_(-c3, ang * ang, hdt);
         else s = sn / ang;
-        float dx = w.x * s, dy = w.y * s, dz = w.z * s, dw = cs;
-        float qx = S.b[d].q[0], qy = S.b[d].q[1], qz = S.b[d].q[2], qw = S.b[d].q[3];
-        float rw = fmaf_(dw, qw, -fmaf_(dx, qx, fmaf_(dy, qy, dz * qz)));
-        float rx = fmaf_(dw, qx, fmaf_(dx, qw, fmaf_(dy, qz, -(dz * qy))));
-        float ry = fmaf_(dw, qy, fmaf_(dy, qw, fmaf_(dz, qx, -(dx * qz))));
-        float rz = fmaf_(dw, qz, fmaf_(dz, qw, fmaf_(dx, qy, -(dy * qx))));
-        float n2 = fmaf_(rx, rx, fmaf_(ry, ry, fmaf_(rz, rz, rw * rw)));
-        float inv = 1.0f / sqrtf(n2);
+        real dx = w.x * s, dy = w.y * s, dz = w.z * s, dw = cs;
+        real qx = S.b[d].q[0], qy = S.b[d].q[1], qz = S.b[d].q[2], qw = S.b[d].q[3];
+        real rw = fma_(dw, qw, -fma_(dx, qx, fma_(dy, qy, dz * qz)));
+        real rx = fma_(dw, qx, fma_(dx, qw, fma_(dy, qz, -(dz * qy))));
+        real ry = fma_(dw, qy, fma_(dy, qw, fma_(dz, qx, -(dx * qz))));
+        real rz = fma_(dw, qz, fma_(dz, qw, fma_(dx, qy, -(dy * qx))));
+        real n2 = fma_(rx, rx, fma_(ry, ry, fma_(rz, rz, rw * rw)));
+        real inv = real(1.0) / sqrt_(n2);
         S.b[d].q[0] = rx * inv;
         S.b[d].q[1] = ry * inv;
         S.b[d].q[2] = rz * inv;
@@ -1545,7 +1522,7 @@ CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx
 // One p.stepSimulation() for this lane's env.
 // FAST: fast-form island rows where the wave allows them (the 512-register kernels).
 template <bool FAST = false>
-CP_DEV void substep(Sim& S, const cp_physics& P, const Lane& L, float* pool, float* pool0, int& overflow,
+CP_DEV void substep(Sim& S, const cp_physics& P, const Lane& L, real* pool, real* pool0, int& overflow,
                     const Mem& G, Stamps& ST, bool live = true) {
     Ctx c;
     substep_prep(S, P, L, pool, pool0, overflow, G, ST, live, c);
@@ -1558,12 +1535,12 @@ CP_DEV void substep(Sim& S, const cp_physics& P, const Lane& L, float* pool, flo
 
 // LINK_FRAME force at the COM on cart (C = 0) or cart2 (C = 1): world = R(q) f
 template <int C>
-CP_DEV void apply_force_link(Sim& S, float fx, float fy) {
+CP_DEV void apply_force_link(Sim& S, real fx, real fy) {
     const Body& B = S.b[C == 0 ? 0 : 2];
     Axes A = quat_axes(B.q[0], B.q[1], B.q[2], B.q[3]);
-    V3 fw = rot(A, mk(fx, fy, 0.0f));
+    V3 fw = rot(A, mk(fx, fy, real(0.0)));
     if constexpr (C == 0) S.f0 = add(S.f0, fw);
     else S.f2 = add(S.f2, fw);
 }
 
-}  // namespace cp
+}  // namespace CP_NS

@@ -18,7 +18,7 @@
 #include <hip/hip_fp16.h>
 
 #include "../../include/cartpole_amd.h"
-#include "cp_math.h"
+// (uses namespace cp's fp32 math: included after the fp32 instantiation of cp_math.h)
 
 namespace cp {
 

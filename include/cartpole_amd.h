@@ -24,7 +24,8 @@
  *                 kind 1: int8    [B][2]     discrete table (see CP_DISCRETE_TABLE)
  *   reward        float32 [B]            (1.0 per step, bullet_cartpole.py:260)
  *   done          uint8   [B]
- *   state (get/set) float32 [CP_STATE_FIELDS][B]  (SoA; see CP_SF_* below)
+ *   state (get/set) [CP_STATE_FIELDS][B] SoA of the handle's real type: float32, or
+ *                 float64 when cfg.precision == CP_PRECISION_F64 (see CP_SF_* below)
  *   pixels        float16 [B][H][W][3][C][R]  raster obs (--use-raw-pixels,
  *                 bullet_cartpole.py:277-306; cp_set_raster)
  */
@@ -37,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CP_ABI_VERSION 1
+#define CP_ABI_VERSION 2
 
 /* Bodies, in the reference's loadURDF order (bullet_cartpole.py:154-160). */
 #define CP_BODY_GROUND 0
@@ -126,7 +127,17 @@ typedef struct cp_config {
     uint64_t seed;               /* Philox key                                 */
     int64_t env_id_offset;       /* global id of env 0 (rank * B when sharded) */
     cp_physics phys;
+    int32_t precision;           /* CP_PRECISION_F32 (the product path) or _F64  */
 } cp_config;
+
+/* Arithmetic type of a handle (cp_config.precision).  F32: the fp32 kernels, state float32.
+ * F64: the same algorithm in double precision (the parity variant: bit-exact against the
+ * oracle's fp64 build, the precision of pybullet's double btScalar), state float64 (the
+ * integer fields' int32 bits in the first 4 bytes of their 8-byte field); obs, terminal
+ * obs, readback, 8-states and pixels stay float32, as the reference's state array
+ * (bullet_cartpole.py:148).  The fp64 kernels run one 512-register wave per SIMD. */
+#define CP_PRECISION_F32 0
+#define CP_PRECISION_F64 1
 
 #define CP_BUMP_PHILOX 0   /* theta = 2*pi*U, U from Philox4x32-10(seed; env, episode, k) */
 #define CP_BUMP_HOST   1   /* parity mode: host supplies the 60 bump forces per env      */
@@ -194,7 +205,8 @@ int cp_set_bump_forces(cp_handle* h, const float* forces, void* stream);
 int cp_set_lqr(cp_handle* h, const float* gains, int per_env, float* state8_out, float done_pos,
                float done_angle);
 
-/* Full env state, SoA float32 [CP_STATE_FIELDS][B] (device pointers). */
+/* Full env state, SoA [CP_STATE_FIELDS][B] of the handle's real type (float32, or float64
+ * for CP_PRECISION_F64 handles), device pointers. */
 int cp_get_state(cp_handle* h, float* state_out, void* stream);
 int cp_set_state(cp_handle* h, const float* state_in, void* stream);
 

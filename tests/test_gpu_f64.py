@@ -1,0 +1,106 @@
+"""The fp64 variant (cp_config.precision = CP_PRECISION_F64, namespace cp64) against the
+oracle's fp64 build: the same algorithm in double precision (pybullet's btScalar), state
+kept in double between steps.  Same bar as the fp32 path: bit-exact obs (float32 outputs),
+done, terminal obs, readback, 8-states and the full float64 state SoA."""
+import numpy as np
+import pytest
+import torch
+
+from cartpoleplusplus_amd import abi, native
+from cartpoleplusplus_amd.batched import BatchedCartpole
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(O, **kw):
+    cfg = native.default_config(**kw)
+    cfg.precision = abi.CP_PRECISION_F64
+    gpu = BatchedCartpole(cfg.num_envs, 0, config=abi.cp_config.from_buffer_copy(cfg))
+    orc = O.Envs(abi.cp_config.from_buffer_copy(cfg), precision="f64")
+    return gpu, orc
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def _same(a, b, what):
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.dtype == b.dtype, (what, a.dtype, b.dtype)
+    if not np.array_equal(a, b):
+        d = np.abs(a.astype(np.float64) - b.astype(np.float64))
+        raise AssertionError(f"{what}: {np.count_nonzero(d)} differ, max |diff| {np.nanmax(d):.3e}")
+
+
+def _state(gpu, orc, what):
+    g = _np(gpu.get_state())
+    assert g.dtype == np.float64
+    _same(g.view(np.uint64), orc.get_state().view(np.uint64), what + " state bits")
+
+
+def test_f64_reset_and_200_continuous_steps(oracle_mod):
+    B = 64
+    gpu, orc = _pair(oracle_mod, num_envs=B, action_repeats=3, initial_force=55.0, seed=7)
+    _same(_np(gpu.reset()), orc.reset(), "reset obs")
+    _state(gpu, orc, "reset")
+    rng = np.random.default_rng(11)
+    for t in range(200):
+        a = rng.uniform(-1, 1, (B, 2, 2)).astype(np.float32)
+        go, gr, gd = gpu.step(torch.from_numpy(a).cuda())
+        oo, orw, od = orc.step(a)
+        _same(_np(go), oo, f"obs step {t}")
+        _same(_np(gd), od, f"done step {t}")
+        if t % 50 == 49:
+            _state(gpu, orc, f"step {t}")
+    assert _np(gd).all()
+
+
+def test_f64_discrete_autoreset_bounds_and_readback(oracle_mod):
+    B = 70
+    gpu, orc = _pair(oracle_mod, num_envs=B, action_repeats=2, steps_per_repeat=2, initial_force=55.0, seed=3,
+                     autoreset=1, done_on_bounds=1, max_episode_len=30)
+    gpu.enable_readback(True, reference_bug=False)
+    _same(_np(gpu.reset()), orc.reset(), "reset")
+    rng = np.random.default_rng(2)
+    for t in range(70):
+        a = rng.integers(0, 5, (B, 2)).astype(np.int8)
+        go, gr, gd = gpu.step(torch.from_numpy(a).cuda())
+        oo, orw, od, ot, orb = orc.step(a, terminal=True, readback=True, readback_bug=False)
+        _same(_np(go), oo, f"obs step {t}")
+        _same(_np(gd), od, f"done step {t}")
+        done = od.astype(bool)
+        _same(_np(gpu.terminal_obs)[done], ot[done], f"terminal obs step {t}")
+        _same(_np(gpu.readback), orb, f"readback step {t}")
+    _state(gpu, orc, "autoreset")
+    _same(_np(gpu.episode_returns()[0]), orc.episode_returns()[0], "returns")
+
+
+def test_f64_host_bumps_and_lqr(oracle_mod):
+    from cartpoleplusplus_amd import lqr
+    B = 40
+    gpu, orc = _pair(oracle_mod, num_envs=B, action_repeats=3, bump_mode=abi.CP_BUMP_HOST, autoreset=1)
+    rng = np.random.default_rng(4)
+    f = rng.uniform(-100, 100, (B, 30, 2, 2)).astype(np.float32)
+    gpu.set_bump_forces(torch.from_numpy(f).cuda())
+    orc.set_bump_forces(f)
+    gains = (np.asarray(lqr.exact_gains(), np.float32)[None] * rng.uniform(0.5, 1.5, (B, 1, 1, 1))).astype(np.float32)
+    gpu.enable_lqr(gains, per_env=True, state8=True, done_pos=3.0, done_angle=float(np.pi / 4))
+    orc.set_lqr(gains, per_env=True, state8=True, done_pos=3.0, done_angle=float(np.pi / 4))
+    _same(_np(gpu.reset()), orc.reset(), "reset obs")
+    for t in range(40):
+        a = rng.uniform(-0.2, 0.2, (B, 2, 2)).astype(np.float32)
+        go, _, gd = gpu.step(torch.from_numpy(a).cuda())
+        oo, _, od = orc.step(a)
+        _same(_np(go), oo, f"obs step {t}")
+        _same(_np(gd), od, f"done step {t}")
+        _same(_np(gpu.state8), orc.state8, f"8-state step {t}")
+    _state(gpu, orc, "lqr")
+
+
+def test_f64_state_dtype_is_enforced():
+    env = BatchedCartpole(8, 0, action_repeats=2, precision="f64")
+    s = env.get_state()
+    assert s.dtype == torch.float64 and s.shape == (abi.CP_STATE_FIELDS, 8)
+    with pytest.raises(ValueError):
+        env.set_state(s.float())
+    env.set_state(s)
