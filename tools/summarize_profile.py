@@ -16,10 +16,14 @@ from collections import defaultdict
 
 
 def kernel_key(name):
+    ns = "cp64::" if "cp64::" in name else ""
     if "cp_step_kernel" in name:
         kind = "discrete" if ("<1>" in name or "<1," in name) else "continuous"
-        return f"cp_step_kernel<{kind}{',lqr' if 'true>' in name else ''}>"
-    for k in ("cp_reset_kernel", "cp_init_kernel", "cp_mask_to_list_kernel", "cp_render_small_kernel",
+        lqr = ",lqr" if ("<1, true" in name or "<0, true" in name) else ""
+        return f"{ns}cp_step_kernel<{kind}{lqr}>"
+    if "cp_reset_kernel" in name:
+        return f"{ns}cp_reset_kernel"
+    for k in ("cp_init_kernel", "cp_mask_to_list_kernel", "cp_render_small_kernel",
               "cp_render_kernel", "cp_raster_table_kernel", "cp_event_kernel"):
         if k in name:
             return k
