@@ -40,11 +40,15 @@ def up_to_date(lib=LIB):
     return all(os.path.getmtime(d) <= t for d in DEPS)
 
 
-def build(force=False, verbose=False, stamps=False):
+def build(force=False, verbose=False, stamps=False, variant=None, defines=()):
+    """variant: build a diagnostic library libcartpole_hip_<variant>.so with extra -D defines
+    (tools/variant_bench.sh runs it through CP_LIB_PATH)."""
     lib = STAMPS_LIB if stamps else LIB
+    if variant:
+        lib = os.path.join(HERE, f"libcartpole_hip_{variant}.so")
     if not force and up_to_date(lib):
         return lib
-    extra = ["-DCP_STAMPS"] if stamps else []
+    extra = (["-DCP_STAMPS"] if stamps else []) + [f"-D{d}" for d in defines]
     objs, procs = [], []
     for src in SRCS:
         obj = lib + "." + os.path.basename(src) + ".o"
@@ -68,6 +72,10 @@ def build(force=False, verbose=False, stamps=False):
 
 
 if __name__ == "__main__":
+    if "--variant" in sys.argv:  # python -m cartpoleplusplus_amd.build --variant TAG DEF1 DEF2 ...
+        i = sys.argv.index("--variant")
+        print(build(force=True, verbose=True, variant=sys.argv[i + 1], defines=sys.argv[i + 2:]))
+        sys.exit(0)
     print(build(force="--force" in sys.argv, verbose=True))
     if "--stamps" in sys.argv:
         print(build(force="--force" in sys.argv, verbose=True, stamps=True))

@@ -256,6 +256,7 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     const Mem G = Mem::make(b.state, b.scratch, B, i, isl);
     const Lane L = Lane::make(isl, cfg.phys);
     Stamps ST;
+    CP_STAMP(k0);
     Sim S;
     load_sim(S, G.st, G.off);  // pending forces survive the reset (pybullet keeps them)
     const int episode = ldi(G.st, CP_SF_EPISODE, G.off);
@@ -275,7 +276,7 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     int ov = 0;
     const int nsub = cfg.settle_steps + cfg.initial_force_steps;
     for (int s = 0; s < nsub; ++s) {
-        substep<LAT && !kF64>(S, cfg.phys, L, pool, pool0, ov, G, ST);
+        substep<LAT && !kF64, LAT && !kF64>(S, cfg.phys, L, pool, pool0, ov, G, ST);
         const int k = s - cfg.settle_steps;
         if (k >= 0) {
             real fx, fy;
@@ -286,6 +287,10 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
         }
     }
     ov += (int)partner_u((uint32_t)ov);
+#ifdef CP_STAMPS
+    CP_STAMP(k1);
+    flush_stamps(ST, b.stamps + 16, k1 - k0);  // the reset kernel's counters: slots 16-26
+#endif
     if (!lead) return;
     store_sim(S, G.st, G.off);
     b.overflow[i] += ov;

@@ -1127,6 +1127,34 @@ CP_DEV bool fast_grow(Dyn& b, real imb, V3 t, V3 rbt, V3 ib, real inv_eff, real 
     return abs_(dl) > tol * inv_eff;  // Bullet residual test (oracle: solve_row)
 }
 
+// fast_grow for a ground manifold whose normal is exactly +z (wave-uniform choice, as
+// isl_row_ez): KIND 0 the normal n = (0, 0, 1), 1 the tangent t1 = (0, -1, 0), 2 the tangent
+// t2 = (1, -0, -0).  The precomputed r x t of such a row has one exact-zero component and
+// M (r x t) equals isl_row_ez's reduced products (FMA(m, x, +-0) = m x), so these are
+// isl_row_ez's operations with its r x t and M (r x t) precomputed.
+template <int KIND, bool FRICTION>
+CP_DEV bool fast_grow_ez(Dyn& b, real imb, const V3& rbt, const V3& ib, real inv_eff, real target, real& lam,
+                         real bound, real tol) {
+    real vn;
+    if constexpr (KIND == 0) vn = b.v.z + fma_(b.w.x, rbt.x, b.w.y * rbt.y);        // r x n = (rb.y, -rb.x, 0)
+    else if constexpr (KIND == 1) vn = -b.v.y + fma_(b.w.x, rbt.x, b.w.z * rbt.z);  // r x t1 = (rb.z, 0, -rb.x)
+    else vn = b.v.x + fma_(b.w.y, rbt.y, b.w.z * rbt.z);                             // r x t2 = (0, rb.z, -rb.y)
+    const real e = target - vn;
+    real dl = e * inv_eff;
+    const real l0 = lam + dl;
+    real ln;
+    if constexpr (!FRICTION) ln = l0 > real(0.0) ? l0 : real(0.0);
+    else ln = bound > real(0.0) ? clamp_sym(l0, bound) : lam;
+    dl = ln - lam;
+    lam = ln;
+    const real sb = dl * imb;
+    if constexpr (KIND == 0) b.v.z = b.v.z + sb;
+    else if constexpr (KIND == 1) b.v.y = b.v.y - sb;
+    else b.v.x = b.v.x + sb;
+    b.w = madd(b.w, ib, dl);
+    return abs_(dl) > tol * inv_eff;  // Bullet residual test (oracle: solve_row)
+}
+
 // one cart-pole normal row: isl_row<1, 2, false> with both bodies' terms precomputed
 CP_DEV bool fast_crow(Isl& I, V3 t, const CRow& R, real& lam, real tol) {
     const real vn = (dot(t, sub(I.d2.v, I.d1.v)) + dot(I.d2.w, R.rbt)) - dot(I.d1.w, R.rat);
@@ -1145,28 +1173,94 @@ CP_DEV bool fast_crow(Isl& I, V3 t, const CRow& R, real& lam, real tol) {
     return abs_(dl) > tol * R.ie;  // Bullet residual test (oracle: solve_row)
 }
 
+// The settle structure: the island's cart on the ground (4 rows of local pair 0, normal
+// exactly +z) and its pole standing on the cart (4 rows of local pair 2), no other rows, no
+// cross contact.  Every island of a reset's 100 settle substeps, and ~85 % of the islands
+// that run to the sweep cap in the step.
+CP_DEV bool c44_ok(const Ctx& c) {
+    return pk_cnt(c.T.pk[0]) == 4 && pk_cnt(c.T.pk[2]) == 4 && pk_cnt(c.T.pk[1]) == 0 && !c.merged &&
+           is_plus_z(c.T.n[0]);
+}
+
+// sweeps_fast when every active lane of the wave has the settle structure: the same rows in
+// the same order (4 ground rows in +z form, then 4 cart-pole rows; no friction, no cross
+// rows), straight-line, without the per-row lane guards of the general loop.
+CP_DEV void sweeps_c44(Ctx& c, FastIsl& F, real tol, int it0, int it1, Stamps& ST) {
+    const V3 n2 = c.T.n[2];
+    for (int it = it0; it < it1; ++it) {
+        if (__ballot(c.active) == 0ull) break;
+#ifdef CP_STAMPS
+        ST.sweeps += 1;
+#endif
+        bool bad = false;
+        if (c.active) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                bad |= fast_grow_ez<0, false>(c.I.d1, c.I.im1, F.g0[k].rbt, F.g0[k].ib, F.g0[k].ie, F.g0[k].tg,
+                                              F.g0[k].lam, real(0.0), tol);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) bad |= fast_crow(c.I, n2, F.c2[k], F.c2[k].lam, tol);
+        }
+        const uint32_t pbad = partner_u(bad ? 1u : 0u);  // every lane that entered the loop is here
+        if (c.active && !bad && pbad == 0u) c.active = false;
+    }
+}
+
 // sweeps() with the island rows in fast form (same row order, same stopping rule)
+template <bool C44>
 CP_DEV void sweeps_fast(Ctx& c, FastIsl& F, Sim& S, const cp_physics& P, real* pool, real* pool0, bool second,
                         int it0, int it1, Stamps& ST) {
     const real tol = sqrt_(real(P.residual_threshold));  // oracle: SQRT((real)threshold)
     const int cnt0 = pk_cnt(c.T.pk[0]), cnt1 = pk_cnt(c.T.pk[1]), cnt2 = pk_cnt(c.T.pk[2]);
     const int fc1 = pk_fcnt(c.T.pk[1]);
     const V3 n0 = c.T.n[0], n1 = c.T.n[1], n2 = c.T.n[2];
+    // ground pairs whose rows all have a +z normal in this wave run fast_grow_ez (wave-uniform)
+#ifdef CP_NO_EZ
+    const bool ez0 = false, ez1 = false;
+#else
+    const bool ez0 = __ballot(cnt0 > 0 && !is_plus_z(n0)) == 0ull;
+    const bool ez1 = __ballot(cnt1 > 0 && !is_plus_z(n1)) == 0ull;
+#endif
     for (int it = it0; it < it1; ++it) {
         if (__ballot(c.active) == 0ull) break;
+#ifndef CP_NO_C44
+        // every still-active lane of the wave in the settle structure: the guard-free loop
+        // (the reset kernel's option: there every settle substep is in it; in the step kernel
+        // the periodic test cost more than it saved, 0.450 -> 0.480 ms at B = 4,096)
+        if constexpr (C44) {
+            if ((it - it0) % 8 == 0 && __ballot(c.active && !c44_ok(c)) == 0ull) {
+                sweeps_c44(c, F, tol, it, it1, ST);
+                return;
+            }
+        }
+#endif
 #ifdef CP_STAMPS
         ST.sweeps += 1;
 #endif
         bool bad = false, badc = false;
         if (c.active) {
+            if (ez0) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (k < cnt0) bad |= fast_grow<false>(c.I.d1, c.I.im1, n0, F.g0[k].rbt, F.g0[k].ib, F.g0[k].ie,
-                                                      F.g0[k].tg, F.g0[k].lam, real(0.0), tol);
+                for (int k = 0; k < 4; ++k)
+                    if (k < cnt0) bad |= fast_grow_ez<0, false>(c.I.d1, c.I.im1, F.g0[k].rbt, F.g0[k].ib, F.g0[k].ie,
+                                                                F.g0[k].tg, F.g0[k].lam, real(0.0), tol);
+            } else {
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (k < cnt1) bad |= fast_grow<false>(c.I.d2, c.I.im2, n1, F.g1[k].rbt, F.g1[k].ib, F.g1[k].ie,
-                                                      F.g1[k].tg, F.g1[k].lam, real(0.0), tol);
+                for (int k = 0; k < 4; ++k)
+                    if (k < cnt0) bad |= fast_grow<false>(c.I.d1, c.I.im1, n0, F.g0[k].rbt, F.g0[k].ib, F.g0[k].ie,
+                                                          F.g0[k].tg, F.g0[k].lam, real(0.0), tol);
+            }
+            if (ez1) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (k < cnt1) bad |= fast_grow_ez<0, false>(c.I.d2, c.I.im2, F.g1[k].rbt, F.g1[k].ib, F.g1[k].ie,
+                                                                F.g1[k].tg, F.g1[k].lam, real(0.0), tol);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (k < cnt1) bad |= fast_grow<false>(c.I.d2, c.I.im2, n1, F.g1[k].rbt, F.g1[k].ib, F.g1[k].ie,
+                                                          F.g1[k].tg, F.g1[k].lam, real(0.0), tol);
+            }
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 if (k < cnt2) bad |= fast_crow(c.I, n2, F.c2[k], F.c2[k].lam, tol);
@@ -1181,14 +1275,27 @@ CP_DEV void sweeps_fast(Ctx& c, FastIsl& F, Sim& S, const cp_physics& P, real* p
             cross_back(c.I, S, second);
         }
         if (c.active) {
+            if (ez1) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (k < fc1) {
-                    const real bound = c.mu1 * F.g1[k].lam;
-                    bad |= fast_grow<true>(c.I.d2, c.I.im2, F.t1, F.f1[k].rbt1, F.f1[k].ib1, F.f1[k].ie1, real(0.0),
-                                           F.f1[k].l1, bound, tol);
-                    bad |= fast_grow<true>(c.I.d2, c.I.im2, F.t2, F.f1[k].rbt2, F.f1[k].ib2, F.f1[k].ie2, real(0.0),
-                                           F.f1[k].l2, bound, tol);
+                for (int k = 0; k < 4; ++k) {
+                    if (k < fc1) {
+                        const real bound = c.mu1 * F.g1[k].lam;
+                        bad |= fast_grow_ez<1, true>(c.I.d2, c.I.im2, F.f1[k].rbt1, F.f1[k].ib1, F.f1[k].ie1,
+                                                     real(0.0), F.f1[k].l1, bound, tol);
+                        bad |= fast_grow_ez<2, true>(c.I.d2, c.I.im2, F.f1[k].rbt2, F.f1[k].ib2, F.f1[k].ie2,
+                                                     real(0.0), F.f1[k].l2, bound, tol);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (k < fc1) {
+                        const real bound = c.mu1 * F.g1[k].lam;
+                        bad |= fast_grow<true>(c.I.d2, c.I.im2, F.t1, F.f1[k].rbt1, F.f1[k].ib1, F.f1[k].ie1,
+                                               real(0.0), F.f1[k].l1, bound, tol);
+                        bad |= fast_grow<true>(c.I.d2, c.I.im2, F.t2, F.f1[k].rbt2, F.f1[k].ib2, F.f1[k].ie2,
+                                               real(0.0), F.f1[k].l2, bound, tol);
+                    }
                 }
             }
         }
@@ -1221,7 +1328,7 @@ CP_DEV void fast_store(const FastIsl& F, const Ctx& c, real* pool) {
 // PGS sweeps [it0, it1) of the lane's island.  FAST: fast-form island rows when no
 // lane of the wave has friction rows on local pairs 0 / 2 (wave-uniform choice; the
 // fast form needs the register budget of the 1-wave-per-SIMD latency kernels).
-template <bool FAST>
+template <bool FAST, bool C44 = false>
 CP_DEV void solve_range(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0, bool second, int it0, int it1,
                         Stamps& ST) {
 #ifndef CP_NO_FAST_ROWS
@@ -1229,7 +1336,7 @@ CP_DEV void solve_range(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* p
         if (__ballot(!fast_ok(c)) == 0ull) {
             FastIsl F;
             fast_build(F, c, pool);
-            sweeps_fast(c, F, S, P, pool, pool0, second, it0, it1, ST);
+            sweeps_fast<C44>(c, F, S, P, pool, pool0, second, it0, it1, ST);
             fast_store(F, c, pool);
             return;
         }
@@ -1520,14 +1627,15 @@ CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx
 
 
 // One p.stepSimulation() for this lane's env.
-// FAST: fast-form island rows where the wave allows them (the 512-register kernels).
-template <bool FAST = false>
+// FAST: fast-form island rows where the wave allows them (the 512-register kernels);
+// C44: with the guard-free settle-structure loop (sweeps_c44; the latency-shaped reset).
+template <bool FAST = false, bool C44 = false>
 CP_DEV void substep(Sim& S, const cp_physics& P, const Lane& L, real* pool, real* pool0, int& overflow,
                     const Mem& G, Stamps& ST, bool live = true) {
     Ctx c;
     substep_prep(S, P, L, pool, pool0, overflow, G, ST, live, c);
     CP_STAMP(t2);
-    solve_range<FAST>(c, S, P, pool, pool0, L.isl != 0, 0, P.solver_iterations, ST);
+    solve_range<FAST, C44>(c, S, P, pool, pool0, L.isl != 0, 0, P.solver_iterations, ST);
     CP_STAMP(t3);
     CP_ACC(solve, t2, t3);
     substep_finish(S, P, L, c, pool, G, ST, live);

@@ -233,13 +233,13 @@ int cp_timing_end(cp_handle* h, double* step_ms, int32_t* step_launches, double*
  * returned by cp_timing_end are the sampled ones. */
 int cp_timing_stride(cp_handle* h, int step_stride, int reset_stride);
 
-/* Diagnostics of a stamp build (-DCP_STAMPS): host array of 16 counters summed over
- * waves since the last reset, 8 for the step / head kernel then 8 for the tail
- * kernel: s_memtime cycles in narrowphase, velocity update + warm start, PGS sweeps,
- * integration + cache; sweep count, substep count, total kernel cycles, waves.
- * Synchronises the device.  Returns 1 in a stamp build, 0 otherwise (counters then
- * stay 0). */
-int cp_debug_stamps(cp_handle* h, uint64_t* out16, int reset);
+/* Diagnostics of a stamp build (-DCP_STAMPS): host array of 32 counters summed over
+ * waves since the last reset: slots 0-7 for the step kernel, 16-23 for the reset kernel,
+ * each: s_memtime cycles in narrowphase + row setup, velocity update + warm start, PGS
+ * sweeps, integration + cache; sweep count, substep count, total kernel cycles, waves;
+ * slots 8-10 / 24-26 split the narrowphase (body selection, box_box, row setup).
+ * Synchronises the device.  Returns 1 in a stamp build, 0 otherwise (counters then stay 0). */
+int cp_debug_stamps(cp_handle* h, uint64_t* out32, int reset);
 
 /* ---- Raster observation (--use-raw-pixels) ----------
  * Replaces render_rgb + set_state_element_for_repeat (bullet_cartpole.py:277-306):
