@@ -125,3 +125,41 @@ def test_product_never_imports_oracle():
             if f.endswith((".py", ".hip", ".h", ".cpp")):
                 src = open(os.path.join(dirpath, f)).read()
                 assert not pat.search(src), f
+
+
+def test_cp_create_rejects_inconsistent_derived_fields():
+    """cp_create validates the host-computed fields before touching a GPU:
+    dt / inv_dt, tan / sin of the angle threshold, the precision flag."""
+    import ctypes as C
+    from cartpoleplusplus_amd import native
+    lib = native.load()
+    h = C.c_void_p()
+    cfg = native.default_config(num_envs=4)
+    cfg.phys.dt = 1.0 / 120.0                     # inv_dt left at 240
+    assert lib.cp_create(C.byref(cfg), 0, C.byref(h)) != 0
+    assert b"inv_dt" in lib.cp_last_error(None)
+    cfg = native.default_config(num_envs=4)
+    cfg.angle_threshold = 0.5                     # tan/sin not recomputed
+    assert lib.cp_create(C.byref(cfg), 0, C.byref(h)) != 0
+    assert b"angle_threshold" in lib.cp_last_error(None)
+    cfg = native.default_config(num_envs=4, precision=7)
+    assert lib.cp_create(C.byref(cfg), 0, C.byref(h)) != 0
+    assert b"precision" in lib.cp_last_error(None)
+
+
+def test_device_buffer_checks_shape_and_dtype():
+    """Sizes the C-ABI trusts are checked with exceptions (not asserts) before any pointer
+    reaches cp_step / cp_reset / cp_set_* (ADVICE r1)."""
+    import torch
+    from cartpoleplusplus_amd.batched import _device_buffer
+    dev = torch.device("cpu")
+    ok = _device_buffer(torch.zeros(8, 2, dtype=torch.int8), (8, 2), torch.int8, dev, "a")
+    assert ok.shape == (8, 2) and ok.is_contiguous()
+    with pytest.raises(ValueError):
+        _device_buffer(torch.zeros(8, 2), (8, 2, 2), torch.float32, dev, "continuous actions")
+    with pytest.raises(ValueError):
+        _device_buffer(torch.zeros(7, 2, dtype=torch.int8), (8, 2), torch.int8, dev, "discrete actions")
+    with pytest.raises(ValueError):
+        _device_buffer(torch.zeros(8, 2, dtype=torch.float32), (8, 2), torch.int8, dev, "float as indices")
+    f = _device_buffer(torch.zeros(8, 2, 2, dtype=torch.float64), (8, 2, 2), torch.float32, dev, "a")
+    assert f.dtype == torch.float32

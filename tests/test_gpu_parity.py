@@ -246,3 +246,24 @@ def test_gym_mirror_matches_oracle_and_reference_errors(oracle_mod):
     with pytest.raises(TypeError):
         denv.step(2)                        # reference: 'int' object is not subscriptable
     denv.step([1, 4])
+
+
+def test_batched_rejects_wrong_buffers_before_the_abi():
+    """Shapes / dtypes the C-ABI would read blindly raise ValueError, and the
+    handle stays usable afterwards."""
+    env = BatchedCartpole(16, 0, action_repeats=2, autoreset=True)
+    env.reset()
+    with pytest.raises(ValueError):
+        env.step(torch.zeros((16, 2), device="cuda"))                   # float (B,2): not a continuous action
+    with pytest.raises(ValueError):
+        env.step(torch.zeros((8, 2), dtype=torch.int8, device="cuda"))  # short batch
+    with pytest.raises(ValueError):
+        env.step(torch.zeros((16, 2, 2), dtype=torch.int32, device="cuda"))
+    with pytest.raises(ValueError):
+        env.reset(mask=torch.ones(15, dtype=torch.uint8, device="cuda"))
+    with pytest.raises(ValueError):
+        env.set_bump_forces(torch.zeros((16, 29, 2, 2), device="cuda"))
+    with pytest.raises(ValueError):
+        env.set_state(torch.zeros((abi.CP_STATE_FIELDS, 15), device="cuda"))
+    o, r, d = env.step(torch.zeros((16, 2), dtype=torch.int8, device="cuda"))
+    assert torch.isfinite(o).all() and (r == 1).all()

@@ -195,3 +195,48 @@ def test_bump_stream_depends_on_env_and_episode(oracle_mod):
     cfg2 = oracle_mod.default_config(num_envs=4, action_repeats=2, initial_force=55.0, seed=9, env_id_offset=1)
     e2 = oracle_mod.Envs(cfg2)
     assert np.array_equal(e2.reset()[0], o1[1])  # global env id = offset + i
+
+
+def _settle(O, prec="f32", n=10, lift2=False, pre=60, **phys):
+    """Sweeps per substep of n substeps after `pre` settle substeps at the default rule (the
+    spawn poses start 5 mm apart: the first substeps' rows are speculative, with lambda 0)."""
+    w = O.World(O.default_config(), precision=prec)
+    if lift2:   # second assembly far above the first: island 1 without rows
+        w.reset_pose(3, (1.0, 0.0, 50.0), (0, 0, 0, 1))
+        w.reset_pose(4, (1.0, 0.0, 60.0), (0, 0, 0, 1))
+    for _ in range(pre):
+        w.step()
+    for k, v in phys.items():
+        setattr(w.cfg.phys, k, v)
+    its = []
+    for _ in range(n):
+        w.step()
+        its.append(w.last_iterations)
+    return its
+
+
+def test_stopping_rule_threshold_zero_runs_every_sweep(oracle_mod):
+    """Bullet's loop stops after the first sweep whose max squared row residual is <=
+    leastSquaresResidualThreshold, else after solver_iterations sweeps: with threshold 0,
+    resting contacts (nonzero corrections in every sweep) run all sweeps."""
+    assert _settle(oracle_mod, residual_threshold=0.0, solver_iterations=17) == [17] * 10
+
+
+def test_stopping_rule_huge_threshold_runs_one_sweep(oracle_mod):
+    """Any sweep passes a huge threshold: exactly one sweep per substep with rows (Bullet
+    checks after the sweep, so at least one always runs)."""
+    assert _settle(oracle_mod, residual_threshold=1e6) == [1] * 10
+
+
+def test_stopping_rule_default_between(oracle_mod):
+    its = _settle(oracle_mod, n=40)
+    assert all(1 <= i <= 50 for i in its) and max(its) > 1
+
+
+def test_one_stop_decision_per_env(oracle_mod):
+    """Both islands are one solver group: the env's sweep count is at
+    least what either assembly needs alone (here: the second assembly lifted out of contact)."""
+    for prec in ("f32", "f64"):
+        joint = _settle(oracle_mod, prec, n=30)
+        alone = _settle(oracle_mod, prec, n=30, lift2=True)
+        assert all(j >= a for j, a in zip(joint, alone))
