@@ -178,6 +178,11 @@ CP_DEV void for_cands(const FaceGeom& G, Fn&& fn) {
 }
 
 // Face contact (oracle: face_contact).  Fills up to 4 selected candidates.
+// ALLIN: when every lane of the wave that reaches this has all four incident vertices inside
+// the reference rectangle (the oracle's `inside == 4` exit: C1 candidates only, at most 4, so
+// no reduction), emit those directly instead of evaluating the 24 candidate slots: the same
+// points in the same order.  Every contact of a reset's settle substeps is of this kind.
+template <bool ALLIN = false>
 CP_DEV void face_contact(const Box& R, int ri, V3 nr, const Box& I, real margin, V3& fc, V3& u, V3& v,
                          Out4& out) {
     int r1 = ri == 2 ? 0 : ri + 1, r2 = ri == 0 ? 2 : ri - 1;
@@ -211,6 +216,28 @@ CP_DEV void face_contact(const Box& R, int ri, V3 nr, const Box& I, real margin,
 #pragma unroll
     for (int k = 0; k < 4; ++k) inside += (abs_(G.Pu[k]) <= G.hu && abs_(G.Pv[k]) <= G.hv) ? 1 : 0;
     G.all_in = inside == 4;
+    if constexpr (ALLIN) {
+        if (__ballot(!G.all_in) == 0ull) {
+            out.m = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (G.Pn[k] <= margin) {
+                    const int m = out.m;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        if (m == q) {
+                            out.u[q] = G.Pu[k];
+                            out.v[q] = G.Pv[k];
+                            out.n[q] = G.Pn[k];
+                            out.id[q] = k;
+                        }
+                    }
+                    out.m = m + 1;
+                }
+            }
+            return;
+        }
+    }
     G.idet = real(0.0);
     if (!G.all_in) {
         real det = fma_(G.e1u, G.e2v, -(G.e1v * G.e2u));
@@ -283,6 +310,7 @@ struct Contact {
 };
 
 // Box-box narrowphase (oracle: box_box).  Normal from A to B.
+template <bool ALLIN = false>
 CP_DEV void box_box(const Box& A, const Box& B, real margin, real edge_bias, Contact& C) {
     C.m = 0;
     V3 d = sub(B.c, A.c);
@@ -359,7 +387,7 @@ CP_DEV void box_box(const Box& A, const Box& B, real margin, real edge_bias, Con
         C.n = selv(fa, nr, neg(nr));
         V3 fc, u, v;
         Out4 o;
-        face_contact(R, ri, nr, I, margin, fc, u, v, o);
+        face_contact<ALLIN>(R, ri, nr, I, margin, fc, u, v, o);
         int code = (fa ? ri : 3 + ri) * 32;
         C.m = o.m;
 #pragma unroll
@@ -1373,6 +1401,7 @@ CP_DEV void island_view(const Sim& S, const Lane& L, Ctx& c) {
 // row setup of the lane's island, unconstrained velocity update of the whole env,
 // the island view and the warm start.  A lane with live == false (done env, padding)
 // makes no contacts and writes nothing.
+template <bool ALLIN = false>
 CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool, real* pool0, int& overflow,
                          const Mem& G, Stamps& ST, bool live, Ctx& c) {
     const real dt = P.dt, inv_dt = P.inv_dt;
@@ -1407,7 +1436,7 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
         C.m = 0;
         C.n = mk(real(0.0), real(0.0), real(1.0));
         CP_STAMP(n1);
-        if (live && !face_separated(A, Bx, P.contact_margin)) box_box(A, Bx, P.contact_margin, P.edge_bias, C);
+        if (live && !face_separated(A, Bx, P.contact_margin)) box_box<ALLIN>(A, Bx, P.contact_margin, P.edge_bias, C);
         CP_STAMP(n2);
         CP_ACC(sel, n0, n1);
         CP_ACC(bb, n1, n2);
@@ -1628,12 +1657,13 @@ CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx
 
 // One p.stepSimulation() for this lane's env.
 // FAST: fast-form island rows where the wave allows them (the 512-register kernels);
-// C44: with the guard-free settle-structure loop (sweeps_c44; the latency-shaped reset).
+// C44: the latency-shaped reset kernel's options: the guard-free settle-structure loop
+// (sweeps_c44) and the all-inside face-contact exit (face_contact<ALLIN>).
 template <bool FAST = false, bool C44 = false>
 CP_DEV void substep(Sim& S, const cp_physics& P, const Lane& L, real* pool, real* pool0, int& overflow,
                     const Mem& G, Stamps& ST, bool live = true) {
     Ctx c;
-    substep_prep(S, P, L, pool, pool0, overflow, G, ST, live, c);
+    substep_prep<C44>(S, P, L, pool, pool0, overflow, G, ST, live, c);
     CP_STAMP(t2);
     solve_range<FAST, C44>(c, S, P, pool, pool0, L.isl != 0, 0, P.solver_iterations, ST);
     CP_STAMP(t3);
