@@ -28,6 +28,10 @@ namespace CP_NS {
 // fp64: only the 1-wave-per-SIMD (512 VGPR) kernel shape, with the slow-form rows (the fast
 // form's precomputed rows do not fit twice the registers)
 constexpr bool kF64 = sizeof(real) == 8;
+#ifndef CP_ALLIN_STEP
+#define CP_ALLIN_STEP 1
+#endif
+constexpr bool kAllinStep = CP_ALLIN_STEP != 0;  // the all-inside face-contact exit in the step kernel (C3 kernel -0.6 %, C2 -2 %)
 
 using Bufs = cpc::Bufs;
 using Lqr = cpc::Lqr;
@@ -370,7 +374,7 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
             }
             for (int r = 0; r < R; ++r) {
                 for (int s = 0; s < SR; ++s) {
-                    substep<LAT && !kF64>(S, cfg.phys, L, pool, pool0, ov, G, ST);
+                    substep<LAT && !kF64, false, kAllinStep>(S, cfg.phys, L, pool, pool0, ov, G, ST);
                     if constexpr (LQR) {  // disturbance + control (:897-901), control from the pre-step state
                         apply_force_link<0>(S, f00 + u[0][0], f01 + u[0][1]);
                         apply_force_link<1>(S, f10 + u[1][0], f11 + u[1][1]);

@@ -1659,11 +1659,11 @@ CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx
 // FAST: fast-form island rows where the wave allows them (the 512-register kernels);
 // C44: the latency-shaped reset kernel's options: the guard-free settle-structure loop
 // (sweeps_c44) and the all-inside face-contact exit (face_contact<ALLIN>).
-template <bool FAST = false, bool C44 = false>
+template <bool FAST = false, bool C44 = false, bool ALLIN = C44>
 CP_DEV void substep(Sim& S, const cp_physics& P, const Lane& L, real* pool, real* pool0, int& overflow,
                     const Mem& G, Stamps& ST, bool live = true) {
     Ctx c;
-    substep_prep<C44>(S, P, L, pool, pool0, overflow, G, ST, live, c);
+    substep_prep<ALLIN>(S, P, L, pool, pool0, overflow, G, ST, live, c);
     CP_STAMP(t2);
     solve_range<FAST, C44>(c, S, P, pool, pool0, L.isl != 0, 0, P.solver_iterations, ST);
     CP_STAMP(t3);
