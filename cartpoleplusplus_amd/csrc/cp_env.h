@@ -280,7 +280,7 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     int ov = 0;
     const int nsub = cfg.settle_steps + cfg.initial_force_steps;
     for (int s = 0; s < nsub; ++s) {
-        substep<LAT && !kF64, LAT && !kF64>(S, cfg.phys, L, pool, pool0, ov, G, ST);
+        substep<LAT && !kF64, true>(S, cfg.phys, L, pool, pool0, ov, G, ST);
         const int k = s - cfg.settle_steps;
         if (k >= 0) {
             real fx, fy;

@@ -979,6 +979,9 @@ struct Ctx {
 // view.  Both lanes of an env stop together, after the first sweep in which no row of
 // the env (island 0, island 1, cross) has a squared residual above the threshold:
 // Bullet solves the two islands as one group (oracle: substep, step 4).
+CP_DEV bool c44_ok(const Ctx& c);
+CP_DEV void sweeps_c44_slow(Ctx& c, real* pool, real tol, int it0, int it1, Stamps& ST);
+template <bool C44 = false>
 CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0, bool second, int it0, int it1,
                    Stamps& ST) {
     const real tol = sqrt_(real(P.residual_threshold));  // oracle: SQRT((real)threshold)
@@ -997,6 +1000,12 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0,
 #endif
     for (int it = it0; it < it1; ++it) {
         if (__ballot(c.active) == 0ull) break;
+        if constexpr (C44) {  // every still-active lane in the settle structure (the reset kernels)
+            if ((it - it0) % 8 == 0 && __ballot(c.active && !c44_ok(c)) == 0ull) {
+                sweeps_c44_slow(c, pool, tol, it, it1, ST);
+                return;
+            }
+        }
 #ifdef CP_STAMPS
         ST.sweeps += 1;
 #endif
@@ -1234,6 +1243,40 @@ CP_DEV void sweeps_c44(Ctx& c, FastIsl& F, real tol, int it0, int it1, Stamps& S
     }
 }
 
+// sweeps() when every active lane of the wave has the settle structure, rows from the LDS
+// pool: then the ground-cart rows are pool slots 0-3 and the cart-pole rows slots 4-7 on every
+// lane (the pool fills in pair order), so the loop is straight-line with compile-time slots.
+CP_DEV void sweeps_c44_slow(Ctx& c, real* pool, real tol, int it0, int it1, Stamps& ST) {
+    const V3 n2 = c.T.n[2];
+    for (int it = it0; it < it1; ++it) {
+        if (__ballot(c.active) == 0ull) break;
+#ifdef CP_STAMPS
+        ST.sweeps += 1;
+#endif
+        bool bad = false;
+        if (c.active) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
+                real lam = pool_n(pool, F_LAM, s);
+                bad |= isl_row_ez<1, 0, false>(c.I, rb, pool_n(pool, F_IE, s), pool_n(pool, F_TG, s), lam, real(0.0),
+                                               tol);
+                pool_n(pool, F_LAM, s) = lam;
+            }
+#pragma unroll
+            for (int s = 4; s < 8; ++s) {
+                const V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
+                real lam = pool_n(pool, F_LAM, s);
+                bad |= isl_row<1, 2, false>(c.I, rb, n2, pool_n(pool, F_IE, s), pool_n(pool, F_TG, s), lam, real(0.0),
+                                            tol);
+                pool_n(pool, F_LAM, s) = lam;
+            }
+        }
+        const uint32_t pbad = partner_u(bad ? 1u : 0u);  // every lane that entered the loop is here
+        if (c.active && !bad && pbad == 0u) c.active = false;
+    }
+}
+
 // sweeps() with the island rows in fast form (same row order, same stopping rule)
 template <bool C44>
 CP_DEV void sweeps_fast(Ctx& c, FastIsl& F, Sim& S, const cp_physics& P, real* pool, real* pool0, bool second,
@@ -1370,7 +1413,7 @@ CP_DEV void solve_range(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* p
         }
     }
 #endif
-    sweeps(c, S, P, pool, pool0, second, it0, it1, ST);
+    sweeps<C44>(c, S, P, pool, pool0, second, it0, it1, ST);
 }
 
 // the lane's island view: its two bodies (cart, pole or cart2, pole2) with their world
