@@ -107,7 +107,13 @@ CP_DEV real sel3(real a, real b, real c, int i) { return i == 0 ? a : (i == 1 ? 
 CP_DEV V3 sel3v(V3 a, V3 b, V3 c, int i) { return mk(sel3(a.x, b.x, c.x, i), sel3(a.y, b.y, c.y, i), sel3(a.z, b.z, c.z, i)); }
 CP_DEV V3 selv(bool t, V3 a, V3 b) { return mk(t ? a.x : b.x, t ? a.y : b.y, t ? a.z : b.z); }
 CP_DEV V3 axis_of(const Axes& A, int i) { return sel3v(A.a0, A.a1, A.a2, i); }
-CP_DEV real h_of(const Box& B, int i) { return i == 0 ? B.h0 : (i == 1 ? B.h1 : B.h2); }
+// (opaque register copies: a select chain over the fields would otherwise become one load through
+// a computed address and keep the box in private memory)
+CP_DEV real h_of(const Box& B, int i) {
+    real h0 = B.h0, h1 = B.h1, h2 = B.h2;
+    asm("" : "+v"(h0), "+v"(h1), "+v"(h2));
+    return i == 0 ? h0 : (i == 1 ? h1 : h2);
+}
 
 // contact point candidate (reference-face coordinates u, v and separation n)
 struct Out4 {
@@ -306,7 +312,8 @@ struct Contact {
     int m;         // points
     V3 p[4];       // world contact points (midway between the surfaces)
     real d[4];    // signed separation (negative = penetration)
-    int id[4];     // feature ids (warm-start keys)
+    uint32_t ids;  // feature ids (warm-start keys), one byte per point (an int array here is
+                   // written under path-dependent indices and lands in private memory)
 };
 
 // Box-box narrowphase (oracle: box_box).  Normal from A to B.
@@ -372,17 +379,22 @@ CP_DEV void box_box(const Box& A, const Box& B, real margin, real edge_bias, Con
         int ri = fa ? bi : bj;
         real sg = fa ? ((sel3(da[0], da[1], da[2], bi) >= real(0.0)) ? real(1.0) : -real(1.0))
                       : ((sel3(db[0], db[1], db[2], bj) >= real(0.0)) ? -real(1.0) : real(1.0));
+        // the half extents as opaque register values: a select between two boxes' fields
+        // otherwise becomes one load through a selected address, which puts both boxes
+        // (and R, I) in private memory (scratch traffic every pair of every substep)
+        real ah0 = A.h0, ah1 = A.h1, ah2 = A.h2, bh0 = B.h0, bh1 = B.h1, bh2 = B.h2;
+        asm("" : "+v"(ah0), "+v"(ah1), "+v"(ah2), "+v"(bh0), "+v"(bh1), "+v"(bh2));
         Box R, I;
         R.c = selv(fa, A.c, B.c);
         R.ax.a0 = selv(fa, A.ax.a0, B.ax.a0);
         R.ax.a1 = selv(fa, A.ax.a1, B.ax.a1);
         R.ax.a2 = selv(fa, A.ax.a2, B.ax.a2);
-        R.h0 = fa ? A.h0 : B.h0; R.h1 = fa ? A.h1 : B.h1; R.h2 = fa ? A.h2 : B.h2;
+        R.h0 = fa ? ah0 : bh0; R.h1 = fa ? ah1 : bh1; R.h2 = fa ? ah2 : bh2;
         I.c = selv(fa, B.c, A.c);
         I.ax.a0 = selv(fa, B.ax.a0, A.ax.a0);
         I.ax.a1 = selv(fa, B.ax.a1, A.ax.a1);
         I.ax.a2 = selv(fa, B.ax.a2, A.ax.a2);
-        I.h0 = fa ? B.h0 : A.h0; I.h1 = fa ? B.h1 : A.h1; I.h2 = fa ? B.h2 : A.h2;
+        I.h0 = fa ? bh0 : ah0; I.h1 = fa ? bh1 : ah1; I.h2 = fa ? bh2 : ah2;
         V3 nr = scl(axis_of(R.ax, ri), sg);
         C.n = selv(fa, nr, neg(nr));
         V3 fc, u, v;
@@ -390,11 +402,12 @@ CP_DEV void box_box(const Box& A, const Box& B, real margin, real edge_bias, Con
         face_contact<ALLIN>(R, ri, nr, I, margin, fc, u, v, o);
         int code = (fa ? ri : 3 + ri) * 32;
         C.m = o.m;
+        C.ids = 0u;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             C.p[k] = madd(madd(madd(fc, u, o.u[k]), v, o.v[k]), nr, o.n[k] * real(0.5));
             C.d[k] = o.n[k];
-            C.id[k] = o.id[k] + code;
+            C.ids |= (uint32_t)(o.id[k] + code) << (8 * k);
         }
         return;
     }
@@ -427,7 +440,7 @@ CP_DEV void box_box(const Box& A, const Box& B, real margin, real edge_bias, Con
     C.m = 1;
     C.p[0] = scl(add(qa, qb), real(0.5));
     C.d[0] = best;
-    C.id[0] = 6 * 32 + 3 * bi + bj;
+    C.ids = (uint32_t)(6 * 32 + 3 * bi + bj);
 }
 
 CP_DEV void plane_space(V3 n, V3& t1, V3& t2) {
@@ -491,6 +504,9 @@ CP_DEV int pk_cnt(uint32_t pk) { return (int)(pk & 7u); }
 CP_DEV int pk_base(uint32_t pk) { return (int)((pk >> 3) & 31u); }
 CP_DEV int pk_fcnt(uint32_t pk) { return (int)((pk >> 8) & 7u); }
 CP_DEV int pk_fbase(uint32_t pk) { return (int)((pk >> 11) & 15u); }
+// warm-start cache slots of the pair that may hold a nonzero impulse: max(new count, old
+// count); the slots past it hold 0 before and after the refresh (substep_finish)
+CP_DEV int pk_wcnt(uint32_t pk) { return (int)((pk >> 16) & 7u); }
 
 // ---- independent island solve: the island's two dynamic bodies in local slots
 // 1 (cart) and 2 (pole); slot 0 is the static ground.  Same arithmetic as the
@@ -1504,7 +1520,7 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
                     real K = row_k_dyn(a, ima, imb, xa, xb, Ma, Mb, rb, C.n);
                     real dist = C.d[k];
                     real tg = dist > real(0.0) ? -(dist * inv_dt) : -((P.erp * dist) * inv_dt);
-                    const int id = C.id[k];
+                    const int id = (int)((C.ids >> (8 * k)) & 0xFFu);
                     real l0 = real(0.0);
                     if ((int)(oid & 0xFFu) == id) l0 = ol0;
                     else if ((int)((oid >> 8) & 0xFFu) == id) l0 = ol1;
@@ -1538,24 +1554,27 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
         fused = fbase + fm;
         CP_STAMP(n3);
         CP_ACC(rows, n2, n3);
-        const uint32_t pk = (uint32_t)m | ((uint32_t)base << 3) | ((uint32_t)fm << 8) | ((uint32_t)fbase << 11);
+        // old point count = the leading non-0xFF bytes of the old id word (written as a prefix)
+        const int om = (oid & 0xFFu) == 0xFFu ? 0 : ((oid >> 8) & 0xFFu) == 0xFFu ? 1
+                     : ((oid >> 16) & 0xFFu) == 0xFFu ? 2 : ((oid >> 24) & 0xFFu) == 0xFFu ? 3 : 4;
+        const uint32_t pk = (uint32_t)m | ((uint32_t)base << 3) | ((uint32_t)fm << 8) | ((uint32_t)fbase << 11) |
+                            ((uint32_t)(m > om ? m : om) << 16);
 #ifdef CP_HDR_SCRATCH
         G.sx(4 * j + 0, C.n.x);
         G.sx(4 * j + 1, C.n.y);
         G.sx(4 * j + 2, C.n.z);
         G.sx(4 * j + 3, bits_to<real>(pk));
 #else
-        // the pair's manifold header into registers: j is wave-uniform, so this is a
-        // scalar switch, not a dynamically indexed register array
-        switch (j) {
-            case 0: T.n[0] = C.n; T.pk[0] = pk; break;
-            case 1: T.n[1] = C.n; T.pk[1] = pk; break;
-            case 2: T.n[2] = C.n; T.pk[2] = pk; break;
-            case 3: T.n[3] = C.n; T.pk[3] = pk; break;
-            default: T.n[4] = C.n; T.pk[4] = pk; break;
+        // the pair's manifold header into registers: a select per slot on the wave-uniform j
+        // (a switch is merged back into one indexed store, which keeps T in private memory)
+#pragma unroll
+        for (int q = 0; q < CP_ISLAND_PAIRS; ++q) {
+            const bool h = j == q;
+            T.n[q] = selv(h, C.n, T.n[q]);
+            T.pk[q] = h ? pk : T.pk[q];
         }
 #endif
-        if (live) G.sw(CP_SF_WS_ID(0, j), bits_to<real>(nid));
+        if (live && nid != oid) G.sw(CP_SF_WS_ID(0, j), bits_to<real>(nid));  // unchanged: no write
     };
 #ifdef CP_NO_GROUND_PEEL
 #pragma unroll 1
@@ -1652,14 +1671,17 @@ CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx
         S.b[3].v = selv(second, I.d2.v, v2);
         S.b[3].w = selv(second, I.d2.w, w2);
     }
-    // refresh the warm-start cache of the lane's island
+    // refresh the warm-start cache of the lane's island.  A slot past both the old and the new
+    // point count holds 0 and stays 0: it is not rewritten (the id word is a 0xFF-padded prefix,
+    // the impulses past it 0, in every state the kernels and cp_init write; oracle: every slot
+    // rewritten, same values)
     if (live) {
 #pragma unroll
         for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
-            const int cnt = pk_cnt(c.T.pk[j]), base = pk_base(c.T.pk[j]);
+            const int cnt = pk_cnt(c.T.pk[j]), base = pk_base(c.T.pk[j]), wc = pk_wcnt(c.T.pk[j]);
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                G.sl(CP_SF_WS_LAM(0, j, k), (k < cnt) ? pool_n(pool, F_LAM, base + k) : real(0.0));
+                if (k < wc) G.sl(CP_SF_WS_LAM(0, j, k), (k < cnt) ? pool_n(pool, F_LAM, base + k) : real(0.0));
         }
     }
     // 5. integrate positions and orientations (both lanes, whole env)
