@@ -50,9 +50,25 @@ CP_DEV void write_rposes(const Sim& S, float* dst) {
 }
 
 // per-wave stamp accumulation into b.stamps (lane 0 writes; CP_STAMPS builds only)
-CP_DEV void flush_stamps(const Stamps& ST, uint64_t* dst, uint64_t total) {
+// Slots 11-15: the longest wave (cycles), and from the 100 MHz constant clock (s_memrealtime):
+// the latest wave end, the complement of the earliest wave start, the sum and the max of the
+// per-wave durations (the launch's wave-duration spread and the shader clock, tools/stamps.py).
+CP_DEV void flush_stamps(const Stamps& ST, uint64_t* dst, uint64_t total, uint64_t rt0 = 0, uint64_t rt1 = 0,
+                         const uint64_t* stamps_base = nullptr) {
 #ifdef CP_STAMPS
     if ((threadIdx.x & (WAVE - 1)) == 0) {
+        atomicMax((unsigned long long*)&dst[11], (unsigned long long)total);
+        atomicMax((unsigned long long*)&dst[12], (unsigned long long)rt1);
+        atomicMax((unsigned long long*)&dst[13], (unsigned long long)~rt0);
+        atomicAdd((unsigned long long*)&dst[14], (unsigned long long)(rt1 - rt0));
+        atomicMax((unsigned long long*)&dst[15], (unsigned long long)(rt1 - rt0));
+        if (dst == stamps_base) {  // the step kernel: wave count and duration per slow-path set
+            // (slots 32-47) and a histogram of wave durations in 50 us bins (slots 48-63)
+            atomicAdd((unsigned long long*)&dst[32 + 2 * ST.flags], 1ull);
+            atomicAdd((unsigned long long*)&dst[33 + 2 * ST.flags], (unsigned long long)(rt1 - rt0));
+            const uint64_t bin = (rt1 - rt0) / 5000u;
+            atomicAdd((unsigned long long*)&dst[48 + (bin < 15u ? bin : 15u)], 1ull);
+        }
         atomicAdd((unsigned long long*)&dst[0], (unsigned long long)ST.narrow);
         atomicAdd((unsigned long long*)&dst[1], (unsigned long long)ST.vel);
         atomicAdd((unsigned long long*)&dst[2], (unsigned long long)ST.solve);
@@ -68,7 +84,7 @@ CP_DEV void flush_stamps(const Stamps& ST, uint64_t* dst, uint64_t total) {
         }
     }
 #else
-    (void)ST; (void)dst; (void)total;
+    (void)ST; (void)dst; (void)total; (void)rt0; (void)rt1; (void)stamps_base;
 #endif
 }
 
@@ -261,6 +277,7 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     const Lane L = Lane::make(isl, cfg.phys);
     Stamps ST;
     CP_STAMP(k0);
+    CP_RT(r0);
     Sim S;
     load_sim(S, G.st, G.off);  // pending forces survive the reset (pybullet keeps them)
     const int episode = ldi(G.st, CP_SF_EPISODE, G.off);
@@ -293,7 +310,8 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     ov += (int)partner_u((uint32_t)ov);
 #ifdef CP_STAMPS
     CP_STAMP(k1);
-    flush_stamps(ST, b.stamps + 16, k1 - k0);  // the reset kernel's counters: slots 16-26
+    CP_RT(r1);
+    flush_stamps(ST, b.stamps + 16, k1 - k0, r0, r1);  // the reset kernel's counters: slots 16-26
 #endif
     if (!lead) return;
     store_sim(S, G.st, G.off);
@@ -333,6 +351,7 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
     bool render_me = false;  // simulated this step: its frames go to the render kernel
     Stamps ST;
     CP_STAMP(k0);
+    CP_RT(r0);
     if (inb) {
         const Mem G = Mem::make(b.state, b.scratch, B, i, isl);
         const Lane L = Lane::make(isl, cfg.phys);
@@ -429,7 +448,8 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
     }
 #ifdef CP_STAMPS
     CP_STAMP(k1);
-    flush_stamps(ST, b.stamps, k1 - k0);
+    CP_RT(r1);
+    flush_stamps(ST, b.stamps, k1 - k0, r0, r1, b.stamps);
 #endif
     if (cfg.autoreset) {
         // wave ballot compaction of the finishing envs into the reset list

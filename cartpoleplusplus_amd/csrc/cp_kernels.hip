@@ -314,7 +314,7 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     CP_ALLOC(h->b.list, B * sizeof(int32_t));
     CP_ALLOC(h->count2, 2 * sizeof(int32_t));
     CP_ALLOC(h->b.scratch, (size_t)4 * CP_ISLAND_PAIRS * 2 * B * rb);
-    CP_ALLOC(h->b.stamps, 32 * sizeof(uint64_t));
+    CP_ALLOC(h->b.stamps, CP_STAMP_SLOTS * sizeof(uint64_t));
     CP_ALLOC(h->b.stepped, B * sizeof(uint8_t));
 #undef CP_ALLOC
     e = hipMemset(h->count2, 0, 2 * sizeof(int32_t));
@@ -323,7 +323,7 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     h->b.count_next = nullptr;
     e = hipMemset(h->b.stepped, 0, B * sizeof(uint8_t));
     if (e != hipSuccess) return fail_free(e, "hipMemset");
-    e = hipMemset(h->b.stamps, 0, 32 * sizeof(uint64_t));
+    e = hipMemset(h->b.stamps, 0, CP_STAMP_SLOTS * sizeof(uint64_t));
     if (e != hipSuccess) return fail_free(e, "hipMemset");
     e = hipMemset(h->b.term_obs, 0, (size_t)R * 14 * B * sizeof(float));
     if (e != hipSuccess) return fail_free(e, "hipMemset");
@@ -525,12 +525,12 @@ int cp_overflow_counts(cp_handle* h, int32_t* out, void* stream) {
     return 0;
 }
 
-int cp_debug_stamps(cp_handle* h, uint64_t* out32, int reset) {
-    if (!h || !out32) return fail(h, "cp_debug_stamps: null argument");
+int cp_debug_stamps(cp_handle* h, uint64_t* out64, int reset) {
+    if (!h || !out64) return fail(h, "cp_debug_stamps: null argument");
     CP_TRY(h, hipSetDevice(h->device));
     CP_TRY(h, hipDeviceSynchronize());
-    CP_TRY(h, hipMemcpy(out32, h->b.stamps, 32 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-    if (reset) CP_TRY(h, hipMemset(h->b.stamps, 0, 32 * sizeof(uint64_t)));
+    CP_TRY(h, hipMemcpy(out64, h->b.stamps, CP_STAMP_SLOTS * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    if (reset) CP_TRY(h, hipMemset(h->b.stamps, 0, CP_STAMP_SLOTS * sizeof(uint64_t)));
 #ifdef CP_STAMPS
     return 1;
 #else

@@ -25,12 +25,15 @@ namespace CP_NS {
 struct Stamps {
     uint64_t narrow = 0, vel = 0, solve = 0, integ = 0, sweeps = 0, substeps = 0;
     uint64_t sel = 0, bb = 0, rows = 0;  // narrowphase split: box/inertia selection, box_box, row setup
+    uint32_t flags = 0;  // slow paths the wave took: 1 merged solve, 2 / 4 ground-cart / ground-pole rows not +z
 };
 #ifdef CP_STAMPS
 #define CP_STAMP(var) uint64_t var = __builtin_amdgcn_s_memtime()
+#define CP_RT(var) uint64_t var = __builtin_amdgcn_s_memrealtime()
 #define CP_ACC(field, a, b) (ST.field += (b) - (a))
 #else
 #define CP_STAMP(var)
+#define CP_RT(var) constexpr uint64_t var = 0
 #define CP_ACC(field, a, b)
 #endif
 
@@ -859,42 +862,55 @@ CP_DEV void pair_friction_rows(Sim& S, const Step& T, bool second, const cp_phys
     }
 }
 
-// ---- uniform-index accessors for the narrowphase pair loop (g may vary by lane) ----
+// ---- body selection of the narrowphase pair loop.  The local pair j is wave-uniform and its
+// bodies differ between the two islands only: with j dispatched through a uniform branch
+// (pair_bodies), every selection is a 2-way select on the lane's island, one v_cndmask_b32 per
+// value.  (A 5-way choice over the lane-varying body id compiles to an exec-mask branch tree:
+// lone-wave narrowphase ~40k cycles per substep against ~30k for four opaque selects.)
+__host__ __device__ constexpr int island_pair_c(int isl, int j) {
+    return (int)(((isl ? 0x87932u : 0x65410u) >> (4 * j)) & 15u);
+}
+// Box of dynamic body G0 (island 0 lanes) or G1 (island 1 lanes), from the pose in S: the
+// axes are rebuilt from the quaternion here rather than kept live through the narrowphase
+// (same arithmetic as the per-body quat_axes / world_inv_inertia).
+template <int G0, int G1>
+CP_DEV Box box_pick(bool second, const Sim& S, const cp_physics& P) {
+    static_assert(G0 >= 1 && G1 >= 1, "dynamic bodies only");
+    const Body& B0 = S.b[G0 - 1];
+    const Body& B1 = S.b[G1 - 1];
+    Box b;
+    b.h0 = second ? real(P.half_extents[G1][0]) : real(P.half_extents[G0][0]);
+    b.h1 = second ? real(P.half_extents[G1][1]) : real(P.half_extents[G0][1]);
+    b.h2 = second ? real(P.half_extents[G1][2]) : real(P.half_extents[G0][2]);
+    b.c = selv(second, B1.x, B0.x);
+    b.ax = quat_axes(second ? B1.q[0] : B0.q[0], second ? B1.q[1] : B0.q[1], second ? B1.q[2] : B0.q[2],
+                     second ? B1.q[3] : B0.q[3]);
+    return b;
+}
+template <int G0, int G1>
+CP_DEV real pick_f(bool second, const float* v) { return second ? real(v[G1]) : real(v[G0]); }
+template <int G0, int G1>
+CP_DEV Sym inertia_pick(bool second, const Box& b, const cp_physics& P) {
+    return world_inv_inertia(b.ax, second ? real(P.inv_inertia[G1][0]) : real(P.inv_inertia[G0][0]),
+                             second ? real(P.inv_inertia[G1][1]) : real(P.inv_inertia[G0][1]),
+                             second ? real(P.inv_inertia[G1][2]) : real(P.inv_inertia[G0][2]));
+}
+// f(std::integral_constant<int, J>) for the wave-uniform local pair j (GROUND: j is 0 or 1)
+template <bool GROUND, typename F>
+CP_DEV void pair_dispatch(int j, F&& f) {
+    if constexpr (GROUND) {
+        if (j == 0) f(std::integral_constant<int, 0>{});
+        else f(std::integral_constant<int, 1>{});
+    } else {
+        if (j == 2) f(std::integral_constant<int, 2>{});
+        else if (j == 3) f(std::integral_constant<int, 3>{});
+        else f(std::integral_constant<int, 4>{});
+    }
+}
 CP_DEV V3 sel5v(int g, V3 z, V3 a, V3 b, V3 c, V3 d) {
     return mk(g == 1 ? a.x : g == 2 ? b.x : g == 3 ? c.x : g == 4 ? d.x : z.x,
               g == 1 ? a.y : g == 2 ? b.y : g == 3 ? c.y : g == 4 ? d.y : z.y,
               g == 1 ? a.z : g == 2 ? b.z : g == 3 ? c.z : g == 4 ? d.z : z.z);
-}
-CP_DEV real sel5(int g, real z, real a, real b, real c, real d) {
-    return g == 1 ? a : g == 2 ? b : g == 3 ? c : g == 4 ? d : z;
-}
-CP_DEV real sel5p(int g, const float* v) { return sel5(g, real(v[0]), real(v[1]), real(v[2]), real(v[3]), real(v[4])); }
-// Box of body g (lane-varying) with its world inverse inertia, from the pose in S:
-// the axes are rebuilt from the quaternion here rather than kept live through the
-// narrowphase (same arithmetic as the per-body quat_axes / world_inv_inertia).
-CP_DEV Box box_sel(int g, const Sim& S, const cp_physics& P) {
-    Box b;
-    b.h0 = sel5(g, P.half_extents[0][0], P.half_extents[1][0], P.half_extents[2][0], P.half_extents[3][0],
-                P.half_extents[4][0]);
-    b.h1 = sel5(g, P.half_extents[0][1], P.half_extents[1][1], P.half_extents[2][1], P.half_extents[3][1],
-                P.half_extents[4][1]);
-    b.h2 = sel5(g, P.half_extents[0][2], P.half_extents[1][2], P.half_extents[2][2], P.half_extents[3][2],
-                P.half_extents[4][2]);
-    b.c = sel5v(g, mk(real(0.0), real(0.0), real(0.0)), S.b[0].x, S.b[1].x, S.b[2].x, S.b[3].x);
-    const real qx = sel5(g, real(0.0), S.b[0].q[0], S.b[1].q[0], S.b[2].q[0], S.b[3].q[0]);
-    const real qy = sel5(g, real(0.0), S.b[0].q[1], S.b[1].q[1], S.b[2].q[1], S.b[3].q[1]);
-    const real qz = sel5(g, real(0.0), S.b[0].q[2], S.b[1].q[2], S.b[2].q[2], S.b[3].q[2]);
-    const real qw = sel5(g, real(1.0), S.b[0].q[3], S.b[1].q[3], S.b[2].q[3], S.b[3].q[3]);
-    b.ax = quat_axes(qx, qy, qz, qw);  // identity, exactly, for the ground
-    return b;
-}
-CP_DEV Sym inertia_sel(int g, const Box& b, const cp_physics& P) {
-    return world_inv_inertia(b.ax, sel5(g, P.inv_inertia[0][0], P.inv_inertia[1][0], P.inv_inertia[2][0],
-                                        P.inv_inertia[3][0], P.inv_inertia[4][0]),
-                             sel5(g, P.inv_inertia[0][1], P.inv_inertia[1][1], P.inv_inertia[2][1],
-                                  P.inv_inertia[3][1], P.inv_inertia[4][1]),
-                             sel5(g, P.inv_inertia[0][2], P.inv_inertia[1][2], P.inv_inertia[2][2],
-                                  P.inv_inertia[3][2], P.inv_inertia[4][2]));
 }
 
 // Broadphase: true when a face axis of A already separates the pair by more than
@@ -1013,6 +1029,9 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0,
 #else
     const bool ez0 = __ballot(pk_cnt(c.T.pk[0]) > 0 && !is_plus_z(c.T.n[0])) == 0ull;
     const bool ez1 = __ballot(pk_cnt(c.T.pk[1]) > 0 && !is_plus_z(c.T.n[1])) == 0ull;
+#endif
+#ifdef CP_STAMPS
+    ST.flags |= (ez0 ? 0u : 2u) | (ez1 ? 0u : 4u);
 #endif
     for (int it = it0; it < it1; ++it) {
         if (__ballot(c.active) == 0ull) break;
@@ -1470,27 +1489,39 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
     //    local pairs (the global pair, hence the bodies, differ between the two lanes)
     int used = 0, fused = 0;
     // one local pair; GROUND: j is 0 or 1, whose first body is the static ground on both
-    // islands, so its box is compile-time (centre 0, identity axes: box_sel's exact values)
+    // islands, so its box is compile-time (centre 0, identity axes)
     auto pair_body = [&](auto ground_tag, const int j) {
         constexpr bool GROUND = decltype(ground_tag)::value;
         const int g = island_pair(L.isl, j);
-        const int a = GROUND ? 0 : pair_a(g), b = pair_b(g);
+        const int a = GROUND ? 0 : pair_a(g);
         CP_STAMP(n0);
         // warm-start cache of the pair, loaded first: its latency overlaps the narrowphase
         const uint32_t oid = to_bits(G.lw(CP_SF_WS_ID(0, j)));
         const real ol0 = G.ll(CP_SF_WS_LAM(0, j, 0)), ol1 = G.ll(CP_SF_WS_LAM(0, j, 1));
         const real ol2 = G.ll(CP_SF_WS_LAM(0, j, 2)), ol3 = G.ll(CP_SF_WS_LAM(0, j, 3));
-        Box A;
-        if constexpr (GROUND) {
-            A.c = mk(real(0.0), real(0.0), real(0.0));
-            A.ax = quat_axes(real(0.0), real(0.0), real(0.0), real(1.0));
-            A.h0 = P.half_extents[0][0];
-            A.h1 = P.half_extents[0][1];
-            A.h2 = P.half_extents[0][2];
-        } else {
-            A = box_sel(a, S, P);
-        }
-        const Box Bx = box_sel(b, S, P);
+        // the island flag through a volatile empty asm per pair: the box selections below are
+        // otherwise loop-invariant per branch, and hoisting all of them out of the pair loop
+        // keeps every body's axes live across the narrowphase (spills)
+        uint32_t sec = (uint32_t)L.isl;
+        asm volatile("" : "+v"(sec));
+        const bool second = sec != 0u;
+        Box A, Bx;
+        pair_dispatch<GROUND>(j, [&](auto jt) {
+            constexpr int J = decltype(jt)::value;
+            constexpr int a0 = pair_a(island_pair_c(0, J)), a1 = pair_a(island_pair_c(1, J));
+            constexpr int b0 = pair_b(island_pair_c(0, J)), b1 = pair_b(island_pair_c(1, J));
+            if constexpr (a0 == 0) {  // the static ground: centre 0, identity axes (exact)
+                static_assert(a1 == 0, "ground pairs are ground pairs on both islands");
+                A.c = mk(real(0.0), real(0.0), real(0.0));
+                A.ax = quat_axes(real(0.0), real(0.0), real(0.0), real(1.0));
+                A.h0 = P.half_extents[0][0];
+                A.h1 = P.half_extents[0][1];
+                A.h2 = P.half_extents[0][2];
+            } else {
+                A = box_pick<a0, a1>(second, S, P);
+            }
+            Bx = box_pick<b0, b1>(second, S, P);
+        });
         Contact C;
         C.m = 0;
         C.n = mk(real(0.0), real(0.0), real(1.0));
@@ -1503,10 +1534,19 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
         int m = 0, fm = 0;
         uint32_t nid = 0xFFFFFFFFu;
         if (__ballot(C.m > 0) != 0ull) {  // row setup, skipped when no lane of the wave has a contact
-        const real mu = sel5p(a, P.friction) * sel5p(b, P.friction);
-        const real ima = sel5p(a, P.inv_mass), imb = sel5p(b, P.inv_mass);
+        real mu, ima, imb;
+        Sym Ma, Mb;
+        pair_dispatch<GROUND>(j, [&](auto jt) {
+            constexpr int J = decltype(jt)::value;
+            constexpr int a0 = pair_a(island_pair_c(0, J)), a1 = pair_a(island_pair_c(1, J));
+            constexpr int b0 = pair_b(island_pair_c(0, J)), b1 = pair_b(island_pair_c(1, J));
+            mu = pick_f<a0, a1>(second, P.friction) * pick_f<b0, b1>(second, P.friction);
+            ima = pick_f<a0, a1>(second, P.inv_mass);
+            imb = pick_f<b0, b1>(second, P.inv_mass);
+            Ma = inertia_pick<a0, a1>(second, A, P);
+            Mb = inertia_pick<b0, b1>(second, Bx, P);
+        });
         const V3 xa = A.c, xb = Bx.c;
-        const Sym Ma = inertia_sel(a, A, P), Mb = inertia_sel(b, Bx, P);
         V3 t1 = mk(real(0.0), real(0.0), real(0.0)), t2 = t1;
         if (mu > real(0.0)) plane_space(C.n, t1, t2);
 #pragma unroll
@@ -1627,6 +1667,9 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
     const uint32_t own_cross = (pk_cnt(T.pk[3]) + pk_cnt(T.pk[4])) > 0 ? 1u : 0u;
     const uint32_t any_cross = own_cross | partner_u(own_cross);
     c.merged = any_cross != 0u;
+#ifdef CP_STAMPS
+    ST.flags |= __ballot(c.merged) != 0ull ? 1u : 0u;
+#endif
     c.used = used;
     c.tot = used + (int)partner_u((uint32_t)used);
     const bool second = L.isl != 0;
@@ -1671,17 +1714,19 @@ CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx
         S.b[3].v = selv(second, I.d2.v, v2);
         S.b[3].w = selv(second, I.d2.w, w2);
     }
-    // refresh the warm-start cache of the lane's island.  A slot past both the old and the new
-    // point count holds 0 and stays 0: it is not rewritten (the id word is a 0xFF-padded prefix,
+    // refresh the warm-start cache of the lane's island.  A pair with no point before or after
+    // the substep holds 0 impulses and keeps them: it is not rewritten (the id word is a 0xFF-padded prefix,
     // the impulses past it 0, in every state the kernels and cp_init write; oracle: every slot
     // rewritten, same values)
     if (live) {
 #pragma unroll
         for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
-            const int cnt = pk_cnt(c.T.pk[j]), base = pk_base(c.T.pk[j]), wc = pk_wcnt(c.T.pk[j]);
+            const int cnt = pk_cnt(c.T.pk[j]), base = pk_base(c.T.pk[j]);
+            if (pk_wcnt(c.T.pk[j]) > 0) {  // one branch per pair: rewriting a zero slot with 0 is harmless
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (k < wc) G.sl(CP_SF_WS_LAM(0, j, k), (k < cnt) ? pool_n(pool, F_LAM, base + k) : real(0.0));
+                for (int k = 0; k < 4; ++k)
+                    G.sl(CP_SF_WS_LAM(0, j, k), (k < cnt) ? pool_n(pool, F_LAM, base + k) : real(0.0));
+            }
         }
     }
     // 5. integrate positions and orientations (both lanes, whole env)

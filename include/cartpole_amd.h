@@ -233,13 +233,19 @@ int cp_timing_end(cp_handle* h, double* step_ms, int32_t* step_launches, double*
  * returned by cp_timing_end are the sampled ones. */
 int cp_timing_stride(cp_handle* h, int step_stride, int reset_stride);
 
-/* Diagnostics of a stamp build (-DCP_STAMPS): host array of 32 counters summed over
- * waves since the last reset: slots 0-7 for the step kernel, 16-23 for the reset kernel,
- * each: s_memtime cycles in narrowphase + row setup, velocity update + warm start, PGS
+/* Diagnostics of a stamp build (-DCP_STAMPS): host array of CP_STAMP_SLOTS (64) counters
+ * summed over waves since the last reset: slots 0-7 for the step kernel, 16-23 for the reset
+ * kernel, each: s_memtime cycles in narrowphase + row setup, velocity update + warm start, PGS
  * sweeps, integration + cache; sweep count, substep count, total kernel cycles, waves;
- * slots 8-10 / 24-26 split the narrowphase (body selection, box_box, row setup).
+ * slots 8-10 / 24-26 split the narrowphase (body selection, box_box, row setup); slots
+ * 11-15 / 27-31 the longest wave (cycles) and, in 10 ns ticks of s_memrealtime, the latest
+ * wave end, the complement of the earliest wave start, the sum and the max of the wave
+ * durations; slots 32-47 (step kernel) wave count and summed duration per set of slow paths
+ * taken (bit 0 merged solve, bit 1 / 2 ground-cart / ground-pole rows not +z), slots 48-63 a
+ * histogram of step-kernel wave durations in 50 us bins (the last open-ended).
  * Synchronises the device.  Returns 1 in a stamp build, 0 otherwise (counters then stay 0). */
-int cp_debug_stamps(cp_handle* h, uint64_t* out32, int reset);
+#define CP_STAMP_SLOTS 64
+int cp_debug_stamps(cp_handle* h, uint64_t* out64, int reset);
 
 /* ---- Raster observation (--use-raw-pixels) ----------
  * Replaces render_rgb + set_state_element_for_repeat (bullet_cartpole.py:277-306):

@@ -25,7 +25,7 @@ acts = torch.randint(0, 5, (steps + 20, B, 2), dtype=torch.int8, device="cuda", 
 env.reset()
 for t in range(20):
     env.step(acts[t])
-out = (C.c_uint64 * 32)()
+out = (C.c_uint64 * 64)()
 rc = env.lib.cp_debug_stamps(env.h, out, 1)
 assert rc == 1, "not a stamp build (set CP_LIB_PATH to libcartpole_hip_stamps.so)"
 for t in range(steps):
@@ -45,4 +45,19 @@ for name, base in (("step_kernel", 0), ("reset_kernel", 16)):
                  "sweeps_per_wave_substep": sweeps / max(1, substeps),
                  "cycles_per_sweep": solve / max(1, sweeps),
                  "kernel_cycles_per_wave": total / max(1, waves)}
+    wmax, rt_end, rt_start_c, rt_sum, rt_max = list(out)[base + 11:base + 16]
+    if waves and rt_sum:
+        # s_memrealtime is a 100 MHz clock; the spans below are summed over every launch of the run
+        mean_rt = rt_sum / waves
+        res[name]["wave_duration"] = {"longest_wave_cycles": wmax, "mean_wave_us": mean_rt / 100.0,
+                                      "longest_wave_us": rt_max / 100.0,
+                                      "shader_clock_ghz": (total / waves) / mean_rt / 10.0,
+                                      "first_start_to_last_end_us_all_launches":
+                                          (rt_end - ((~rt_start_c) & (2 ** 64 - 1))) / 100.0}
+o = list(out)
+res["step_kernel"]["waves_by_slow_paths"] = {
+    ("+".join(n for bit, n in ((1, "merged"), (2, "ground_cart_not_z"), (4, "ground_pole_not_z")) if f & bit) or "none"):
+        {"waves": o[32 + 2 * f], "mean_us": o[33 + 2 * f] / max(1, o[32 + 2 * f]) / 100.0}
+    for f in range(8) if o[32 + 2 * f]}
+res["step_kernel"]["wave_duration_hist_50us"] = o[48:64]
 print(json.dumps(res, indent=1))
