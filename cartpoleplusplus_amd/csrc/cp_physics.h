@@ -1453,7 +1453,13 @@ CP_DEV void solve_range(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* p
 
 // the lane's island view: its two bodies (cart, pole or cart2, pole2) with their world
 // inverse inertias, and the island's friction products
-CP_DEV void island_view(const Sim& S, const Lane& L, Ctx& c) {
+CP_DEV void island_view(const Sim& S, const cp_physics& P, int isl_, Ctx& c) {
+    // the island's constants are rebuilt here from the kernel arguments (a few selects) through
+    // an opaque island flag: built once per kernel they stay live across the narrowphase and
+    // are spilled there (scratch traffic every substep)
+    uint32_t isl = (uint32_t)isl_;
+    asm volatile("" : "+v"(isl));
+    const Lane L = Lane::make((int)isl, P);
     const bool second = L.isl != 0;
     Isl& I = c.I;
     I.d1.x = selv(second, S.b[2].x, S.b[0].x);
@@ -1673,7 +1679,7 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
     c.used = used;
     c.tot = used + (int)partner_u((uint32_t)used);
     const bool second = L.isl != 0;
-    island_view(S, L, c);
+    island_view(S, P, L.isl, c);
     Isl& I = c.I;
     CP_STAMP(t2);
     CP_ACC(vel, t1, t2);
