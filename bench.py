@@ -28,9 +28,11 @@ roofline: the step kernel's algorithmic HBM bytes per launch ove
 average duration from HIP events recorded on its launch stream in the timed region
 (every 4th launch sampled: the events themselves cost wall time).
 cpu_baseline (rank 0, N = 1): the oracle (a port: same algorithm, gcc -O3 -march=native,
-the kernel's results) on bounded samples: C3 on all cores (OpenMP), C3 on one core, C1.
+the kernel's results) on bounded samples: C3 on every CPU of the process's affinity mask
+(OpenMP; `value`), on 16 threads and on one core, and C1.
 parity (rank 0, N = 1): SURVEY.md §8d's matrix, GPU vs the oracle's fp32 build (bit-exact
-bar) and fp64 build (drift), with and without the PGS early exit.
+bar) and fp64 build (drift), with and without the PGS early exit; every GPU handle of the
+parity leg runs the kernel shapes the timed region ran (cp_set_kernel_shape).
 """
 import argparse
 import json
@@ -157,13 +159,6 @@ def pmc_valu(kernel, batch, repeats, kind):
     return None, None
 
 
-def step_shape(B):
-    """The step-kernel shape cp_create picks (cp_kernels.hip choose_reset_shape)."""
-    e = os.environ.get("CP_STEP_LATENCY")
-    lat = (e == "1") if e in ("0", "1") else B <= 32768
-    return "latency" if lat else "throughput"
-
-
 # ------------------------------------------------------------------- workload
 def workload(args, world):
     B, R = args.batch, args.repeats
@@ -186,6 +181,8 @@ def workload(args, world):
         s += ", bounds termination on (bullet_cartpole.py:243-253)"
     if args.solver_iterations is not None:
         s += f", solver_iterations={args.solver_iterations} (diagnostic)"
+    if getattr(args, "rollout", 0):
+        s += f", cp_rollout launches of up to {args.rollout} steps (not the per-step cp_step headline)"
     if idx is not None:
         s += f" (BASELINE.json configs[{idx}])"
     return name, s
@@ -199,16 +196,25 @@ def episodes(env):
     return st.view(torch.int32).to(torch.int64)
 
 
-def timed(env, actions, t0, K, world, dev, gather_at_end):
-    """K steps between barrier + synchronize; -> (max-over-ranks seconds, histogram, gathers)."""
+def timed(env, actions, t0, K, world, dev, gather_at_end, rollout=0):
+    """K steps between barrier + synchronize; -> (max-over-ranks seconds, histogram, gathers).
+    rollout > 0: the steps run as cp_rollout launches of up to `rollout` steps, split at the
+    200-step window boundaries (where the return gather runs)."""
     hist, gathers = None, 0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     start = time.perf_counter()
-    for t in range(K):
-        env.step(actions[t0 + t])
-        if (t0 + t + 1) % WINDOW == 0:
+    t = 0
+    while t < K:
+        if rollout:
+            n = min(rollout, K - t, WINDOW - (t0 + t) % WINDOW)
+            env.rollout(actions[t0 + t:t0 + t + n])
+        else:
+            n = 1
+            env.step(actions[t0 + t])
+        t += n
+        if (t0 + t) % WINDOW == 0:
             r, _ = env.episode_returns()
             hist = return_histogram(gather_returns(r), WINDOW)   # RCCL all-gather when world > 1
             gathers += 1
@@ -232,7 +238,7 @@ def cpu_baseline(R, budget_s):
     import numpy as np
 
     from oracle import oracle as O
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    all_cpus = len(os.sched_getaffinity(0))
     lib = O.load("native")
 
     def run(B, steps, threads_, R_, seed):
@@ -272,7 +278,8 @@ def cpu_baseline(R, budget_s):
         return {"value": round(max(B, 64) * steps / dt, 1), "cores": used,
                 "sample": f"{max(B, 64)} envs x {steps} steps ({dt:.1f} s)"}
 
-    omp = sized(threads, budget_s)
+    omp = sized(all_cpus, budget_s)
+    t16 = sized(min(16, all_cpus), budget_s / 2)
     one = sized(1, budget_s / 2)
     # C1: B = 1, R = 2 (reference default), discrete random actions, seeds 0..9, autoreset
     c1_steps, c1_t = 0, 0.0
@@ -285,7 +292,10 @@ def cpu_baseline(R, budget_s):
     return {"value": omp["value"], "unit": "env-steps/s", "cores": omp["cores"], "kind": "port",
             "sample": (f"oracle/cp_oracle.c fp32 built gcc -O3 -march=native (same algorithm; bit-identical "
                        f"to the parity build: {same}), C3 workload (R={R}, discrete random actions, autoreset "
-                       f"incl.), OpenMP on {omp['cores']} threads: {omp['sample']}"),
+                       f"incl.), OpenMP on {omp['cores']} threads (every CPU of the affinity mask): "
+                       f"{omp['sample']}"),
+            "threads_16": {"value": t16["value"], "unit": "env-steps/s", "cores": t16["cores"],
+                           "sample": "C3 workload, " + t16["sample"]},
             "single_thread": {"value": one["value"], "unit": "env-steps/s", "cores": 1,
                               "sample": "C3 workload, " + one["sample"]},
             "c1_single_thread": {"value": round(c1_steps / c1_t, 1), "unit": "env-steps/s", "cores": 1,
@@ -302,7 +312,11 @@ def _pose_diffs(g, o):
     return float(d[..., 0:3].max()), float(d[..., 3:7].max())
 
 
-def parity_case(device, R, B, F, stream, steps, thr=None, seed=0, precision="f32"):
+def _oracle_threads():
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def parity_case(device, R, B, F, stream, steps, thr=None, seed=0, precision="f32", shape=None):
     """One SURVEY §8d parity run: B envs from reset (seed, F_init = F), 200 steps of one
     continuous action stream, GPU vs oracle; per step the max |dpos| and |dquat|.
     precision "f32": the fp32 kernels vs the oracle's f32 and f64 builds; "f64": the fp64
@@ -310,7 +324,7 @@ def parity_case(device, R, B, F, stream, steps, thr=None, seed=0, precision="f32
     import numpy as np
 
     from oracle import oracle as O
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    threads = _oracle_threads()
     over = {} if thr is None else {"residual_threshold": thr}
     cfg = O.default_config(num_envs=B, action_repeats=R, initial_force=float(F), seed=seed, autoreset=0)
     for k, v in over.items():
@@ -318,6 +332,8 @@ def parity_case(device, R, B, F, stream, steps, thr=None, seed=0, precision="f32
     if precision == "f64":
         cfg.precision = abi.CP_PRECISION_F64
     gpu = BatchedCartpole(B, device.index, config=abi.cp_config.from_buffer_copy(cfg))
+    if shape is not None and precision == "f32":
+        gpu.set_kernel_shape(*shape)
     orc = {p: O.Envs(abi.cp_config.from_buffer_copy(cfg), precision=p)
            for p in (("f32", "f64") if precision == "f32" else ("f64",))}
     g = gpu.reset().cpu().numpy()
@@ -350,17 +366,21 @@ def parity_case(device, R, B, F, stream, steps, thr=None, seed=0, precision="f32
     return out
 
 
-def parity_c3(device, R, B=512, steps=WINDOW):
-    """The bench workload itself (C3: random discrete actions, autoreset, seed 1234): GPU vs
-    the fp32 oracle over 200 steps (the bit-exact bar)."""
+def parity_c3(device, R, shape, B=2048, steps=WINDOW + 20):
+    """The bench workload itself (C3: bench.py's hashed discrete actions, autoreset, seed 1234)
+    on the kernel shapes the timed region ran: GPU vs the fp32 oracle over 220 steps (one
+    autoreset burst inside), the bit-exact bar."""
     import numpy as np
 
     from oracle import oracle as O
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    threads = _oracle_threads()
     cfg = O.default_config(num_envs=B, action_repeats=R, initial_force=55.0, seed=SEED, autoreset=1)
     gpu = BatchedCartpole(B, device.index, config=abi.cp_config.from_buffer_copy(cfg))
+    gpu.set_kernel_shape(*shape)
+    ran = gpu.kernel_shape()
     orc = O.Envs(abi.cp_config.from_buffer_copy(cfg))
-    d = np.abs(gpu.reset().cpu().numpy() - orc.reset()).max()
+    g, o = gpu.reset().cpu().numpy(), orc.reset()
+    d, nbits = float(np.abs(g - o).max()), int(np.count_nonzero(g.view(np.uint32) != o.view(np.uint32)))
     acts = make_actions(False, B, 0, steps, SEED, device)
     rew = np.zeros(B, np.float32)
     done = np.zeros(B, np.uint8)
@@ -368,12 +388,14 @@ def parity_c3(device, R, B=512, steps=WINDOW):
         g = gpu.step(acts[t])[0].cpu().numpy()
         o = np.zeros((B, R, 2, 7), np.float32)
         orc.step_omp(np.ascontiguousarray(acts[t].cpu().numpy()), abi.CP_ACTION_DISCRETE, o, rew, done, threads)
-        d = max(d, np.abs(g - o).max())
+        d = max(d, float(np.abs(g - o).max()))
+        nbits += int(np.count_nonzero(g.view(np.uint32) != o.view(np.uint32)))   # also catches -0.0 vs +0.0
     gpu.close()
-    return {"envs": B, "steps": steps, "max_abs_pose_diff": float(d), "bit_exact": bool(d == 0.0)}
+    return {"envs": B, "steps": steps, "kernel_shape": {"step": ran[0], "reset": ran[1]},
+            "max_abs_pose_diff": d, "elements_with_different_bits": nbits, "bit_exact": nbits == 0}
 
 
-def parity_check(device, R, B=128, steps=WINDOW):
+def parity_check(device, R, shape, B=128, steps=WINDOW):
     """SURVEY.md §8d's parity matrix: seed 0, F_init in {0, 55} x action streams {zero,
     constant (0.5, -0.25), random U[-1,1]}, 200 steps from reset, |dpos| and |dquat|
     separately, against the oracle's fp32 build (the kernel's bar: 0) and its fp64 build
@@ -386,7 +408,7 @@ def parity_check(device, R, B=128, steps=WINDOW):
         for F in (0, 55):
             for stream in ("zero", "constant", "random"):
                 log(f"  parity {variant} F={F} {stream}")
-                matrix[f"{variant}/F{F}/{stream}"] = parity_case(device, R, B, F, stream, steps, thr)
+                matrix[f"{variant}/F{F}/{stream}"] = parity_case(device, R, B, F, stream, steps, thr, shape=shape)
     worst32 = max(max(v["f32"]["max_dpos"], v["f32"]["max_dquat"]) for v in matrix.values())
     # the fp64 kernel variant (cp_config.precision = F64) on the early-exit cases: the GPU
     # computing the double-precision algorithm, against the oracle's fp64 build
@@ -398,9 +420,10 @@ def parity_check(device, R, B=128, steps=WINDOW):
             f64[f"early_exit/F{F}/{stream}"] = {"max_dpos": r["max_dpos"], "max_dquat": r["max_dquat"]}
     worst64 = max(max(v["max_dpos"], v["max_dquat"]) for v in f64.values())
     return {"envs_per_case": B, "steps": steps, "repeats": R, "actions": "continuous (B,2,2)",
+            "kernel_shape": {"step": shape[0], "reset": shape[1]},
             "bit_exact_vs_oracle_f32": worst32 == 0.0, "max_abs_diff_vs_oracle_f32": worst32,
             "fp64_kernel_vs_oracle_f64": {"bit_exact": worst64 == 0.0, "max_abs_diff": worst64, "cases": f64},
-            "c3_workload_vs_oracle_f32": parity_c3(device, R),
+            "c3_workload_vs_oracle_f32": parity_c3(device, R, shape),
             "matrix": matrix, "vs_pybullet": None,
             "note": "pybullet is not installed (parity with it unpinned, SURVEY.md §8c); f64 = the oracle's "
                     "algorithm in double precision, state kept in double (DESIGN.md §7)"}
@@ -427,6 +450,9 @@ def main():
     ap.add_argument("--done-on-bounds", action="store_true",
                     help="the reference's commented-out bounds termination (bullet_cartpole.py:243-253): "
                          "episodes end early, so the C4 return histogram is not degenerate (diagnostic config)")
+    ap.add_argument("--rollout", type=int, default=0, metavar="K",
+                    help="run the steps as cp_rollout launches of up to K steps (one launch advances every env "
+                         "through K steps; a separately labelled line, not the per-step headline)")
     ap.add_argument("--solver-iterations", type=int, default=None,
                     help="override the PGS sweep cap (default: the model's 50; non-default runs are diagnostics)")
     args = ap.parse_args()
@@ -462,15 +488,16 @@ def main():
 
     ep0 = episodes(env)
     env.timing_begin(K)
-    env.timing_stride(STEP_EVENT_STRIDE, 1)
-    elapsed, hist, gathers = timed(env, actions, W, K, world, dev, gather_at_end=world > 1)
+    env.timing_stride(1 if args.rollout else STEP_EVENT_STRIDE, 1)
+    elapsed, hist, gathers = timed(env, actions, W, K, world, dev, gather_at_end=world > 1, rollout=args.rollout)
     tm = env.timing_end()
     resets = int((episodes(env) - ep0).sum().item())
 
     steady = None
     if ss_steps:
         ep1 = episodes(env)
-        el2, hist2, g2 = timed(env, actions, W + K, ss_steps, world, dev, gather_at_end=world > 1)
+        el2, hist2, g2 = timed(env, actions, W + K, ss_steps, world, dev, gather_at_end=world > 1,
+                               rollout=args.rollout)
         r2 = torch.tensor([int((episodes(env) - ep1).sum().item())], device=dev, dtype=torch.int64)
         if world > 1:
             dist.all_reduce(r2)
@@ -487,8 +514,11 @@ def main():
     kind = "continuous" if args.continuous else "discrete"
     per_launch_s = tm["step_ms"] / max(1, tm["step_launches"]) / 1e3
     bytes_launch = B * step_kernel_bytes(R, 16 if args.continuous else 2, 8 if args.dtype == "f64" else 4)
-    achieved = bytes_launch / per_launch_s / 1e9
     kernel = f"cp_step_kernel<{kind}>" if args.dtype == "f32" else f"cp64::cp_step_kernel<{kind}>"
+    if args.rollout:   # one launch = many env-steps: per-step kernel time = launch time / steps per launch
+        per_launch_s = tm["step_ms"] / 1e3 / K
+        kernel = kernel.replace("cp_step_kernel", "cp_rollout_kernel") + " (time per env-step of the launch)"
+    achieved = bytes_launch / per_launch_s / 1e9
     traffic, traffic_src = pmc_traffic(kernel, B, R, kind)
     if args.raster:
         # C5: the render kernel writes 2.9 GB per step and is the dominant HBM consumer
@@ -508,6 +538,7 @@ def main():
                     "peak": round(VALU_PEAK_WINST_PER_S / 1e12, 4), "unit": "T wave-instr/s",
                     "frac": round(ach / VALU_PEAK_WINST_PER_S, 4), "source": vsrc + " SQ_INSTS_VALU"}
     name, wl = workload(args, world)
+    shape = env.kernel_shape()
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -523,7 +554,7 @@ def main():
         "data": "synthetic (hashed random actions keyed by global env id, Philox bump pushes; no pybullet, "
                 "see DESIGN.md)",
         "config": {"workload": wl, "name": name, "global_batch": world * B, "envs_per_gpu": B, "action_repeats": R,
-                   "steps_per_repeat": 1, "action_kind": kind, "step_kernel_shape": "latency (fp64)" if args.dtype == "f64" else step_shape(B),
+                   "steps_per_repeat": 1, "action_kind": kind, "kernel_shape": {"step": shape[0], "reset": shape[1]},
                    "parallelism": f"dp{world} (independent env shards, no per-step collective)",
                    "solver_iterations": env.cfg.phys.solver_iterations,
                    "residual_threshold": env.cfg.phys.residual_threshold},
@@ -539,7 +570,7 @@ def main():
                      "bytes_per_launch": bytes_launch,
                      "avg_launch_ms": round(per_launch_s * 1e3, 4),
                      "launches": tm["step_launches"],
-                     "launch_sample_stride": STEP_EVENT_STRIDE,
+                     "launch_sample_stride": 1 if args.rollout else STEP_EVENT_STRIDE,
                      "reset_kernel_avg_ms": round(tm["reset_ms"] / max(1, tm["reset_launches"]), 4),
                      **({"step_kernel_avg_ms": round(tm["step_ms"] / max(1, tm["step_launches"]), 4),
                          "render_launches": tm["render_launches"]} if args.raster else {})},
@@ -554,7 +585,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(R, args.cpu_seconds)
         if not args.no_parity:
             log("parity vs oracle ...")
-            out["parity"] = parity_check(dev, R)
+            out["parity"] = parity_check(dev, R, shape)
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:

@@ -5,7 +5,7 @@ library's entry points with these types.
 """
 import ctypes as C
 
-CP_ABI_VERSION = 2
+CP_ABI_VERSION = 3
 
 CP_BODY_GROUND, CP_BODY_CART, CP_BODY_POLE, CP_BODY_CART2, CP_BODY_POLE2 = range(5)
 CP_NUM_BODIES = 5
@@ -76,7 +76,22 @@ class cp_physics(C.Structure):
         ("inv_inertia", _F3 * CP_NUM_BODIES),
         ("friction", C.c_float * CP_NUM_BODIES),
         ("spawn_pos", _F3 * CP_NUM_BODIES),
+        ("model_flags", C.c_int32),
     ]
+
+
+# cp_physics.model_flags: alternatives to the default contact model (oracle-only unless in
+# CP_MODEL_GPU_FLAGS; DESIGN.md §3 sensitivity study)
+CP_MODEL_SPLIT_ISLANDS = 0x1
+CP_MODEL_VEL_FRICTION = 0x2
+CP_MODEL_PERSISTENT = 0x4
+CP_MODEL_GPU_FLAGS = 0x0
+
+# kernel shapes (cp_set_kernel_shape)
+CP_SHAPE_AUTO = -1
+CP_SHAPE_THROUGHPUT = 0
+CP_SHAPE_LATENCY = 1
+SHAPES = {"auto": CP_SHAPE_AUTO, "throughput": CP_SHAPE_THROUGHPUT, "latency": CP_SHAPE_LATENCY}
 
 
 class cp_config(C.Structure):

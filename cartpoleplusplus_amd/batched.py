@@ -62,6 +62,11 @@ class BatchedCartpole:
                 setattr(config.phys, k, v)
             if "dt" in phys and "inv_dt" not in phys:  # both are used by the kernels (cp_create checks)
                 config.phys.inv_dt = 1.0 / float(phys["dt"])
+            if "inertia" in phys and "inv_inertia" not in phys:  # the kernels read both (cp_create checks)
+                for b in range(abi.CP_NUM_BODIES):
+                    for k in range(3):
+                        i_ = float(config.phys.inertia[b][k])
+                        config.phys.inv_inertia[b][k] = 1.0 / i_ if i_ > 0 else 0.0
         self.cfg = config
         self.B, self.R, self.S = config.num_envs, config.action_repeats, config.steps_per_repeat
         # the state's real type (cp_config.precision); obs and all other outputs are float32
@@ -124,6 +129,52 @@ class BatchedCartpole:
                      "cp_step")
         return self.obs, self.reward, self.done
 
+    def rollout(self, actions, terminal=None):
+        """K env-steps in one kernel launch (cp_rollout): actions (K,B,2,2) float32 or (K,B,2)
+        int8 -> (obs (K,B,R,2,7), reward (K,B), done (K,B)); bit for bit K step() calls.
+        With autoreset, self.rollout_terminal_obs (K,B,R,2,7) holds the finishing obs of the
+        episodes that ended (terminal=False skips it).  The output tensors are reused by the
+        next rollout of the same K (clone them to keep them)."""
+        if not isinstance(actions, torch.Tensor):
+            actions = torch.as_tensor(actions)
+        if actions.dim() < 3:
+            raise ValueError(f"actions: (K, B, 2) int8 or (K, B, 2, 2) float, got shape {tuple(actions.shape)}")
+        K = int(actions.shape[0])
+        if actions.dtype == torch.int8:
+            kind = abi.CP_ACTION_DISCRETE
+            actions = _device_buffer(actions, (K, self.B, 2), torch.int8, self.device, "discrete actions")
+        else:
+            kind = abi.CP_ACTION_CONTINUOUS
+            if not actions.is_floating_point():
+                raise ValueError(f"actions: int8 indices (K, B, 2) or float (K, B, 2, 2), got {actions.dtype}")
+            actions = _device_buffer(actions, (K, self.B, 2, 2), torch.float32, self.device, "continuous actions")
+        want_term = bool(self.cfg.autoreset if terminal is None else terminal)
+        key = (K, want_term)
+        if getattr(self, "_roll_key", None) != key:   # output buffers reused across rollouts of one K
+            f32 = dict(device=self.device, dtype=torch.float32)
+            self._roll_bufs = (torch.empty((K, self.B, self.R, 2, 7), **f32), torch.empty((K, self.B), **f32),
+                               torch.empty((K, self.B), device=self.device, dtype=torch.uint8),
+                               torch.zeros((K, self.B, self.R, 2, 7), **f32) if want_term else None)
+            self._roll_key = key
+        obs, rew, done, self.rollout_terminal_obs = self._roll_bufs
+        native.check(self.h, self.lib.cp_rollout(self.h, K, _ptr(actions), kind, _ptr(obs), _ptr(rew), _ptr(done),
+                                                 _ptr(self.rollout_terminal_obs), self._stream()), "cp_rollout")
+        self.obs.copy_(obs[-1])
+        return obs, rew, done
+
+    def set_kernel_shape(self, step="auto", reset="auto"):
+        """Override the step / autoreset kernel shapes ("auto", "throughput" or "latency";
+        cp_set_kernel_shape).  Both shapes compute the same numbers."""
+        native.check(self.h, self.lib.cp_set_kernel_shape(self.h, abi.SHAPES[step], abi.SHAPES[reset]),
+                     "cp_set_kernel_shape")
+
+    def kernel_shape(self):
+        """-> (step shape, reset shape) in use: "throughput" or "latency"."""
+        st, rs = C.c_int(), C.c_int()
+        native.check(self.h, self.lib.cp_get_kernel_shape(self.h, C.byref(st), C.byref(rs)), "cp_get_kernel_shape")
+        names = {abi.CP_SHAPE_THROUGHPUT: "throughput", abi.CP_SHAPE_LATENCY: "latency"}
+        return names[st.value], names[rs.value]
+
     def enable_readback(self, on=True, reference_bug=True):
         """Per-substep 12-state pole readback (bullet_cartpole.py:212-234) into
         self.readback (B, 2, R, S, 4, 3) = (xyz, rpy, linvel, angvel)."""
@@ -175,6 +226,8 @@ class BatchedCartpole:
 
     def get_state(self):
         s = torch.empty((abi.CP_STATE_FIELDS, self.B), device=self.device, dtype=self.real)
+        if s.numel() * s.element_size() != self.lib.cp_state_bytes(self.h):
+            raise native.CartpoleError("state buffer size disagrees with cp_state_bytes")
         native.check(self.h, self.lib.cp_get_state(self.h, _ptr(s), self._stream()), "cp_get_state")
         return s
 

@@ -126,6 +126,9 @@ struct Bufs {
     void launch_step(bool lat, int kind, const cp_config& cfg, const cpc::Bufs& b, const void* actions,          \
                      float* obs_out, float* reward_out, uint8_t* done_out, float* term_out, float* readback,    \
                      int rb_bug, const cpc::Lqr& lq, hipStream_t st);                                            \
+    void launch_rollout(bool lat, int kind, const cp_config& cfg, const cpc::Bufs& b, int steps,                 \
+                        const void* actions, float* obs_out, float* reward_out, uint8_t* done_out,              \
+                        float* term_out, const cpc::Lqr& lq, hipStream_t st);                                   \
     }
 CP_DECLARE_LAUNCHES(cp)
 CP_DECLARE_LAUNCHES(cp64)

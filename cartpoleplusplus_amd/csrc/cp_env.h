@@ -472,6 +472,200 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
     }
 }
 
+// One env-step's action forces, action_force * action (bullet_cartpole.py:201-207): continuous
+// float4 (a00 a01 a10 a11) or discrete int8 x 2 through kDiscrete (out-of-range index = 0).
+template <int KIND>
+CP_DEV void action_forces(const void* actions, size_t row, real F, real f[4]) {
+    real a00, a01, a10, a11;
+    if constexpr (KIND == CP_ACTION_CONTINUOUS) {
+        const float4 a = reinterpret_cast<const float4*>(actions)[row];
+        a00 = a.x; a01 = a.y; a10 = a.z; a11 = a.w;
+    } else {
+        const char2 a = reinterpret_cast<const char2*>(actions)[row];
+        int k0 = a.x, k1 = a.y;
+        k0 = (k0 < 0 || k0 >= CP_NUM_DISCRETE) ? 0 : k0;
+        k1 = (k1 < 0 || k1 >= CP_NUM_DISCRETE) ? 0 : k1;
+        a00 = kDiscrete[k0][0]; a01 = kDiscrete[k0][1];
+        a10 = kDiscrete[k1][0]; a11 = kDiscrete[k1][1];
+    }
+    f[0] = a00 * F; f[1] = a01 * F; f[2] = a10 * F; f[3] = a11 * F;
+}
+
+// cp_rollout: K consecutive env-steps of every env in one launch, bit for bit the outputs and
+// final state of K cp_step calls (bullet_cartpole.py:178-275 K times, each finishing episode
+// reset in its step, :313-346).  Each lane pair runs a state machine over substeps:
+//   STEP   the R x S substeps of step k, each followed by the step's action forces (+ LQR),
+//          obs at each repeat end, reward / done at the end;
+//   RESET  (autoreset of an episode that ended in step k) spawn poses, settle + bump substeps;
+//          its obs are step k's obs, the finishing obs step k's terminal obs.
+// Every lane with work runs ONE substep per loop trip whatever its phase, so an env that resets
+// costs its own 130 substeps instead of stalling the wave's other envs at a step boundary, and a
+// wave no longer waits for the slowest wave of the grid between steps.  The substep variant is
+// the step kernel's (the reset kernel's C44 / ALLIN options compute the same numbers).  The
+// episode counters live in registers for the whole launch (both lanes of a pair hold identical
+// copies: no cross-lane memory traffic) and are written back once at the end.
+template <int KIND, bool LQR, bool LAT>
+__global__ void __launch_bounds__(WAVE)
+__attribute__((amdgpu_waves_per_eu(LAT ? 1 : CP_WAVES_PER_EU, LAT ? 1 : CP_WAVES_PER_EU)))
+cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_out, float* reward_out,
+                  uint8_t* done_out, float* term_out, Lqr lq) {
+    __shared__ real lds_pool[POOL_FLOATS * WAVE];
+    const int B = cfg.num_envs;
+    const int t = blockIdx.x * WAVE + threadIdx.x;
+    const int i = t >> 1, isl = t & 1;
+    if (i >= B) return;  // whole lane pairs (B envs = 2B lanes)
+    const bool lead = isl == 0;
+    const int R = cfg.action_repeats, SR = cfg.steps_per_repeat, RS = R * SR;
+    const int nreset = cfg.settle_steps + cfg.initial_force_steps;
+    real* pool = lds_pool + threadIdx.x;
+    real* pool0 = lds_pool + (threadIdx.x & ~1u);
+    const Mem G = Mem::make(b.state, b.scratch, B, i, isl);
+    const Lane L = Lane::make(isl, cfg.phys);
+    const SoaF term = SoaF::make(b.term_obs, B, R * 14);
+    const uint32_t toff = SoaF::eoff(i);
+    const size_t obs_step = (size_t)B * R * 14;
+    Stamps ST;
+    Sim S;
+    load_sim(S, G.st, G.off);
+    int steps = ldi(G.st, CP_SF_STEPS, G.off);
+    int episode = ldi(G.st, CP_SF_EPISODE, G.off);
+    bool done_flag = ldi(G.st, CP_SF_DONE, G.off) != 0;
+    float ret_acc = b.ret_acc[i];
+    int ov = 0;
+    int k = 0, sub = 0;
+    bool resetting = false, lqr_done = false, last_sim = false;
+    real f[4];
+    real u[2][2] = {{real(0.0), real(0.0)}, {real(0.0), real(0.0)}};
+    const float* Kg = nullptr;
+    if constexpr (LQR) Kg = lq.gains + (lq.per_env ? (size_t)i * 32 : 0);
+    // the next simulated step from k on: steps of an env that is done before them only return its
+    // last obs, reward 0, done 1 (:179-181); false when the K steps are over
+    auto begin_step = [&]() -> bool {
+        for (; k < K && done_flag; ++k) {
+            last_sim = false;
+            if (lead) {
+                float* o = obs_out + (size_t)k * obs_step + (size_t)i * R * 14;
+                for (int q = 0; q < R * 14; ++q) o[q] = term.ld(q, toff);
+                reward_out[(size_t)k * B + i] = 0.0f;
+                done_out[(size_t)k * B + i] = 1;
+            }
+        }
+        if (k >= K) return false;
+        last_sim = true;
+        action_forces<KIND>(actions, (size_t)k * B + i, real(cfg.action_force), f);
+        if constexpr (LQR) {
+            lqr_done = false;
+            lqr_observe(S, cfg, lq, Kg, u, nullptr);
+        }
+        sub = 0;
+        return true;
+    };
+    bool work = begin_step();
+    while (__ballot(work) != 0ull) {
+        if (!work) continue;
+        substep<LAT && !kF64, false, kAllinStep>(S, cfg.phys, L, pool, pool0, ov, G, ST);
+        if (!resetting) {
+            if constexpr (LQR) {
+                apply_force_link<0>(S, f[0] + u[0][0], f[1] + u[0][1]);
+                apply_force_link<1>(S, f[2] + u[1][0], f[3] + u[1][1]);
+                lqr_done |= lqr_observe(S, cfg, lq, Kg, u, nullptr);
+            } else {
+                apply_force_link<0>(S, f[0], f[1]);
+                apply_force_link<1>(S, f[2], f[3]);
+            }
+            ++sub;
+            float* obs = obs_out + (size_t)k * obs_step + (size_t)i * R * 14;
+            if (lead && sub % SR == 0) {
+                float row[14];
+                write_obs_row(S, row);
+                const int r = sub / SR - 1;
+#pragma unroll
+                for (int q = 0; q < 14; ++q) obs[r * 14 + q] = row[q];
+            }
+            if (sub < RS) continue;
+            // step end (the step kernel's epilogue)
+            steps += 1;
+            bool done = steps >= cfg.max_episode_len;
+            if (cfg.done_on_bounds && bounds_exceeded(S, cfg)) done = true;
+            if (LQR && lqr_done) done = true;
+            const float ret = ret_acc + 1.0f;
+            if (lead) {
+                reward_out[(size_t)k * B + i] = 1.0f;
+                done_out[(size_t)k * B + i] = done ? 1 : 0;
+            }
+            if (done) {
+                if (lead) {
+                    b.last_ret[i] = ret;
+                    b.last_len[i] = steps;
+                    for (int q = 0; q < R * 14; ++q) term.st(q, toff, obs[q]);
+                    if (term_out)
+                        for (int q = 0; q < R * 14; ++q) term_out[(size_t)k * obs_step + (size_t)i * R * 14 + q] = obs[q];
+                }
+                ret_acc = 0.0f;
+                done_flag = true;
+                if (cfg.autoreset) {  // the reset kernel's prologue: pending forces survive
+                    resetting = true;
+                    sub = 0;
+#pragma unroll
+                    for (int d = 0; d < CP_NUM_DYN; ++d) {
+                        S.b[d].x = mk(cfg.phys.spawn_pos[d + 1][0], cfg.phys.spawn_pos[d + 1][1],
+                                      cfg.phys.spawn_pos[d + 1][2]);
+                        S.b[d].q[0] = real(0.0); S.b[d].q[1] = real(0.0); S.b[d].q[2] = real(0.0);
+                        S.b[d].q[3] = real(1.0);
+                        S.b[d].v = mk(real(0.0), real(0.0), real(0.0));
+                        S.b[d].w = mk(real(0.0), real(0.0), real(0.0));
+                    }
+#pragma unroll
+                    for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
+                        G.sw(CP_SF_WS_ID(0, j), bits_to<real>(0xFFFFFFFFu));
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) G.sl(CP_SF_WS_LAM(0, j, q), real(0.0));
+                    }
+                    continue;
+                }
+            } else {
+                ret_acc = ret;
+            }
+            ++k;
+            work = begin_step();
+        } else {
+            const int kb = sub - cfg.settle_steps;
+            if (kb >= 0) {
+                real fx, fy;
+                bump_force(cfg, b.bumps, i, episode, kb, 0, fx, fy);
+                apply_force_link<0>(S, fx, fy);
+                bump_force(cfg, b.bumps, i, episode, kb, 1, fx, fy);
+                apply_force_link<1>(S, fx, fy);
+            }
+            if (++sub < nreset) continue;
+            // reset end (the reset kernel's epilogue): every repeat slot shows the new pose
+            if (lead) {
+                float row[14];
+                write_obs_row(S, row);
+                float* o = obs_out + (size_t)k * obs_step + (size_t)i * R * 14;
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int q = 0; q < 14; ++q) o[r * 14 + q] = row[q];
+            }
+            resetting = false;
+            steps = 0;
+            done_flag = false;
+            episode += 1;
+            ++k;
+            work = begin_step();
+        }
+    }
+    ov += (int)partner_u((uint32_t)ov);  // both lanes of every pair are here
+    if (!lead) return;
+    store_sim(S, G.st, G.off);
+    sti(G.st, CP_SF_STEPS, G.off, steps);
+    sti(G.st, CP_SF_EPISODE, G.off, episode);
+    sti(G.st, CP_SF_DONE, G.off, done_flag ? 1 : 0);
+    b.ret_acc[i] = ret_acc;
+    b.stepped[i] = last_sim ? 1 : 0;  // step K-1's value, as after the K-th cp_step
+    if (ov) b.overflow[i] += ov;
+}
+
 // ---------------------------------------------------------------- host launchers
 static inline unsigned env_grid(int n, int block) { return (unsigned)((n + block - 1) / block); }
 
@@ -506,6 +700,36 @@ static void launch_step_t(bool lat, const cp_config& cfg, const Bufs& b, const v
         else
             hipLaunchKernelGGL((cp_step_kernel<K, Q, false>), grid, block, 0, st, cfg, b, actions, obs_out, reward_out,
                                done_out, term_out, readback, rb_bug, lq);
+    }
+}
+
+template <int K, bool Q>
+static void launch_rollout_t(bool lat, const cp_config& cfg, const Bufs& b, int steps, const void* actions,
+                             float* obs_out, float* reward_out, uint8_t* done_out, float* term_out, const Lqr& lq,
+                             hipStream_t st) {
+    const dim3 grid(env_grid(2 * cfg.num_envs, WAVE)), block(WAVE);  // two lanes per env
+    if (lat || kF64)
+        hipLaunchKernelGGL((cp_rollout_kernel<K, Q, true>), grid, block, 0, st, cfg, b, steps, actions, obs_out,
+                           reward_out, done_out, term_out, lq);
+    else
+        hipLaunchKernelGGL((cp_rollout_kernel<K, Q, false>), grid, block, 0, st, cfg, b, steps, actions, obs_out,
+                           reward_out, done_out, term_out, lq);
+}
+
+void launch_rollout(bool lat, int kind, const cp_config& cfg, const Bufs& b, int steps, const void* actions,
+                    float* obs_out, float* reward_out, uint8_t* done_out, float* term_out, const Lqr& lq,
+                    hipStream_t st) {
+    const bool q = lq.gains != nullptr;
+    if (kind == CP_ACTION_CONTINUOUS) {
+        if (q) launch_rollout_t<CP_ACTION_CONTINUOUS, true>(lat, cfg, b, steps, actions, obs_out, reward_out, done_out,
+                                                            term_out, lq, st);
+        else launch_rollout_t<CP_ACTION_CONTINUOUS, false>(lat, cfg, b, steps, actions, obs_out, reward_out, done_out,
+                                                           term_out, lq, st);
+    } else {
+        if (q) launch_rollout_t<CP_ACTION_DISCRETE, true>(lat, cfg, b, steps, actions, obs_out, reward_out, done_out,
+                                                          term_out, lq, st);
+        else launch_rollout_t<CP_ACTION_DISCRETE, false>(lat, cfg, b, steps, actions, obs_out, reward_out, done_out,
+                                                         term_out, lq, st);
     }
 }
 

@@ -154,6 +154,8 @@ struct cp_handle {
     int par;           // counter the next call appends to
     int reset_lat;     // 1: latency-shaped autoreset kernel (episodes end at different steps)
     int step_lat;      // 1: latency-shaped step kernel (every wave gets a SIMD of its own)
+    int reset_req;     // cp_set_kernel_shape request (CP_SHAPE_AUTO: choose_reset_shape decides)
+    int step_req;
     std::string err;
 };
 
@@ -270,9 +272,22 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     // host-computed derived fields must agree with their sources (the kernels use both)
     if (!(cfg->phys.dt > 0.0f) || std::fabs((double)cfg->phys.dt * (double)cfg->phys.inv_dt - 1.0) > 1e-6)
         return fail(nullptr, "cp_create: phys.inv_dt must be 1 / phys.dt (recompute it when dt changes)");
-    if (std::fabs((double)cfg->tan_angle_threshold - std::tan((double)cfg->angle_threshold)) > 1e-6 ||
-        std::fabs((double)cfg->sin_angle_threshold - std::sin((double)cfg->angle_threshold)) > 1e-6)
-        return fail(nullptr, "cp_create: tan/sin_angle_threshold must be tan/sin(angle_threshold)");
+    {   // relative tolerance: near pi/2 tan's slope makes the float32 rounding of the angle visible
+        const double a = (double)cfg->angle_threshold, t = std::tan(a), s = std::sin(a);
+        if (std::fabs((double)cfg->tan_angle_threshold - t) > 1e-6 * std::max(1.0, std::fabs(t)) ||
+            std::fabs((double)cfg->sin_angle_threshold - s) > 1e-6)
+            return fail(nullptr, "cp_create: tan/sin_angle_threshold must be tan/sin(angle_threshold)");
+    }
+    for (int b = 0; b < CP_NUM_BODIES; ++b) {   // the kernels read both members of each pair
+        for (int k = 0; k < 3; ++k) {
+            const double I = cfg->phys.inertia[b][k], iI = cfg->phys.inv_inertia[b][k];
+            if (I > 0.0 ? std::fabs(I * iI - 1.0) > 1e-6 : iI != 0.0)
+                return fail(nullptr, "cp_create: phys.inv_inertia must be 1 / phys.inertia (0 for a static body)");
+        }
+    }
+    if (cfg->phys.model_flags & ~CP_MODEL_GPU_FLAGS)
+        return fail(nullptr, "cp_create: phys.model_flags names a model alternative the HIP kernels do not "
+                             "implement (oracle-only, DESIGN.md §3)");
     if (!(cfg->phys.residual_threshold >= 0.0f)) return fail(nullptr, "cp_create: negative residual_threshold");
     if (cfg->precision != CP_PRECISION_F32 && cfg->precision != CP_PRECISION_F64)
         return fail(nullptr, "cp_create: precision must be CP_PRECISION_F32 or CP_PRECISION_F64");
@@ -288,6 +303,7 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     h->lqr = cpc::Lqr{nullptr, 0, nullptr, 0.0f, 0.0f};
     h->f64 = cfg->precision == CP_PRECISION_F64;
     h->pixels = nullptr;
+    h->reset_req = h->step_req = CP_SHAPE_AUTO;
     choose_reset_shape(h);
     cp_default_raster_config(&h->raster);
     std::memset(&h->b, 0, sizeof(h->b));
@@ -406,6 +422,9 @@ static void choose_reset_shape(cp_handle* h) {
     h->reset_lat = (e && (e[0] == '0' || e[0] == '1')) ? e[0] == '1' : (h->cfg.done_on_bounds || lqr_done || small);
     const char* es = std::getenv("CP_STEP_LATENCY");
     h->step_lat = (es && (es[0] == '0' || es[0] == '1')) ? es[0] == '1' : small;
+    if (h->reset_req != CP_SHAPE_AUTO) h->reset_lat = h->reset_req == CP_SHAPE_LATENCY;
+    if (h->step_req != CP_SHAPE_AUTO) h->step_lat = h->step_req == CP_SHAPE_LATENCY;
+    if (h->f64) h->reset_lat = h->step_lat = 1;  // fp64: the 512-register shape only
 }
 
 static int launch_reset_from_list(cp_handle* h, float* obs_out, hipStream_t st, bool render) {
@@ -460,6 +479,30 @@ int cp_step(cp_handle* h, const void* actions, int action_kind, float* obs_out, 
     return 0;
 }
 
+int cp_rollout(cp_handle* h, int steps, const void* actions, int action_kind, float* obs_out, float* reward_out,
+               uint8_t* done_out, float* terminal_obs_out, void* stream) {
+    if (!h || !actions || !obs_out || !reward_out || !done_out) return fail(h, "cp_rollout: null argument");
+    if (steps <= 0) return fail(h, "cp_rollout: steps must be > 0");
+    if (action_kind != CP_ACTION_CONTINUOUS && action_kind != CP_ACTION_DISCRETE)
+        return fail(h, "cp_rollout: action_kind must be CP_ACTION_CONTINUOUS or CP_ACTION_DISCRETE");
+    if (h->readback || h->lqr.state8 || h->pixels)
+        return fail(h, "cp_rollout: the per-step side outputs (readback, LQR 8-states, raster obs) are cp_step-only; "
+                       "disable them first");
+    hipStream_t st = (hipStream_t)stream;
+    CP_TRY(h, hipSetDevice(h->device));
+    hipEvent_t* ev = timing_slot(h, 0);
+    if (ev) CP_TRY(h, hipEventRecord(ev[0], st));
+    if (h->f64)
+        cp64::launch_rollout(true, action_kind, h->cfg, h->b, steps, actions, obs_out, reward_out, done_out,
+                             terminal_obs_out, h->lqr, st);
+    else
+        cp::launch_rollout(h->step_lat != 0, action_kind, h->cfg, h->b, steps, actions, obs_out, reward_out, done_out,
+                           terminal_obs_out, h->lqr, st);
+    CP_TRY(h, hipGetLastError());
+    if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
+    return 0;
+}
+
 int cp_set_readback(cp_handle* h, float* readback_out, int reference_bug) {
     if (!h) return fail(h, "cp_set_readback: null handle");
     h->readback = readback_out;
@@ -488,7 +531,32 @@ int cp_set_bump_forces(cp_handle* h, const float* forces, void* stream) {
     return 0;
 }
 
-int cp_get_state(cp_handle* h, float* state_out, void* stream) {
+int64_t cp_state_bytes(const cp_handle* h) {
+    if (!h) return fail(nullptr, "cp_state_bytes: null handle");
+    return (int64_t)CP_STATE_FIELDS * h->cfg.num_envs * (h->f64 ? (int64_t)sizeof(double) : (int64_t)sizeof(float));
+}
+
+int cp_set_kernel_shape(cp_handle* h, int step_shape, int reset_shape) {
+    if (!h) return fail(h, "cp_set_kernel_shape: null handle");
+    auto ok = [](int v) { return v == CP_SHAPE_AUTO || v == CP_SHAPE_THROUGHPUT || v == CP_SHAPE_LATENCY; };
+    if (!ok(step_shape) || !ok(reset_shape))
+        return fail(h, "cp_set_kernel_shape: shapes must be CP_SHAPE_AUTO, CP_SHAPE_THROUGHPUT or CP_SHAPE_LATENCY");
+    if (h->f64 && (step_shape == CP_SHAPE_THROUGHPUT || reset_shape == CP_SHAPE_THROUGHPUT))
+        return fail(h, "cp_set_kernel_shape: fp64 handles have the latency shape only");
+    h->step_req = step_shape;
+    h->reset_req = reset_shape;
+    choose_reset_shape(h);
+    return 0;
+}
+
+int cp_get_kernel_shape(const cp_handle* h, int* step_shape, int* reset_shape) {
+    if (!h) return fail(nullptr, "cp_get_kernel_shape: null handle");
+    if (step_shape) *step_shape = h->step_lat ? CP_SHAPE_LATENCY : CP_SHAPE_THROUGHPUT;
+    if (reset_shape) *reset_shape = h->reset_lat ? CP_SHAPE_LATENCY : CP_SHAPE_THROUGHPUT;
+    return 0;
+}
+
+int cp_get_state(cp_handle* h, void* state_out, void* stream) {
     if (!h || !state_out) return fail(h, "cp_get_state: null argument");
     CP_TRY(h, hipSetDevice(h->device));
     size_t n = (size_t)CP_STATE_FIELDS * h->cfg.num_envs;
@@ -497,7 +565,7 @@ int cp_get_state(cp_handle* h, float* state_out, void* stream) {
     return 0;
 }
 
-int cp_set_state(cp_handle* h, const float* state_in, void* stream) {
+int cp_set_state(cp_handle* h, const void* state_in, void* stream) {
     if (!h || !state_in) return fail(h, "cp_set_state: null argument");
     CP_TRY(h, hipSetDevice(h->device));
     size_t n = (size_t)CP_STATE_FIELDS * h->cfg.num_envs;

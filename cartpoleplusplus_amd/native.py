@@ -21,6 +21,7 @@ EXPORTS = (
     "cp_debug_stamps", "cp_default_raster_config", "cp_set_raster", "cp_timing_render",
     "cp_event_record_bytes", "cp_encode_events", "cp_eventlog_open", "cp_eventlog_write", "cp_eventlog_close",
     "cp_set_lqr", "cp_get_stepped", "cp_replay_init", "cp_replay_add", "cp_replay_sample",
+    "cp_state_bytes", "cp_set_kernel_shape", "cp_get_kernel_shape", "cp_rollout",
 )
 
 _lib = None
@@ -73,6 +74,10 @@ def load():
         "cp_replay_init": (I, [P(abi.cp_replay), VP, I, VP]),
         "cp_replay_add": (I, [P(abi.cp_replay), VP, I, VP, VP, I, VP, VP, VP, VP, VP, I, VP]),
         "cp_replay_sample": (I, [P(abi.cp_replay), I, VP, C.c_uint64, C.c_uint64, P(abi.cp_replay_batch), VP]),
+        "cp_state_bytes": (C.c_int64, [VP]),
+        "cp_rollout": (I, [VP, I, VP, I, VP, VP, VP, VP, VP]),
+        "cp_set_kernel_shape": (I, [VP, I, I]),
+        "cp_get_kernel_shape": (I, [VP, P(I), P(I)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CP_ABI_VERSION 2
+#define CP_ABI_VERSION 3
 
 /* Bodies, in the reference's loadURDF order (bullet_cartpole.py:154-160). */
 #define CP_BODY_GROUND 0
@@ -105,7 +105,20 @@ typedef struct cp_physics {
     float inv_inertia[CP_NUM_BODIES][3];
     float friction[CP_NUM_BODIES];        /* lateral friction; pair mu = product */
     float spawn_pos[CP_NUM_BODIES][3];    /* bullet_cartpole.py:154-160,319-323  */
+    int32_t model_flags;      /* CP_MODEL_* alternatives to the default model (0) */
 } cp_physics;
+
+/* Alternatives to the default contact model (cp_physics.model_flags), for the sensitivity
+ * study of the [ext] choices.  cp_create rejects a flag the HIP kernels do
+ * not implement (the oracle implements all of them). */
+#define CP_MODEL_SPLIT_ISLANDS   0x1  /* the two islands as separate solver groups, one stopping
+                                         decision each (instead of one group per env)          */
+#define CP_MODEL_VEL_FRICTION    0x2  /* velocity-dependent first friction direction (Bullet's
+                                         convertContact default) instead of btPlaneSpace1 only  */
+#define CP_MODEL_PERSISTENT      0x4  /* Bullet's persistent manifold (getCacheEntry matching,
+                                         replaceContactPoint, sortCachedPoints,
+                                         refreshContactPoints) instead of feature-id matching   */
+#define CP_MODEL_GPU_FLAGS       0x0  /* the flags the HIP kernels implement                     */
 
 typedef struct cp_config {
     int32_t num_envs;            /* B                                          */
@@ -179,6 +192,21 @@ int cp_step(cp_handle* h, const void* actions, int action_kind,
             float* obs_out, float* reward_out, uint8_t* done_out,
             float* terminal_obs_out, void* stream);
 
+/* K consecutive env-steps in ONE kernel launch: the outputs and the final state are bit for bit
+ * those of K cp_step calls with actions[k] (k = 0..K-1), autoreset included (an episode that
+ * ends in step k is reset in step k: obs_out[k] holds the new episode's first obs and
+ * terminal_obs_out[k] the finishing obs).  Replaces the agents' per-step loop over
+ * BulletCartpole.step (bullet_cartpole.py:178-275; e.g. the reference's random / LQR rollouts,
+ * random_action_agent.py:876-906) when the actions are known in advance or come from the
+ * in-kernel LQR policy (cp_set_lqr, without the 8-state output).  Each env advances through its
+ * own substeps without waiting for the other envs between steps.
+ * Layouts: actions [K][B][2][2] f32 or [K][B][2] i8; obs_out and terminal_obs_out (may be NULL)
+ * [K][B][R][2][7]; reward_out [K][B]; done_out [K][B] (device pointers).  The per-step side
+ * outputs (readback, 8-states, raster) must be disabled.  With cp_timing_begin active the
+ * launch is timed as one step-kernel launch. */
+int cp_rollout(cp_handle* h, int steps, const void* actions, int action_kind, float* obs_out,
+               float* reward_out, uint8_t* done_out, float* terminal_obs_out, void* stream);
+
 /* Optional per-substep 12-state readback of both poles (bullet_cartpole.py:212-234,
  * exposed there as monkey_positions / monkey_velocities):
  * float32 [B][2 poles][R][S][4][3] = (xyz, rpy, linvel, angvel).  Enabled when
@@ -206,9 +234,22 @@ int cp_set_lqr(cp_handle* h, const float* gains, int per_env, float* state8_out,
                float done_angle);
 
 /* Full env state, SoA [CP_STATE_FIELDS][B] of the handle's real type (float32, or float64
- * for CP_PRECISION_F64 handles), device pointers. */
-int cp_get_state(cp_handle* h, float* state_out, void* stream);
-int cp_set_state(cp_handle* h, const float* state_in, void* stream);
+ * for CP_PRECISION_F64 handles), device pointers of cp_state_bytes(h) bytes. */
+int cp_get_state(cp_handle* h, void* state_out, void* stream);
+int cp_set_state(cp_handle* h, const void* state_in, void* stream);
+int64_t cp_state_bytes(const cp_handle* h);   /* CP_STATE_FIELDS * B * sizeof(real); <0: error */
+
+/* Kernel shapes.  The step and autoreset kernels each come in two register budgets:
+ * THROUGHPUT (2 waves per SIMD; bursts and batches above 32,768 envs) and LATENCY (1 wave
+ * per SIMD with 512 registers and fast-form solver rows; short reset lists and small
+ * batches).  Both compute the same numbers (the GPU parity suite runs every case on both).
+ * cp_create picks them (CP_SHAPE_AUTO: DESIGN.md §5); this call overrides either
+ * (fp64 handles have only the latency shape and reject THROUGHPUT). */
+#define CP_SHAPE_AUTO       (-1)
+#define CP_SHAPE_THROUGHPUT 0
+#define CP_SHAPE_LATENCY    1
+int cp_set_kernel_shape(cp_handle* h, int step_shape, int reset_shape);
+int cp_get_kernel_shape(const cp_handle* h, int* step_shape, int* reset_shape);   /* the shapes in use */
 
 /* Last completed episode per env: return (float32 [B]) and length (int32 [B]);
  * either pointer may be NULL.  Feeds the RCCL return histogram. */

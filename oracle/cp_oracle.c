@@ -748,7 +748,7 @@ static void warm_pair(sim_t* S, const cp_physics* P, island_t* I, int isl, int j
 
 /* one p.stepSimulation() of the scene (DESIGN.md §Physics model, steps 1-8) */
 static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* iters_out, int32_t* npts_out,
-                    int32_t* isl_iters) {
+                    int32_t* isl_iters, int32_t* merged_out) {
     const real dt = (real)P->dt, inv_dt = (real)P->inv_dt;
     /* 1. orientation matrices, world inverse inertia */
     for (int d = 0; d < CP_NUM_DYN; ++d) {
@@ -849,6 +849,7 @@ static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* i
     const real tol = SQRT((real)P->residual_threshold);
     int merged = 0;
     for (int p = 0; p < CP_NUM_ISLANDS; ++p) merged |= (isl[p].man[3].cnt + isl[p].man[4].cnt) > 0;
+    if (merged_out) *merged_out += merged;
     int it = 0;
     if (!merged) {
         for (int p = 0; p < CP_NUM_ISLANDS; ++p)
@@ -990,7 +991,7 @@ void orc_world_reset_pose(orc_world* w, int body, const double p[3], const doubl
 void orc_world_step(orc_world* w, const cp_config* cfg) {
     sim_t S;
     world_load(w, &S);
-    substep(&S, &cfg->phys, &w->overflow, &w->last_iterations, &w->last_points, NULL);
+    substep(&S, &cfg->phys, &w->overflow, &w->last_iterations, &w->last_points, NULL, NULL);
     world_store(w, &S);
 }
 void orc_world_apply_force_link(orc_world* w, int body, double fx, double fy, double fz) {
@@ -1092,6 +1093,7 @@ int orc_envs_create(const cp_config* cfg, orc_envs** out) {
     e->last_len = (int32_t*)calloc(B, sizeof(int32_t));
     e->overflow = (int32_t*)calloc(B, sizeof(int32_t));
     e->sweeps = (int32_t*)calloc((size_t)B * 2, sizeof(int32_t));
+    e->merged = (int32_t*)calloc(B, sizeof(int32_t));
     for (int i = 0; i < e->B; ++i) {
         for (int d = 0; d < CP_NUM_DYN; ++d) {
             for (int k = 0; k < 3; ++k) SF(e, CP_SF_BODY(d, k), i) = cfg->phys.spawn_pos[d + 1][k];
@@ -1109,7 +1111,7 @@ int orc_envs_create(const cp_config* cfg, orc_envs** out) {
 void orc_envs_destroy(orc_envs* e) {
     if (!e) return;
     free(e->state); free(e->term_obs); free(e->bump_forces); free(e->ret_acc);
-    free(e->last_ret); free(e->last_len); free(e->overflow); free(e->sweeps);
+    free(e->last_ret); free(e->last_len); free(e->overflow); free(e->sweeps); free(e->merged);
     free(e);
 }
 void orc_envs_set_bump_forces(orc_envs* e, const float* f) {
@@ -1164,9 +1166,9 @@ static void reset_one(orc_envs* e, int i, float* obs_row /* R*14 */) {
             for (int k = 0; k < 4; ++k) S.ws_lam[p][j][k] = RC(0);
         }
     int32_t ov = 0;
-    for (int s = 0; s < cfg->settle_steps; ++s) substep(&S, &cfg->phys, &ov, NULL, NULL, NULL);
+    for (int s = 0; s < cfg->settle_steps; ++s) substep(&S, &cfg->phys, &ov, NULL, NULL, NULL, NULL);
     for (int k = 0; k < cfg->initial_force_steps; ++k) {
-        substep(&S, &cfg->phys, &ov, NULL, NULL, NULL);
+        substep(&S, &cfg->phys, &ov, NULL, NULL, NULL, NULL);
         for (int c = 0; c < 2; ++c) {
             real fx, fy;
             bump_force(e, i, episode, k, c, &fx, &fy);
@@ -1287,13 +1289,14 @@ static void step_one(orc_envs* e, int i, const void* actions, int kind, float* o
     int32_t ov = 0;
     int32_t* sw = e->sweeps + (size_t)i * 2;
     sw[0] = sw[1] = 0;
+    e->merged[i] = 0;
     real u[2][2] = {{RC(0), RC(0)}, {RC(0), RC(0)}};
     int lqr_done = 0;
     const float* K = e->lqr_gains ? e->lqr_gains + (e->lqr_per_env ? (size_t)i * 32 : 0) : NULL;
     if (K) lqr_observe(e, &S, K, u, NULL);
     for (int r = 0; r < R; ++r) {
         for (int s = 0; s < Sn; ++s) {
-            substep(&S, &cfg->phys, &ov, NULL, NULL, sw);
+            substep(&S, &cfg->phys, &ov, NULL, NULL, sw, &e->merged[i]);
             if (K) {   /* disturbance + control from the pre-step state (:897-901) */
                 apply_force_link(&S, 0, a[0][0] * F + u[0][0], a[0][1] * F + u[0][1], RC(0));
                 apply_force_link(&S, 2, a[1][0] * F + u[1][0], a[1][1] * F + u[1][1], RC(0));
@@ -1361,6 +1364,7 @@ int orc_envs_step_omp(orc_envs* e, const void* actions, int kind, float* obs_out
     return used;
 }
 void orc_envs_sweeps(const orc_envs* e, int32_t* out) { memcpy(out, e->sweeps, (size_t)e->B * 2 * sizeof(int32_t)); }
+void orc_envs_merged(const orc_envs* e, int32_t* out) { memcpy(out, e->merged, (size_t)e->B * sizeof(int32_t)); }
 void orc_envs_episode_returns(const orc_envs* e, float* ret, int32_t* len) {
     if (ret) memcpy(ret, e->last_ret, (size_t)e->B * sizeof(float));
     if (len) memcpy(len, e->last_len, (size_t)e->B * sizeof(int32_t));

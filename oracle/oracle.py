@@ -87,6 +87,7 @@ def load(precision="f32"):
         "orc_envs_step_omp": (C.c_int, [VP, VP, C.c_int, VP, VP, VP, C.c_int]),
         "orc_envs_episode_returns": (None, [VP, VP, VP]),
         "orc_envs_sweeps": (None, [VP, VP]),
+        "orc_envs_merged": (None, [VP, VP]),
         "orc_render_frame": (None, [VP, VP, VP, C.c_int, VP]),
         "orc_philox4x32_10": (None, [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]),
         "orc_sincos_turns": (None, [C.c_float, P(C.c_float), P(C.c_float)]),
@@ -266,6 +267,13 @@ class Envs:
         n = np.zeros(self.B, np.int32)
         self.lib.orc_envs_episode_returns(self.h, _ptr(r), _ptr(n))
         return r, n
+
+    def merged(self):
+        """(B,) diagnostic: substeps of the last step whose solve was merged (a cross-island
+        contact: pairs 5-8, solved in the order 0 2 1 3 4 9 5 6 7 8)."""
+        out = np.zeros(self.B, np.int32)
+        self.lib.orc_envs_merged(self.h, _ptr(out))
+        return out
 
     def sweeps(self):
         """(B, 2) diagnostic: max PGS sweeps per island over the last step."""

@@ -8,7 +8,7 @@ import torch
 
 from cartpoleplusplus_amd import abi
 from cartpoleplusplus_amd.lqr import exact_gains
-from tests.test_gpu_parity import _assert_same, _np, _pair
+from tests.test_gpu_parity import _assert_same, _np, _pair, shapes
 
 pytestmark = pytest.mark.gpu
 
@@ -17,12 +17,14 @@ def _same_state(gpu, orc, what):
     _assert_same(_np(gpu.get_state()).view(np.uint32), orc.get_state().view(np.uint32), what)
 
 
-def test_per_env_gains_autoreset_bounds(oracle_mod):
+@shapes
+def test_per_env_gains_autoreset_bounds(oracle_mod, shape):
     B = 128
-    gpu, orc = _pair(oracle_mod, num_envs=B, action_repeats=3, initial_force=55.0, seed=21, autoreset=1)
+    gpu, orc = _pair(oracle_mod, shape, num_envs=B, action_repeats=3, initial_force=55.0, seed=21, autoreset=1)
     rng = np.random.default_rng(5)
     K = (exact_gains()[None] * rng.uniform(0.0, 1.5, (B, 1, 1, 8))).astype(np.float32)
     gpu.enable_lqr(torch.from_numpy(K), per_env=True, done_pos=0.02, done_angle=0.02)
+    assert gpu.kernel_shape() == tuple(shape)   # the requested shapes survive cp_set_lqr
     orc.set_lqr(K, per_env=True, state8=True, done_pos=0.02, done_angle=0.02)
     _assert_same(_np(gpu.reset()), orc.reset(), "reset obs")
     n_done = 0
@@ -39,10 +41,11 @@ def test_per_env_gains_autoreset_bounds(oracle_mod):
     assert n_done > 0      # the bounds termination fired somewhere
 
 
+@shapes
 @pytest.mark.parametrize("R,S", [(2, 2), (1, 1)])
-def test_exact_gains_discrete(oracle_mod, R, S):
+def test_exact_gains_discrete(oracle_mod, R, S, shape):
     B = 64
-    gpu, orc = _pair(oracle_mod, num_envs=B, action_repeats=R, steps_per_repeat=S, initial_force=55.0, seed=8)
+    gpu, orc = _pair(oracle_mod, shape, num_envs=B, action_repeats=R, steps_per_repeat=S, initial_force=55.0, seed=8)
     gpu.enable_lqr(torch.from_numpy(exact_gains()))
     orc.set_lqr(exact_gains(), state8=True)
     _assert_same(_np(gpu.reset()), orc.reset(), "reset obs")

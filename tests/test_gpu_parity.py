@@ -2,8 +2,11 @@
 
 The kernel and the fp32 oracle perform the same fp32 operations in the same order
 (explicit fma, -ffp-contract=off on both sides, own transcendentals), so the bar is
-bit-exact equality of obs / reward / done / full state.  Full-size (B = 65,536)
-runs are checked on a random subset of envs plus size-independent properties.
+bit-exact equality (raw bits: a signed-zero difference fails) of obs / reward / done /
+full state.  Every case runs on both register budgets of the step and autoreset kernels
+(SHAPES: cp_set_kernel_shape), so the throughput shape that bench.py times at 65,536 envs
+is under the same bar as the latency shape small batches pick by default.  Full-size
+(B = 65,536) runs are checked on a random subset of envs plus size-independent properties.
 """
 import argparse
 import ctypes as C
@@ -18,9 +21,19 @@ from cartpoleplusplus_amd.batched import BatchedCartpole
 pytestmark = pytest.mark.gpu
 
 
-def _pair(O, **kw):
+# (step kernel shape, autoreset kernel shape): every combination the library can run
+SHAPES = [("throughput", "throughput"), ("latency", "latency"), ("throughput", "latency"),
+          ("latency", "throughput")]
+SHAPE_IDS = ["tp-tp", "lat-lat", "tp-lat", "lat-tp"]
+shapes = pytest.mark.parametrize("shape", SHAPES, ids=SHAPE_IDS)
+
+
+def _pair(O, shape=None, **kw):
     cfg = native.default_config(**kw)
     gpu = BatchedCartpole(cfg.num_envs, 0, config=abi.cp_config.from_buffer_copy(cfg))
+    if shape is not None:
+        gpu.set_kernel_shape(*shape)
+        assert gpu.kernel_shape() == tuple(shape)
     orc = O.Envs(abi.cp_config.from_buffer_copy(cfg))
     return gpu, orc
 
@@ -30,28 +43,37 @@ def _np(t):
 
 
 def _assert_same(a, b, what):
+    """Bit-exact: float32 arrays are compared as their uint32 bits (-0.0 != +0.0, NaN bits)."""
     a, b = np.asarray(a), np.asarray(b)
-    if not np.array_equal(a, b, equal_nan=True):
+    if a.dtype == np.float32 and b.dtype == np.float32:
+        same = np.array_equal(np.ascontiguousarray(a).view(np.uint32), np.ascontiguousarray(b).view(np.uint32))
+    else:
+        same = np.array_equal(a, b, equal_nan=True)
+    if not same:
         d = np.abs(a.astype(np.float64) - b.astype(np.float64))
         idx = np.unravel_index(np.nanargmax(d), d.shape)
-        raise AssertionError(f"{what}: {np.count_nonzero(d)} elements differ, max |diff| {np.nanmax(d):.3e} at {idx}")
+        nbits = np.count_nonzero(np.ascontiguousarray(a).view(np.uint32) != np.ascontiguousarray(b).view(np.uint32)) \
+            if a.dtype == b.dtype == np.float32 else np.count_nonzero(d)
+        raise AssertionError(f"{what}: {nbits} elements differ, max |diff| {np.nanmax(d):.3e} at {idx}")
 
 
 def _compare_state(gpu, orc, what):
     _assert_same(_np(gpu.get_state()), orc.get_state(), what + " state")
 
 
-def test_reset_philox_bitexact(oracle_mod):
-    gpu, orc = _pair(oracle_mod, num_envs=200, action_repeats=3, initial_force=55.0, seed=1234)
+@shapes
+def test_reset_philox_bitexact(oracle_mod, shape):
+    gpu, orc = _pair(oracle_mod, shape, num_envs=200, action_repeats=3, initial_force=55.0, seed=1234)
     _assert_same(_np(gpu.reset()), orc.reset(), "reset obs")
     _compare_state(gpu, orc, "reset")
     _assert_same(_np(gpu.overflow_counts()), np.zeros(200, np.int32), "overflow")
 
 
+@shapes
 @pytest.mark.parametrize("R,S", [(3, 1), (2, 1), (3, 4)])
-def test_continuous_random_actions_200_steps(oracle_mod, R, S):
+def test_continuous_random_actions_200_steps(oracle_mod, R, S, shape):
     B = 96
-    gpu, orc = _pair(oracle_mod, num_envs=B, action_repeats=R, steps_per_repeat=S, initial_force=55.0, seed=7)
+    gpu, orc = _pair(oracle_mod, shape, num_envs=B, action_repeats=R, steps_per_repeat=S, initial_force=55.0, seed=7)
     _assert_same(_np(gpu.reset()), orc.reset(), "reset obs")
     rng = np.random.default_rng(123)
     for t in range(200):
@@ -65,9 +87,10 @@ def test_continuous_random_actions_200_steps(oracle_mod, R, S):
     assert _np(gd).all()   # max_episode_len = 200
 
 
-def test_discrete_autoreset_bounds(oracle_mod):
+@shapes
+def test_discrete_autoreset_bounds(oracle_mod, shape):
     B = 130
-    gpu, orc = _pair(oracle_mod, num_envs=B, action_repeats=3, initial_force=55.0, seed=99, autoreset=1,
+    gpu, orc = _pair(oracle_mod, shape, num_envs=B, action_repeats=3, initial_force=55.0, seed=99, autoreset=1,
                      done_on_bounds=1, max_episode_len=40)
     _assert_same(_np(gpu.reset()), orc.reset(), "reset")
     rng = np.random.default_rng(5)
@@ -87,9 +110,10 @@ def test_discrete_autoreset_bounds(oracle_mod):
     assert (orl > 0).all() and (orl <= 40).all()
 
 
-def test_host_bump_mode(oracle_mod):
+@shapes
+def test_host_bump_mode(oracle_mod, shape):
     B = 33
-    gpu, orc = _pair(oracle_mod, num_envs=B, action_repeats=2, bump_mode=abi.CP_BUMP_HOST)
+    gpu, orc = _pair(oracle_mod, shape, num_envs=B, action_repeats=2, bump_mode=abi.CP_BUMP_HOST)
     rng = np.random.default_rng(0)
     f = rng.uniform(-200, 200, (B, 30, 2, 2)).astype(np.float32)
     gpu.set_bump_forces(torch.from_numpy(f).cuda())
@@ -102,10 +126,11 @@ def test_host_bump_mode(oracle_mod):
         _assert_same(_np(go), oo, f"obs step {t}")
 
 
+@shapes
 @pytest.mark.parametrize("bug", [True, False])
-def test_readback_12_state(oracle_mod, bug):
+def test_readback_12_state(oracle_mod, bug, shape):
     B, R, S = 40, 3, 2
-    gpu, orc = _pair(oracle_mod, num_envs=B, action_repeats=R, steps_per_repeat=S, initial_force=55.0, seed=3)
+    gpu, orc = _pair(oracle_mod, shape, num_envs=B, action_repeats=R, steps_per_repeat=S, initial_force=55.0, seed=3)
     gpu.enable_readback(True, reference_bug=bug)
     gpu.reset()
     orc.reset()
@@ -120,9 +145,10 @@ def test_readback_12_state(oracle_mod, bug):
         assert np.array_equal(r[:, 1, :, :, 2:4], r[:, 0, :, :, 2:4])
 
 
-def test_step_after_done_and_mask_reset(oracle_mod):
+@shapes
+def test_step_after_done_and_mask_reset(oracle_mod, shape):
     B = 64
-    gpu, orc = _pair(oracle_mod, num_envs=B, action_repeats=2, max_episode_len=3, seed=11, initial_force=55.0)
+    gpu, orc = _pair(oracle_mod, shape, num_envs=B, action_repeats=2, max_episode_len=3, seed=11, initial_force=55.0)
     gpu.reset()
     orc.reset()
     a = np.zeros((B, 2, 2), np.float32)
@@ -143,15 +169,17 @@ def test_step_after_done_and_mask_reset(oracle_mod):
     _compare_state(gpu, orc, "masked reset")
 
 
-def test_state_roundtrip_into_oracle(oracle_mod):
+@shapes
+def test_state_roundtrip_into_oracle(oracle_mod, shape):
     B = 50
-    gpu, orc = _pair(oracle_mod, num_envs=B, action_repeats=3, initial_force=200.0, seed=5)
+    gpu, orc = _pair(oracle_mod, shape, num_envs=B, action_repeats=3, initial_force=200.0, seed=5)
     gpu.reset()
     rng = np.random.default_rng(2)
     for _ in range(20):
         gpu.step(torch.from_numpy(rng.uniform(-1, 1, (B, 2, 2)).astype(np.float32)).cuda())
     orc.set_state(_np(gpu.get_state()))
     gpu2 = BatchedCartpole(B, 0, config=abi.cp_config.from_buffer_copy(gpu.cfg))
+    gpu2.set_kernel_shape(*shape[::-1])   # the copy runs the other shapes
     gpu2.set_state(gpu.get_state())
     for t in range(10):
         a = rng.uniform(-1, 1, (B, 2, 2)).astype(np.float32)
@@ -160,6 +188,70 @@ def test_state_roundtrip_into_oracle(oracle_mod):
         oo, _, _ = orc.step(a)
         _assert_same(_np(g1), oo, f"obs {t}")
         _assert_same(_np(g2), oo, f"obs (set_state copy) {t}")
+
+
+@shapes
+def test_cross_island_contact_merged_solve(oracle_mod, shape):
+    """The merged path: cart2 + pole2 placed against cart + pole (gap 0-3 cm, yaw up to
+    0.6 rad, y offset up to 15 cm) and the carts pushed into each other, then random pushes.
+    The cross pairs 5-8 touch, so the oracle solves those envs merged (one group, pair order
+    0 2 1 3 4 9 5 6 7 8; DPP whole-env view in the kernels, cp_physics.h cross_view), and the
+    GPU must stay bit-exact through it on both kernel shapes."""
+    B = 96
+    gpu, orc = _pair(oracle_mod, shape, num_envs=B, action_repeats=3, initial_force=0.0, seed=3)
+    gpu.reset()
+    orc.reset()
+    st = orc.get_state()
+    _assert_same(_np(gpu.get_state()), st, "reset state")
+    rng = np.random.default_rng(17)
+    gap = rng.uniform(0.0, 0.03, B)
+    yaw = rng.uniform(-0.6, 0.6, B)
+    dy = rng.uniform(-0.15, 0.15, B)
+    for d in (2, 3):                                   # cart2, pole2
+        st[abi.CP_SF_BODY(d, 0)] = (0.2 + gap).astype(np.float32)
+        st[abi.CP_SF_BODY(d, 1)] = dy.astype(np.float32)
+        st[abi.CP_SF_BODY(d, 5)] = np.sin(0.5 * yaw).astype(np.float32)
+        st[abi.CP_SF_BODY(d, 6)] = np.cos(0.5 * yaw).astype(np.float32)
+    orc.set_state(st)
+    gpu.set_state(torch.from_numpy(st).cuda())
+    merged = np.zeros(B, np.int64)
+    for t in range(80):
+        if t < 40:                                     # cart +x, cart2 -x (discrete table 2 / 1)
+            a = np.tile(np.array([2, 1], np.int8), (B, 1))
+        else:
+            a = rng.integers(0, 5, (B, 2)).astype(np.int8)
+        go, gr, gd = gpu.step(torch.from_numpy(a).cuda())
+        oo, orw, od = orc.step(a)
+        merged += orc.merged()
+        _assert_same(_np(go), oo, f"obs step {t}")
+        _assert_same(_np(gd), od, f"done step {t}")
+    _compare_state(gpu, orc, "after the merged rollout")
+    assert (merged > 0).sum() >= B * 3 // 4, f"only {(merged > 0).sum()} envs ran a merged solve"
+    assert merged.sum() >= 30 * B
+
+
+def test_full_size_c2_200_steps(oracle_mod):
+    """BASELINE configs[1] (C2) at its full size: 4,096 envs, continuous U[-1,1] actions (bench.py's
+    hashed stream), R = 3, F_init 55, seed 1234, 200 steps from reset on the kernel shapes bench.py
+    times at this size (cp_create's choice), every env bit-exact against the oracle."""
+    import os
+
+    import bench
+    B = 4096
+    gpu, orc = _pair(oracle_mod, None, num_envs=B, action_repeats=3, initial_force=55.0, seed=bench.SEED)
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    _assert_same(_np(gpu.reset()), orc.reset(), "reset obs")
+    acts = bench.make_actions(True, B, 0, 200, bench.SEED, gpu.device)
+    rew = np.zeros(B, np.float32)
+    done = np.zeros(B, np.uint8)
+    for t in range(200):
+        go, gr, gd = gpu.step(acts[t])
+        oo = np.zeros((B, 3, 2, 7), np.float32)
+        orc.step_omp(np.ascontiguousarray(_np(acts[t])), abi.CP_ACTION_CONTINUOUS, oo, rew, done, threads)
+        _assert_same(_np(go), oo, f"obs step {t}")
+        _assert_same(_np(gd), done, f"done step {t}")
+    _compare_state(gpu, orc, "C2 after 200 steps")
+    assert done.all()
 
 
 def test_full_size_bench_config_subset_parity_and_properties(oracle_mod):
@@ -174,6 +266,7 @@ def test_full_size_bench_config_subset_parity_and_properties(oracle_mod):
     cfg = native.default_config(num_envs=B, action_repeats=3, initial_force=55.0, seed=1234, autoreset=1)
     g1 = BatchedCartpole(B, 0, config=abi.cp_config.from_buffer_copy(cfg))
     g2 = BatchedCartpole(B, 0, config=abi.cp_config.from_buffer_copy(cfg))
+    assert g1.kernel_shape() == ("throughput", "throughput")   # what bench.py times at C3
     g1.reset()
     g2.reset()
     gen = torch.Generator(device="cuda").manual_seed(1234)

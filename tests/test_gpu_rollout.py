@@ -1,0 +1,112 @@
+"""cp_rollout (K env-steps in one launch, per-lane step/reset state machine, cp_env.h) against
+K cp_step calls on a second handle and against the oracle: obs, reward, done, terminal obs of
+every step, episode returns and the final state SoA, bit for bit, on both kernel shapes.
+Episodes end at different steps (bounds termination, short max_episode_len), so lanes of one
+wave are in different phases (step / reset) in the same substep trip."""
+import numpy as np
+import pytest
+import torch
+
+from cartpoleplusplus_amd import abi, native
+from cartpoleplusplus_amd.batched import BatchedCartpole
+from cartpoleplusplus_amd.lqr import exact_gains
+from tests.test_gpu_parity import _assert_same, _np, shapes
+
+pytestmark = pytest.mark.gpu
+
+
+def _handles(shape, **kw):
+    cfg = native.default_config(**kw)
+    hs = []
+    for _ in range(2):
+        h = BatchedCartpole(cfg.num_envs, 0, config=abi.cp_config.from_buffer_copy(cfg))
+        h.set_kernel_shape(*shape)
+        hs.append(h)
+    return cfg, hs
+
+
+def _stepwise(env, actions):
+    obs, rew, done, term = [], [], [], []
+    for k in range(actions.shape[0]):
+        o, r, d = env.step(actions[k])
+        obs.append(o.clone())
+        rew.append(r.clone())
+        done.append(d.clone())
+        term.append(env.terminal_obs.clone() if env.terminal_obs is not None else None)
+    return torch.stack(obs), torch.stack(rew), torch.stack(done), term
+
+
+def _compare(roll, step_env, actions, what):
+    ro, rr, rd = roll.rollout(actions)
+    so, sr, sd, st = _stepwise(step_env, actions)
+    _assert_same(_np(rd), _np(sd), what + " done")
+    _assert_same(_np(rr), _np(sr), what + " reward")
+    _assert_same(_np(ro), _np(so), what + " obs")
+    if roll.rollout_terminal_obs is not None:
+        d = _np(sd).astype(bool)
+        for k in range(actions.shape[0]):
+            _assert_same(_np(roll.rollout_terminal_obs[k])[d[k]], _np(st[k])[d[k]], f"{what} terminal obs step {k}")
+    _assert_same(_np(roll.get_state()), _np(step_env.get_state()), what + " state")
+    _assert_same(_np(roll.episode_returns()[0]), _np(step_env.episode_returns()[0]), what + " returns")
+    _assert_same(_np(roll.episode_returns()[1]), _np(step_env.episode_returns()[1]), what + " lengths")
+    return _np(rd)
+
+
+@shapes
+def test_rollout_equals_steps_discrete_bounds_autoreset(shape):
+    B, K = 192, 90
+    _, (roll, step_env) = _handles(shape, num_envs=B, action_repeats=3, initial_force=55.0, seed=31, autoreset=1,
+                                   done_on_bounds=1, max_episode_len=35)
+    roll.reset()
+    step_env.reset()
+    g = torch.Generator(device="cuda").manual_seed(5)
+    acts = torch.randint(0, 5, (K, B, 2), device="cuda", generator=g, dtype=torch.int8)
+    d = _compare(roll, step_env, acts, "discrete")
+    assert d.sum() > B and len({int(k) for k in np.nonzero(d)[0]}) > 10   # resets spread over many steps
+    # a second rollout continues where the first ended
+    acts2 = torch.randint(0, 5, (17, B, 2), device="cuda", generator=g, dtype=torch.int8)
+    _compare(roll, step_env, acts2, "discrete, second rollout")
+
+
+@shapes
+def test_rollout_continuous_vs_oracle(oracle_mod, shape):
+    B, K = 96, 60
+    cfg, (roll, _) = _handles(shape, num_envs=B, action_repeats=2, steps_per_repeat=2, initial_force=55.0, seed=4,
+                              autoreset=1, max_episode_len=25)
+    orc = oracle_mod.Envs(abi.cp_config.from_buffer_copy(cfg))
+    _assert_same(_np(roll.reset()), orc.reset(), "reset")
+    rng = np.random.default_rng(3)
+    a = rng.uniform(-1, 1, (K, B, 2, 2)).astype(np.float32)
+    go, gr, gd = roll.rollout(torch.from_numpy(a).cuda())
+    for k in range(K):
+        oo, orw, od, ot = orc.step(a[k], terminal=True)
+        _assert_same(_np(go[k]), oo, f"obs step {k}")
+        _assert_same(_np(gd[k]), od, f"done step {k}")
+        dk = od.astype(bool)
+        _assert_same(_np(roll.rollout_terminal_obs[k])[dk], ot[dk], f"terminal obs step {k}")
+    _assert_same(_np(roll.get_state()), orc.get_state(), "final state")
+
+
+@shapes
+def test_rollout_lqr_policy_and_step_after_done(shape):
+    B, K = 64, 30
+    _, (roll, step_env) = _handles(shape, num_envs=B, action_repeats=2, initial_force=55.0, seed=12,
+                                   max_episode_len=12)
+    for env in (roll, step_env):
+        env.enable_lqr(torch.from_numpy(exact_gains()), state8=False)
+        env.reset()
+    a = torch.zeros((K, B, 2, 2), device="cuda")
+    d = _compare(roll, step_env, a, "lqr, no autoreset")
+    assert d[12:].all() and not d[:11].any()     # steps after done return the last obs, done 1
+
+
+def test_rollout_rejects_side_outputs():
+    env = BatchedCartpole(16, 0, action_repeats=2)
+    env.reset()
+    env.enable_readback(True)
+    with pytest.raises(native.CartpoleError):
+        env.rollout(torch.zeros((3, 16, 2), dtype=torch.int8, device="cuda"))
+    env.enable_readback(False)
+    o, r, d = env.rollout(torch.zeros((3, 16, 2), dtype=torch.int8, device="cuda"))
+    assert o.shape == (3, 16, 2, 2, 7) and torch.isfinite(o).all()
+    assert env.lib.cp_rollout(env.h, 0, o.data_ptr(), 1, o.data_ptr(), r.data_ptr(), d.data_ptr(), None, None) != 0
