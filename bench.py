@@ -305,6 +305,38 @@ def cpu_baseline(R, budget_s):
             "pybullet": "not importable (SURVEY.md §8c): the reference's own CPU path cannot be timed here"}
 
 
+def gym_mirror_rate(steps=400):
+    """The reference's own surface (BulletCartpole, B = 1, R = 2, discrete, numpy in / numpy copy
+    out per step, the step replayed as a hipGraph) on this GPU, for comparison with the CPU
+    path's C1 rate: a B = 1 step is latency-bound (2 substeps of one wave)."""
+    import argparse
+
+    import numpy as np
+
+    from cartpoleplusplus_amd import bullet_cartpole
+    p = argparse.ArgumentParser()
+    bullet_cartpole.add_opts(p)
+    opts = p.parse_args(["--initial-force", "55"])
+    env = bullet_cartpole.BulletCartpole(opts, discrete_actions=True)
+    rng = np.random.default_rng(0)
+    np.random.seed(0)
+    t0 = time.perf_counter()
+    env.reset()
+    t_reset = time.perf_counter() - t0
+    n, resets, t0 = 0, 0, time.perf_counter()
+    while n < steps:
+        _, _, done, _ = env.step(rng.integers(0, 5, 2))
+        n += 1
+        if done:
+            env.reset()
+            resets += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 1), "unit": "env-steps/s", "ms_per_step": round(dt / n * 1e3, 4),
+            "reset_ms": round(t_reset * 1e3, 2), "step_as_hipgraph": env.use_graph,
+            "sample": f"C1 config on the GPU: B=1, R=2, F_init 55, discrete random actions, {n} steps incl. "
+                      f"{resets} resets ({dt:.2f} s)"}
+
+
 def _pose_diffs(g, o):
     """per-step max over envs/repeats of |dpos| (xyz of cart + pole) and |dquat|."""
     import numpy as np
@@ -583,6 +615,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
         out["cpu_baseline"] = cpu_baseline(R, args.cpu_seconds)
+        out["cpu_baseline"]["gym_mirror_b1_gpu"] = gym_mirror_rate()
         if not args.no_parity:
             log("parity vs oracle ...")
             out["parity"] = parity_check(dev, R, shape)

@@ -10,7 +10,10 @@ Same surface as /root/reference/bullet_cartpole.py so the agents
   .render(mode, close), .seed(), .configure()  no-ops (:169-176)
   .monkey_positions / .monkey_velocities  12-state pole readback (:212-234)
 
-The env is one lane of the batched kernel (B = 1) on a GPU.  Bump forces are
+The env is one lane pair of the batched kernel (B = 1) on a GPU.  After the first step the
+step is a captured hipGraph (torch.cuda.CUDAGraph on ROCm): action H2D from a pinned host
+buffer, cp_step, obs + readback D2H into pinned host buffers, then one host sync; a
+launch-bound B = 1 step pays one graph launch instead of four API calls.  Bump forces are
 drawn from the global legacy `np.random` stream in the reference's order and with
 its formula (:354-359: theta = U * 2 * pi, f = F (cos, sin)), so a given
 `np.random.seed` produces the reference's pushes exactly (parity mode,
@@ -109,6 +112,13 @@ class BulletCartpole(Env):
             self._env.enable_raster(True, width=self.render_width, height=self.render_height,
                                     num_cameras=self.num_cameras)
         self._act = torch.zeros((1, 2, 2), dtype=torch.float32, device=self._env.device)
+        # pinned host staging for the graph-captured step (see _step_graph)
+        self._h_act = torch.zeros((1, 2, 2), dtype=torch.float32).pin_memory()
+        self._h_obs = torch.zeros((1, self.repeats, 2, 7), dtype=torch.float32).pin_memory()
+        self._h_rb = torch.zeros(abi.readback_shape(1, self.repeats, self.steps_per_repeat),
+                                 dtype=torch.float32).pin_memory()
+        self._graph = None
+        self.use_graph = not self.use_raw_pixels and not self.event_log
 
     def _capture(self, obs):
         # set_state_element_for_repeat (:298-311): pixels (float16 values, float32 state)
@@ -126,6 +136,31 @@ class BulletCartpole(Env):
 
     def render(self, mode, close):
         pass
+
+    def _step_eager(self, a):
+        self._act.copy_(torch.from_numpy(a).view(1, 2, 2))
+        obs, _, _ = self._env.step(self._act)
+        self._h_obs.copy_(obs)
+        self._h_rb.copy_(self._env.readback)
+
+    def _step_graph(self, a):
+        """One env step as a replay of the captured graph (H2D action, cp_step, D2H obs and
+        readback); the handle has no autoreset and no timing, so the launches are the same on
+        every call and capture once."""
+        self._h_act.numpy()[...] = a.reshape(1, 2, 2)
+        if self._graph is None:
+            self._graph = torch.cuda.CUDAGraph()
+            stream = torch.cuda.Stream(self._env.device)
+            stream.wait_stream(torch.cuda.current_stream(self._env.device))
+            with torch.cuda.stream(stream):
+                with torch.cuda.graph(self._graph, stream=stream):
+                    self._act.copy_(self._h_act, non_blocking=True)
+                    obs, _, _ = self._env.step(self._act)
+                    self._h_obs.copy_(obs, non_blocking=True)
+                    self._h_rb.copy_(self._env.readback, non_blocking=True)
+            torch.cuda.current_stream(self._env.device).wait_stream(stream)
+        self._graph.replay()
+        torch.cuda.current_stream(self._env.device).synchronize()
 
     def reset(self):
         self.steps = 0
@@ -152,12 +187,17 @@ class BulletCartpole(Env):
             fx, fy = action[0]
             fx2, fy2 = action[1]
             a = np.asarray([[fx, fy], [fx2, fy2]], np.float32)
-        self._act.copy_(torch.from_numpy(a).view(1, 2, 2))
-        obs, _, done = self._env.step(self._act)
+        if self.use_graph:
+            self._step_graph(a)
+        else:
+            self._step_eager(a)
         if self.delay > 0:
             time.sleep(self.delay * self.repeats * self.steps_per_repeat)
-        self._capture(obs)
-        rb = self._env.readback[0].cpu().numpy()     # (2, R, S, 4, 3)
+        if self.use_raw_pixels:
+            self._capture(None)
+        else:
+            self.state[...] = self._h_obs.numpy()[0]
+        rb = self._h_rb.numpy()[0]     # (2, R, S, 4, 3)
         self.monkey_positions = np.ascontiguousarray(rb[:, :, :, 0:2, :]).astype(np.float64)
         self.monkey_velocities = np.ascontiguousarray(rb[:, :, :, 2:4, :]).astype(np.float64)
         self.steps += 1

@@ -504,6 +504,15 @@ CP_DEV void action_forces(const void* actions, size_t row, real F, real f[4]) {
 // the step kernel's (the reset kernel's C44 / ALLIN options compute the same numbers).  The
 // episode counters live in registers for the whole launch (both lanes of a pair hold identical
 // copies: no cross-lane memory traffic) and are written back once at the end.
+// The state machine's cold per-lane values (step index, substep, counters, flags, LQR forces)
+// are kept in the lane's column of the scratch SoA between substeps (Mem::lx / sx: coalesced,
+// L2-resident, each lane reads only its own writes) rather than in registers across the
+// substep, whose peak register pressure they would add to; the action forces are re-read
+// from the action array after each substep.
+enum : int { RC_K = 0, RC_SUB, RC_STEPS, RC_EPISODE, RC_FLAGS, RC_RET, RC_U0, RC_U1, RC_U2, RC_U3, RC_FIELDS };
+enum : uint32_t { RF_DONE = 1u, RF_RESETTING = 2u, RF_LAST_SIM = 4u, RF_LQR_DONE = 8u };
+static_assert(RC_FIELDS <= 4 * CP_ISLAND_PAIRS, "rollout state must fit the scratch SoA's per-lane fields");
+
 template <int KIND, bool LQR, bool LAT>
 __global__ void __launch_bounds__(WAVE)
 __attribute__((amdgpu_waves_per_eu(LAT ? 1 : CP_WAVES_PER_EU, LAT ? 1 : CP_WAVES_PER_EU)))
@@ -522,59 +531,68 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
     const Mem G = Mem::make(b.state, b.scratch, B, i, isl);
     const Lane L = Lane::make(isl, cfg.phys);
     const SoaF term = SoaF::make(b.term_obs, B, R * 14);
-    const uint32_t toff = SoaF::eoff(i);
     const size_t obs_step = (size_t)B * R * 14;
+    // the env index through an opaque register copy wherever the loop body forms an address: the
+    // 64-bit per-lane addresses are otherwise hoisted out of the substep loop and spilled
+    auto env = [&]() { uint32_t v = (uint32_t)i; asm volatile("" : "+v"(v)); return (size_t)v; };
+    auto ldc = [&](int f) { return (int)to_bits(G.lx(f)); };
+    auto stc = [&](int f, int v) { G.sx(f, bits_to<real>((uint32_t)v)); };
+    auto ldu = [&](int f) { return G.lx(f); };
     Stamps ST;
     Sim S;
     load_sim(S, G.st, G.off);
-    int steps = ldi(G.st, CP_SF_STEPS, G.off);
-    int episode = ldi(G.st, CP_SF_EPISODE, G.off);
-    bool done_flag = ldi(G.st, CP_SF_DONE, G.off) != 0;
-    float ret_acc = b.ret_acc[i];
     int ov = 0;
-    int k = 0, sub = 0;
-    bool resetting = false, lqr_done = false, last_sim = false;
-    real f[4];
-    real u[2][2] = {{real(0.0), real(0.0)}, {real(0.0), real(0.0)}};
-    const float* Kg = nullptr;
-    if constexpr (LQR) Kg = lq.gains + (lq.per_env ? (size_t)i * 32 : 0);
+    real u[2][2];
     // the next simulated step from k on: steps of an env that is done before them only return its
-    // last obs, reward 0, done 1 (:179-181); false when the K steps are over
-    auto begin_step = [&]() -> bool {
-        for (; k < K && done_flag; ++k) {
-            last_sim = false;
+    // last obs, reward 0, done 1 (:179-181); writes the cold state; false when the K steps are over
+    auto begin_step = [&](int k, int steps, int episode, uint32_t flags, float ret_acc) -> bool {
+        for (; k < K && (flags & RF_DONE); ++k) {
+            flags &= ~RF_LAST_SIM;
             if (lead) {
-                float* o = obs_out + (size_t)k * obs_step + (size_t)i * R * 14;
-                for (int q = 0; q < R * 14; ++q) o[q] = term.ld(q, toff);
-                reward_out[(size_t)k * B + i] = 0.0f;
-                done_out[(size_t)k * B + i] = 1;
+                const size_t e = env();
+                float* o = obs_out + (size_t)k * obs_step + e * R * 14;
+                for (int q = 0; q < R * 14; ++q) o[q] = term.ld(q, SoaF::eoff((int)e));
+                reward_out[(size_t)k * B + e] = 0.0f;
+                done_out[(size_t)k * B + e] = 1;
             }
         }
-        if (k >= K) return false;
-        last_sim = true;
-        action_forces<KIND>(actions, (size_t)k * B + i, real(cfg.action_force), f);
-        if constexpr (LQR) {
-            lqr_done = false;
-            lqr_observe(S, cfg, lq, Kg, u, nullptr);
+        const bool more = k < K;
+        if (more) {
+            flags |= RF_LAST_SIM;
+            if constexpr (LQR) {
+                flags &= ~RF_LQR_DONE;
+                lqr_observe(S, cfg, lq, lq.gains + (lq.per_env ? (size_t)i * 32 : 0), u, nullptr);
+                G.sx(RC_U0, u[0][0]); G.sx(RC_U1, u[0][1]); G.sx(RC_U2, u[1][0]); G.sx(RC_U3, u[1][1]);
+            }
         }
-        sub = 0;
-        return true;
+        stc(RC_K, k); stc(RC_SUB, 0); stc(RC_STEPS, steps); stc(RC_EPISODE, episode); stc(RC_FLAGS, (int)flags);
+        G.sx(RC_RET, bits_to<real>(__float_as_uint(ret_acc)));
+        return more;
     };
-    bool work = begin_step();
+    bool work = begin_step(0, ldi(G.st, CP_SF_STEPS, G.off), ldi(G.st, CP_SF_EPISODE, G.off),
+                           ldi(G.st, CP_SF_DONE, G.off) != 0 ? RF_DONE : 0u, b.ret_acc[i]);
     while (__ballot(work) != 0ull) {
         if (!work) continue;
         substep<LAT && !kF64, false, kAllinStep>(S, cfg.phys, L, pool, pool0, ov, G, ST);
-        if (!resetting) {
+        int k = ldc(RC_K), sub = ldc(RC_SUB);
+        uint32_t flags = (uint32_t)ldc(RC_FLAGS);
+        if (!(flags & RF_RESETTING)) {
+            real f[4];
+            const size_t e = env();
+            action_forces<KIND>(actions, (size_t)k * B + e, real(cfg.action_force), f);
             if constexpr (LQR) {
+                u[0][0] = ldu(RC_U0); u[0][1] = ldu(RC_U1); u[1][0] = ldu(RC_U2); u[1][1] = ldu(RC_U3);
                 apply_force_link<0>(S, f[0] + u[0][0], f[1] + u[0][1]);
                 apply_force_link<1>(S, f[2] + u[1][0], f[3] + u[1][1]);
-                lqr_done |= lqr_observe(S, cfg, lq, Kg, u, nullptr);
+                if (lqr_observe(S, cfg, lq, lq.gains + (lq.per_env ? (size_t)i * 32 : 0), u, nullptr))
+                    flags |= RF_LQR_DONE;
+                G.sx(RC_U0, u[0][0]); G.sx(RC_U1, u[0][1]); G.sx(RC_U2, u[1][0]); G.sx(RC_U3, u[1][1]);
             } else {
                 apply_force_link<0>(S, f[0], f[1]);
                 apply_force_link<1>(S, f[2], f[3]);
             }
             ++sub;
-            float* obs = obs_out + (size_t)k * obs_step + (size_t)i * R * 14;
+            float* obs = obs_out + (size_t)k * obs_step + e * R * 14;
             if (lead && sub % SR == 0) {
                 float row[14];
                 write_obs_row(S, row);
@@ -582,30 +600,32 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
 #pragma unroll
                 for (int q = 0; q < 14; ++q) obs[r * 14 + q] = row[q];
             }
-            if (sub < RS) continue;
+            if (sub < RS) {
+                stc(RC_SUB, sub);
+                if (LQR) stc(RC_FLAGS, (int)flags);
+                continue;
+            }
             // step end (the step kernel's epilogue)
-            steps += 1;
+            const int steps = ldc(RC_STEPS) + 1;
+            const int episode = ldc(RC_EPISODE);
             bool done = steps >= cfg.max_episode_len;
             if (cfg.done_on_bounds && bounds_exceeded(S, cfg)) done = true;
-            if (LQR && lqr_done) done = true;
-            const float ret = ret_acc + 1.0f;
+            if (LQR && (flags & RF_LQR_DONE)) done = true;
+            const float ret = __uint_as_float(to_bits(G.lx(RC_RET))) + 1.0f;
             if (lead) {
-                reward_out[(size_t)k * B + i] = 1.0f;
-                done_out[(size_t)k * B + i] = done ? 1 : 0;
+                reward_out[(size_t)k * B + e] = 1.0f;
+                done_out[(size_t)k * B + e] = done ? 1 : 0;
             }
             if (done) {
                 if (lead) {
-                    b.last_ret[i] = ret;
-                    b.last_len[i] = steps;
-                    for (int q = 0; q < R * 14; ++q) term.st(q, toff, obs[q]);
+                    b.last_ret[e] = ret;
+                    b.last_len[e] = steps;
+                    for (int q = 0; q < R * 14; ++q) term.st(q, SoaF::eoff((int)e), obs[q]);
                     if (term_out)
-                        for (int q = 0; q < R * 14; ++q) term_out[(size_t)k * obs_step + (size_t)i * R * 14 + q] = obs[q];
+                        for (int q = 0; q < R * 14; ++q) term_out[(size_t)k * obs_step + e * R * 14 + q] = obs[q];
                 }
-                ret_acc = 0.0f;
-                done_flag = true;
+                flags |= RF_DONE;
                 if (cfg.autoreset) {  // the reset kernel's prologue: pending forces survive
-                    resetting = true;
-                    sub = 0;
 #pragma unroll
                     for (int d = 0; d < CP_NUM_DYN; ++d) {
                         S.b[d].x = mk(cfg.phys.spawn_pos[d + 1][0], cfg.phys.spawn_pos[d + 1][1],
@@ -621,48 +641,50 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
 #pragma unroll
                         for (int q = 0; q < 4; ++q) G.sl(CP_SF_WS_LAM(0, j, q), real(0.0));
                     }
+                    stc(RC_SUB, 0);
+                    stc(RC_STEPS, steps);
+                    stc(RC_FLAGS, (int)(flags | RF_RESETTING));
+                    G.sx(RC_RET, bits_to<real>(__float_as_uint(0.0f)));
                     continue;
                 }
-            } else {
-                ret_acc = ret;
             }
-            ++k;
-            work = begin_step();
+            work = begin_step(k + 1, steps, episode, flags, done ? 0.0f : ret);
         } else {
             const int kb = sub - cfg.settle_steps;
             if (kb >= 0) {
+                const int episode = ldc(RC_EPISODE);
                 real fx, fy;
-                bump_force(cfg, b.bumps, i, episode, kb, 0, fx, fy);
+                const int e = (int)env();
+                bump_force(cfg, b.bumps, e, episode, kb, 0, fx, fy);
                 apply_force_link<0>(S, fx, fy);
-                bump_force(cfg, b.bumps, i, episode, kb, 1, fx, fy);
+                bump_force(cfg, b.bumps, e, episode, kb, 1, fx, fy);
                 apply_force_link<1>(S, fx, fy);
             }
-            if (++sub < nreset) continue;
+            if (++sub < nreset) {
+                stc(RC_SUB, sub);
+                continue;
+            }
             // reset end (the reset kernel's epilogue): every repeat slot shows the new pose
             if (lead) {
                 float row[14];
                 write_obs_row(S, row);
-                float* o = obs_out + (size_t)k * obs_step + (size_t)i * R * 14;
+                float* o = obs_out + (size_t)k * obs_step + env() * R * 14;
                 for (int r = 0; r < R; ++r)
 #pragma unroll
                     for (int q = 0; q < 14; ++q) o[r * 14 + q] = row[q];
             }
-            resetting = false;
-            steps = 0;
-            done_flag = false;
-            episode += 1;
-            ++k;
-            work = begin_step();
+            work = begin_step(k + 1, 0, ldc(RC_EPISODE) + 1, flags & ~(RF_DONE | RF_RESETTING), 0.0f);
         }
     }
     ov += (int)partner_u((uint32_t)ov);  // both lanes of every pair are here
     if (!lead) return;
+    const uint32_t flags = (uint32_t)ldc(RC_FLAGS);
     store_sim(S, G.st, G.off);
-    sti(G.st, CP_SF_STEPS, G.off, steps);
-    sti(G.st, CP_SF_EPISODE, G.off, episode);
-    sti(G.st, CP_SF_DONE, G.off, done_flag ? 1 : 0);
-    b.ret_acc[i] = ret_acc;
-    b.stepped[i] = last_sim ? 1 : 0;  // step K-1's value, as after the K-th cp_step
+    sti(G.st, CP_SF_STEPS, G.off, ldc(RC_STEPS));
+    sti(G.st, CP_SF_EPISODE, G.off, ldc(RC_EPISODE));
+    sti(G.st, CP_SF_DONE, G.off, (flags & RF_DONE) ? 1 : 0);
+    b.ret_acc[i] = __uint_as_float(to_bits(G.lx(RC_RET)));
+    b.stepped[i] = (flags & RF_LAST_SIM) ? 1 : 0;  // step K-1's value, as after the K-th cp_step
     if (ov) b.overflow[i] += ov;
 }
 

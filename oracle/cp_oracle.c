@@ -341,6 +341,12 @@ static const int PAIR_B[CP_NUM_PAIRS] = {1, 2, 3, 4, 2, 3, 4, 3, 4, 4};
 static const int ISLAND_PAIR[CP_NUM_ISLANDS][CP_ISLAND_PAIRS] = {{0, 1, 4, 5, 6}, {2, 3, 9, 7, 8}};
 
 /* --------------------------------------------------------------- simulation */
+/* CP_MODEL_PERSISTENT: one pair's persistent contact manifold, Bullet's btPersistentManifold
+ * restated (oracle only): up to 4 cached points, each with its local points on A and B
+ * (m_localPointA/B), its normal (stored A -> B here; Bullet keeps m_normalWorldOnB = -n), its
+ * separation m_distance1 and its applied normal impulse (the warm start). */
+typedef struct { int cnt; v3 la[4], lb[4], n[4]; real d[4], lam[4]; } pman_t;
+
 typedef struct {
     v3 x[CP_NUM_DYN];
     real q[CP_NUM_DYN][4];
@@ -350,11 +356,15 @@ typedef struct {
     real M[CP_NUM_DYN][6];
     uint32_t ws_id[CP_NUM_ISLANDS][CP_ISLAND_PAIRS];   /* warm-start cache (4 packed feature ids) */
     real ws_lam[CP_NUM_ISLANDS][CP_ISLAND_PAIRS][4];
+    pman_t pm[CP_NUM_ISLANDS][CP_ISLAND_PAIRS];        /* CP_MODEL_PERSISTENT only */
 } sim_t;
 
 typedef struct { v3 n; int cnt, base, fcnt, fbase; real mu; } manifold_t;
-typedef struct { v3 rb; real inv_eff, target, lam; int id; } point_t;
-typedef struct { real lam1, lam2, inv_eff1, inv_eff2; } fpoint_t;
+/* n: the row's normal (the manifold normal, or a cached point's own normal under
+ * CP_MODEL_PERSISTENT); pm: index of the cached point (CP_MODEL_PERSISTENT) */
+typedef struct { v3 rb, n; real inv_eff, target, lam; int id, pm; } point_t;
+/* t1, t2: the friction directions (btPlaneSpace1 of the normal, or velocity-dependent) */
+typedef struct { real lam1, lam2, inv_eff1, inv_eff2; v3 t1, t2; } fpoint_t;
 
 /* collision shape accessor: body g (0 = ground, static at the origin, identity axes) */
 typedef struct { v3 c; v3 ax[3]; real h[3]; } box_t;
@@ -718,7 +728,7 @@ static void sweep_normal(sim_t* S, const cp_physics* P, island_t* I, int isl, in
     manifold_t* m = &I->man[j];
     for (int k = 0; k < m->cnt; ++k) {
         point_t* q = &I->pt[m->base + k];
-        *bad |= solve_row(S, P, a, b, q->rb, m->n, q->inv_eff, q->target, &q->lam, 0, RC(0), tol);
+        *bad |= solve_row(S, P, a, b, q->rb, q->n, q->inv_eff, q->target, &q->lam, 0, RC(0), tol);
     }
 }
 static void sweep_friction(sim_t* S, const cp_physics* P, island_t* I, int isl, int j, real tol, int* bad) {
@@ -726,14 +736,12 @@ static void sweep_friction(sim_t* S, const cp_physics* P, island_t* I, int isl, 
     if (m->fcnt == 0) return;
     int g = ISLAND_PAIR[isl][j];
     int a = PAIR_A[g], b = PAIR_B[g];
-    v3 t1, t2;
-    plane_space(m->n, &t1, &t2);
     for (int k = 0; k < m->fcnt; ++k) {
         point_t* q = &I->pt[m->base + k];
         fpoint_t* f = &I->fp[m->fbase + k];
         real bound = m->mu * q->lam;
-        *bad |= solve_row(S, P, a, b, q->rb, t1, f->inv_eff1, RC(0), &f->lam1, 1, bound, tol);
-        *bad |= solve_row(S, P, a, b, q->rb, t2, f->inv_eff2, RC(0), &f->lam2, 1, bound, tol);
+        *bad |= solve_row(S, P, a, b, q->rb, f->t1, f->inv_eff1, RC(0), &f->lam1, 1, bound, tol);
+        *bad |= solve_row(S, P, a, b, q->rb, f->t2, f->inv_eff2, RC(0), &f->lam2, 1, bound, tol);
     }
 }
 static void warm_pair(sim_t* S, const cp_physics* P, island_t* I, int isl, int j) {
@@ -742,8 +750,123 @@ static void warm_pair(sim_t* S, const cp_physics* P, island_t* I, int isl, int j
     manifold_t* m = &I->man[j];
     for (int k = 0; k < m->cnt; ++k) {
         point_t* q = &I->pt[m->base + k];
-        apply_impulse(S, P, a, b, q->rb, m->n, q->lam);
+        apply_impulse(S, P, a, b, q->rb, q->n, q->lam);
     }
+}
+
+#ifdef ORC_DOUBLE
+#define ORC_SIMD_EPSILON 2.2204460492503131e-16   /* btScalar double: DBL_EPSILON */
+#else
+#define ORC_SIMD_EPSILON 1.1920928955078125e-07f  /* btScalar float: FLT_EPSILON */
+#endif
+
+/* world point of a box-local point and back (the ground box has identity axes at the origin) */
+static inline v3 box_to_world(const box_t* B, v3 l) { return add(B->c, rot(B->ax, l)); }
+static inline v3 box_to_local(const box_t* B, v3 w) { return rot_t(B->ax, sub(w, B->c)); }
+
+/* btPersistentManifold::sortCachedPoints (gContactCalcArea3Points, KEEP_DEEPEST_POINT): the
+ * cache slot the new point replaces when 4 points are cached -- never the deepest point, else
+ * the one whose removal leaves the largest area (in A's local frame); first maximum wins. */
+static int pm_sort_cached(const pman_t* M, v3 la, real d) {
+    int deepest = -1;
+    real maxpen = d;
+    for (int i = 0; i < 4; ++i)
+        if (M->d[i] < maxpen) { deepest = i; maxpen = M->d[i]; }
+    real res[4] = {RC(0), RC(0), RC(0), RC(0)};
+    static const int O[4][3] = {{1, 3, 2}, {0, 3, 2}, {0, 3, 1}, {0, 2, 1}};  /* a = new - [0]; b = [1] - [2] */
+    for (int i = 0; i < 4; ++i) {
+        if (i == deepest) continue;
+        v3 a0 = sub(la, M->la[O[i][0]]);
+        v3 b0 = sub(M->la[O[i][1]], M->la[O[i][2]]);
+        v3 c = cross(a0, b0);
+        res[i] = dot(c, c);
+    }
+    int best = -1;
+    real bv = -RC(1e30);
+    for (int i = 0; i < 4; ++i)
+        if (FABS(res[i]) > bv) { bv = FABS(res[i]); best = i; }
+    return best;
+}
+
+/* CP_MODEL_PERSISTENT: Bullet's box-box collision of one pair with a persistent manifold
+ * (btBoxBoxCollisionAlgorithm::processCollision with USE_PERSISTENT_CONTACTS):
+ *   1. new points from the box-box detector, which reports overlapping boxes only (dBoxBox2
+ *      returns nothing for a separating axis; penetrating candidates only): box_box at margin 0;
+ *   2. each new point (btManifoldResult::addContactPoint): getCacheEntry -- the cached point
+ *      nearest in A's local frame within the breaking threshold -- is replaced, keeping its
+ *      applied impulse (replaceContactPoint, MAINTAIN_PERSISTENCY); else the point is added, a
+ *      5th one replacing the slot sortCachedPoints picks;
+ *   3. refreshContactPoints: every cached point's world positions from its local points and the
+ *      current poses, its separation along its own normal; points separated by more than the
+ *      breaking threshold, or drifted sideways by more than it, are removed (last slot moved in).
+ * The breaking threshold is relative (btCollisionDispatcher's default
+ * CD_USE_RELATIVE_CONTACT_BREAKING_THRESHOLD): gContactBreakingThreshold (contact_margin, 0.02)
+ * times the smaller of the two shapes' getAngularMotionDisc (the bounding-sphere radius |h| of a
+ * box centred in its link frame): 2.9 mm for the cart pairs, 5.0 mm for pole-ground and
+ * pole-pole, 2.9 mm for cart-pole.  Returns the
+ * cached points as rows: the point on B (the solver's lever point for both bodies here; Bullet
+ * uses A's own point for A, which moves only the friction rows' lever arms, by d along n), its
+ * normal (A -> B) and separation. */
+static int persistent_manifold(pman_t* M, const box_t* A, const box_t* B, const cp_physics* P, v3 pts[4],
+                               v3 nrm[4], real dist[4]) {
+    const real ra = SQRT(dot(mk(A->h[0], A->h[1], A->h[2]), mk(A->h[0], A->h[1], A->h[2])));
+    const real rb = SQRT(dot(mk(B->h[0], B->h[1], B->h[2]), mk(B->h[0], B->h[1], B->h[2])));
+    const real thr = (real)P->contact_margin * (ra < rb ? ra : rb);
+    v3 n, np[4];
+    real nd[4];
+    int nid[4];
+    int cnt = box_box(A, B, RC(0), (real)P->edge_bias, &n, np, nd, nid);
+    for (int k = 0; k < cnt; ++k) {
+        v3 pa = madd(np[k], n, -(nd[k] * RC(0.5)));   /* on A's surface */
+        v3 pb = madd(np[k], n, nd[k] * RC(0.5));      /* on B's surface */
+        v3 la = box_to_local(A, pa), lb = box_to_local(B, pb);
+        real best = thr * thr;
+        int idx = -1;
+        for (int c = 0; c < M->cnt; ++c) {
+            v3 df = sub(M->la[c], la);
+            real d2 = dot(df, df);
+            if (d2 < best) { best = d2; idx = c; }
+        }
+        real lam = RC(0);
+        if (idx >= 0) {
+            lam = M->lam[idx];
+        } else if (M->cnt == 4) {
+            idx = pm_sort_cached(M, la, nd[k]);
+        } else {
+            idx = M->cnt++;
+        }
+        M->la[idx] = la;
+        M->lb[idx] = lb;
+        M->n[idx] = n;
+        M->d[idx] = nd[k];
+        M->lam[idx] = lam;
+    }
+    for (int c = M->cnt - 1; c >= 0; --c) {
+        v3 pa = box_to_world(A, M->la[c]), pb = box_to_world(B, M->lb[c]);
+        real d = dot(sub(pb, pa), M->n[c]);
+        int keep = d <= thr;
+        if (keep) {
+            v3 proj = madd(pa, M->n[c], d);
+            v3 df = sub(pb, proj);
+            keep = dot(df, df) <= thr * thr;
+        }
+        if (keep) {
+            M->d[c] = d;
+        } else {
+            int last = M->cnt - 1;
+            if (c != last) {
+                M->la[c] = M->la[last]; M->lb[c] = M->lb[last]; M->n[c] = M->n[last];
+                M->d[c] = M->d[last]; M->lam[c] = M->lam[last];
+            }
+            M->cnt--;
+        }
+    }
+    for (int c = 0; c < M->cnt; ++c) {
+        pts[c] = box_to_world(B, M->lb[c]);
+        nrm[c] = M->n[c];
+        dist[c] = M->d[c];
+    }
+    return M->cnt;
 }
 
 /* one p.stepSimulation() of the scene (DESIGN.md §Physics model, steps 1-8) */
@@ -757,6 +880,7 @@ static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* i
     }
     /* 2. narrowphase + row setup at the start-of-step poses, per island: its 3 own
      *    pairs then its 2 cross pairs, into its own capped pool */
+    const int persistent = (P->model_flags & CP_MODEL_PERSISTENT) != 0;
     island_t isl[CP_NUM_ISLANDS];
     for (int p = 0; p < CP_NUM_ISLANDS; ++p) {
         island_t* I = &isl[p];
@@ -767,10 +891,18 @@ static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* i
             box_t A, B;
             get_box(S, P, a, &A);
             get_box(S, P, b, &B);
-            v3 n, pts[4];
+            v3 n, pts[4], pn[4] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
             real dist[4];
-            int ids[4];
-            int cnt = box_box(&A, &B, (real)P->contact_margin, (real)P->edge_bias, &n, pts, dist, ids);
+            int ids[4], pmi[4];
+            int cnt;
+            if (!persistent) {
+                cnt = box_box(&A, &B, (real)P->contact_margin, (real)P->edge_bias, &n, pts, dist, ids);
+                for (int k = 0; k < cnt; ++k) { pn[k] = n; pmi[k] = -1; }
+            } else {
+                cnt = persistent_manifold(&S->pm[p][j], &A, &B, P, pts, pn, dist);
+                n = cnt ? pn[0] : mk(RC(0), RC(0), RC(1));
+                for (int k = 0; k < cnt; ++k) { ids[k] = k; pmi[k] = k; }
+            }
             int m = cnt < CP_ISLAND_POINTS - I->used ? cnt : CP_ISLAND_POINTS - I->used;
             *overflow += cnt - m;
             manifold_t* man = &I->man[j];
@@ -783,29 +915,26 @@ static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* i
             for (int k = 0; k < m; ++k) {
                 point_t* q = &I->pt[I->used + k];
                 q->rb = sub(pts[k], S->x[b - 1]);
-                real K = row_k(S, P, a, b, q->rb, n);
+                q->n = pn[k];
+                real K = row_k(S, P, a, b, q->rb, pn[k]);
                 q->inv_eff = RC(1) / K;
                 q->target = dist[k] > RC(0) ? -(dist[k] * inv_dt) : -(((real)P->erp * dist[k]) * inv_dt);
                 q->id = ids[k];
-                /* warm start: impulse of the same feature in the last substep */
+                q->pm = pmi[k];
                 real l0 = RC(0);
-                for (int q4 = 0; q4 < 4; ++q4) {
-                    if ((int)((S->ws_id[p][j] >> (8 * q4)) & 0xFFu) == ids[k]) { l0 = S->ws_lam[p][j][q4]; break; }
+                if (!persistent) {  /* warm start: impulse of the same feature in the last substep */
+                    for (int q4 = 0; q4 < 4; ++q4) {
+                        if ((int)((S->ws_id[p][j] >> (8 * q4)) & 0xFFu) == ids[k]) { l0 = S->ws_lam[p][j][q4]; break; }
+                    }
+                } else {            /* the cached point's applied impulse */
+                    l0 = S->pm[p][j].lam[k];
                 }
                 q->lam = (real)P->warmstart * l0;
             }
-            if (man->mu > RC(0) && m > 0) {
+            if (man->mu > RC(0) && m > 0) {  /* friction rows: directions and masses after step 3 */
                 int fm = m < CP_ISLAND_FRICTION - I->fused ? m : CP_ISLAND_FRICTION - I->fused;
                 *overflow += m - fm;
                 man->fcnt = fm;
-                v3 t1, t2;
-                plane_space(n, &t1, &t2);
-                for (int k = 0; k < fm; ++k) {
-                    fpoint_t* f = &I->fp[I->fused + k];
-                    f->inv_eff1 = RC(1) / row_k(S, P, a, b, I->pt[I->used + k].rb, t1);
-                    f->inv_eff2 = RC(1) / row_k(S, P, a, b, I->pt[I->used + k].rb, t2);
-                    f->lam1 = f->lam2 = RC(0);
-                }
                 I->fused += fm;
             }
             I->used += m;
@@ -835,6 +964,48 @@ static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* i
         S->v[d] = madd(v, acc, dt);
         S->w[d] = madd(w, accw, dt);
     }
+    /* 3b. friction rows (the rows' masses depend on positions only, so setting them up after
+     *     the velocity update changes no value of the default model).  Directions: btPlaneSpace1
+     *     of the normal; CP_MODEL_VEL_FRICTION: the lateral relative velocity at the point when
+     *     its length^2 exceeds SIMD_EPSILON, the second direction its cross with Bullet's normal
+     *     (convertContact of the rigid-body solver), else btPlaneSpace1. */
+    for (int p = 0; p < CP_NUM_ISLANDS; ++p) {
+        island_t* I = &isl[p];
+        for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
+            manifold_t* man = &I->man[j];
+            int g = ISLAND_PAIR[p][j];
+            int a = PAIR_A[g], b = PAIR_B[g];
+            for (int k = 0; k < man->fcnt; ++k) {
+                point_t* q = &I->pt[man->base + k];
+                fpoint_t* f = &I->fp[man->fbase + k];
+                v3 t1, t2;
+                plane_space(q->n, &t1, &t2);
+                if (P->model_flags & CP_MODEL_VEL_FRICTION) {
+                    v3 vb = add(S->v[b - 1], cross(S->w[b - 1], q->rb));
+                    v3 va = mk(RC(0), RC(0), RC(0));
+                    if (a != 0) {
+                        v3 ra = add(q->rb, sub(S->x[b - 1], S->x[a - 1]));
+                        va = add(S->v[a - 1], cross(S->w[a - 1], ra));
+                    }
+                    v3 vel = sub(va, vb);
+                    v3 lat = madd(vel, q->n, -dot(q->n, vel));
+                    real l2 = dot(lat, lat);
+                    if (l2 > ORC_SIMD_EPSILON) {
+                        real il = RC(1) / SQRT(l2);
+                        t1 = scl(lat, il);
+                        v3 c = cross(t1, neg(q->n));
+                        real cl = RC(1) / SQRT(dot(c, c));
+                        t2 = scl(c, cl);
+                    }
+                }
+                f->t1 = t1;
+                f->t2 = t2;
+                f->inv_eff1 = RC(1) / row_k(S, P, a, b, q->rb, t1);
+                f->inv_eff2 = RC(1) / row_k(S, P, a, b, q->rb, t2);
+                f->lam1 = f->lam2 = RC(0);
+            }
+        }
+    }
     /* 4. warm start + projected Gauss-Seidel over ONE solver group per env.  Bullet's
      *    island manager batches islands into one solve until the group holds
      *    m_minimumSolverBatchSize (128) constraints [ext], so the two cart-pole islands
@@ -851,7 +1022,23 @@ static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* i
     for (int p = 0; p < CP_NUM_ISLANDS; ++p) merged |= (isl[p].man[3].cnt + isl[p].man[4].cnt) > 0;
     if (merged_out) *merged_out += merged;
     int it = 0;
-    if (!merged) {
+    if (!merged && (P->model_flags & CP_MODEL_SPLIT_ISLANDS)) {
+        /* one solver group per island (m_minimumSolverBatchSize <= 1): own warm start, own
+         * stopping decision; the islands share no dynamic body, so their order is immaterial */
+        for (int p = 0; p < CP_NUM_ISLANDS; ++p) {
+            for (int j = 0; j < 3; ++j) warm_pair(S, P, &isl[p], p, j);
+            if (isl[p].used == 0) continue;
+            int itp;
+            for (itp = 0; itp < iters;) {
+                int bad = 0;
+                for (int j = 0; j < 3; ++j) sweep_normal(S, P, &isl[p], p, j, tol, &bad);
+                for (int j = 0; j < 3; ++j) sweep_friction(S, P, &isl[p], p, j, tol, &bad);
+                ++itp;
+                if (!bad) break;
+            }
+            if (itp > it) it = itp;
+        }
+    } else if (!merged) {
         for (int p = 0; p < CP_NUM_ISLANDS; ++p)
             for (int j = 0; j < 3; ++j) warm_pair(S, P, &isl[p], p, j);
         if (isl[0].used + isl[1].used > 0) {
@@ -888,7 +1075,15 @@ static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* i
 #ifdef ORC_STATS  /* diagnostic build only (tools/row_classes.py): row structure + sweeps per island */
     for (int p = 0; p < CP_NUM_ISLANDS; ++p) orc_stats_island(&isl[p], merged, it);
 #endif
-    /* 4c. refresh the warm-start cache */
+    /* 4c. refresh the warm-start cache (CP_MODEL_PERSISTENT: the cached points' impulses) */
+    for (int p = 0; p < CP_NUM_ISLANDS; ++p)
+        for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
+            const manifold_t* m = &isl[p].man[j];
+            for (int k = 0; k < m->cnt; ++k) {
+                const point_t* q = &isl[p].pt[m->base + k];
+                if (q->pm >= 0) S->pm[p][j].lam[q->pm] = q->lam;
+            }
+        }
     for (int p = 0; p < CP_NUM_ISLANDS; ++p) {
         for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
             manifold_t* m = &isl[p].man[j];
@@ -946,6 +1141,7 @@ static void apply_force_link(sim_t* S, int d, real fx, real fy, real fz) {
 
 /* ------------------------------------------------------------ world-level API */
 static void world_load(const orc_world* w, sim_t* S) {
+    memset(S->pm, 0, sizeof(S->pm));  /* CP_MODEL_PERSISTENT is an env-level (orc_envs) option */
     for (int d = 0; d < CP_NUM_DYN; ++d) {
         S->x[d] = mk((real)w->pos[d][0], (real)w->pos[d][1], (real)w->pos[d][2]);
         for (int k = 0; k < 4; ++k) S->q[d][k] = (real)w->quat[d][k];
@@ -1037,6 +1233,7 @@ static void env_load(const orc_envs* e, int i, sim_t* S) {
             memcpy(&S->ws_id[p][j], &SF(e, CP_SF_WS_ID(p, j), i), 4);
             for (int k = 0; k < 4; ++k) S->ws_lam[p][j][k] = SF(e, CP_SF_WS_LAM(p, j, k), i);
         }
+    memcpy(S->pm, (const pman_t*)e->pman + (size_t)i * CP_NUM_PAIRS, sizeof(S->pm));
 }
 static void env_store(orc_envs* e, int i, const sim_t* S) {
     for (int d = 0; d < CP_NUM_DYN; ++d) {
@@ -1061,6 +1258,7 @@ static void env_store(orc_envs* e, int i, const sim_t* S) {
             memcpy(&SF(e, CP_SF_WS_ID(p, j), i), &S->ws_id[p][j], 4);
             for (int k = 0; k < 4; ++k) SF(e, CP_SF_WS_LAM(p, j, k), i) = S->ws_lam[p][j][k];
         }
+    memcpy((pman_t*)e->pman + (size_t)i * CP_NUM_PAIRS, S->pm, sizeof(S->pm));
 }
 static int32_t get_i(const orc_envs* e, int f, int i) {
     int32_t v;
@@ -1094,6 +1292,7 @@ int orc_envs_create(const cp_config* cfg, orc_envs** out) {
     e->overflow = (int32_t*)calloc(B, sizeof(int32_t));
     e->sweeps = (int32_t*)calloc((size_t)B * 2, sizeof(int32_t));
     e->merged = (int32_t*)calloc(B, sizeof(int32_t));
+    e->pman = calloc(B * CP_NUM_PAIRS, sizeof(pman_t));
     for (int i = 0; i < e->B; ++i) {
         for (int d = 0; d < CP_NUM_DYN; ++d) {
             for (int k = 0; k < 3; ++k) SF(e, CP_SF_BODY(d, k), i) = cfg->phys.spawn_pos[d + 1][k];
@@ -1111,7 +1310,7 @@ int orc_envs_create(const cp_config* cfg, orc_envs** out) {
 void orc_envs_destroy(orc_envs* e) {
     if (!e) return;
     free(e->state); free(e->term_obs); free(e->bump_forces); free(e->ret_acc);
-    free(e->last_ret); free(e->last_len); free(e->overflow); free(e->sweeps); free(e->merged);
+    free(e->last_ret); free(e->last_len); free(e->overflow); free(e->sweeps); free(e->merged); free(e->pman);
     free(e);
 }
 void orc_envs_set_bump_forces(orc_envs* e, const float* f) {
@@ -1164,6 +1363,7 @@ static void reset_one(orc_envs* e, int i, float* obs_row /* R*14 */) {
         for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
             S.ws_id[p][j] = 0xFFFFFFFFu;
             for (int k = 0; k < 4; ++k) S.ws_lam[p][j][k] = RC(0);
+            S.pm[p][j].cnt = 0;   /* resetBasePositionAndOrientation: no contact survives the teleport */
         }
     int32_t ov = 0;
     for (int s = 0; s < cfg->settle_steps; ++s) substep(&S, &cfg->phys, &ov, NULL, NULL, NULL, NULL);

@@ -341,6 +341,40 @@ def test_gym_mirror_matches_oracle_and_reference_errors(oracle_mod):
     denv.step([1, 4])
 
 
+@pytest.mark.parametrize("graph", [True, False], ids=["hipgraph", "eager"])
+def test_gym_mirror_discrete_c1_vs_oracle(oracle_mod, graph):
+    """C1's configuration through the reference's surface: B = 1, R = 2 (the reference default),
+    F_init 55, discrete actions, two episodes of 200 steps with the reference's own reset loop
+    (the agent calls reset() after done); obs and the 12-state readback (monkey_positions /
+    velocities, the :224 bug included) bit-exact against the oracle, with the step replayed as a
+    hipGraph and eagerly."""
+    from cartpoleplusplus_amd.bullet_cartpole import BulletCartpole, add_opts, draw_bump_forces
+    ap = argparse.ArgumentParser()
+    add_opts(ap)
+    opts = ap.parse_args(["--initial-force", "55"])
+    env = BulletCartpole(opts, discrete_actions=True)
+    env.use_graph = graph
+    cfg = oracle_mod.default_config(num_envs=1, action_repeats=2, initial_force=55.0, bump_mode=abi.CP_BUMP_HOST)
+    orc = oracle_mod.Envs(cfg)
+    rng = np.random.default_rng(21)
+    for ep in range(2):
+        np.random.seed(100 + ep)
+        obs = env.reset()
+        np.random.seed(100 + ep)
+        orc.set_bump_forces(draw_bump_forces(55.0, True)[None].astype(np.float32))
+        _assert_same(obs, orc.reset()[0], f"episode {ep} reset")
+        done, t = False, 0
+        while not done:
+            a = rng.integers(0, 5, 2)
+            o, r, done, info = env.step(a)
+            oo, _, od, rb = orc.step(a.astype(np.int8).reshape(1, 2), readback=True, readback_bug=True)
+            _assert_same(o, oo[0], f"episode {ep} step {t} obs")
+            _assert_same(env.monkey_positions.astype(np.float32), rb[0][..., 0:2, :], f"episode {ep} step {t} positions")
+            _assert_same(env.monkey_velocities.astype(np.float32), rb[0][..., 2:4, :], f"step {t} velocities")
+            t += 1
+        assert t == 200 and info == {"done_reason": "episode length"}
+
+
 def test_batched_rejects_wrong_buffers_before_the_abi():
     """Shapes / dtypes the C-ABI would read blindly raise ValueError, and the
     handle stays usable afterwards."""

@@ -1,12 +1,12 @@
 #!/bin/bash
 # One GPU session (under gpurun): the GPU suite, smoke, then bench lines given as arguments
 # (each "tag|bench args"), every step under its own time limit; stops at the first failure.
-# usage: bash tools/gpu_session.sh <tag> ["name|--bench --args" ...]
+# usage: [PYTEST_K="expr"] [SKIP_TESTS=1] bash tools/gpu_session.sh <tag> ["name|--bench --args" ...]
 set -u
 TAG=${1:-dev}; shift || true
 mkdir -p gpurun_out
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} \
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} \
       > gpurun_out/pytest_$TAG.log 2>&1
   rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|error" gpurun_out/pytest_$TAG.log | tail -3
   [ $rc -ne 0 ] && exit $rc

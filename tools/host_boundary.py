@@ -20,11 +20,12 @@ from cartpoleplusplus_amd import bullet_cartpole  # noqa: E402
 from cartpoleplusplus_amd.batched import BatchedCartpole  # noqa: E402
 
 
-def gym_mirror(steps=300):
+def gym_mirror(steps=300, graph=True):
     p = argparse.ArgumentParser()
     bullet_cartpole.add_opts(p)
     opts = p.parse_args([])
     env = bullet_cartpole.BulletCartpole(opts, discrete_actions=True)
+    env.use_graph = graph
     rng = np.random.default_rng(0)
     t0 = time.perf_counter()
     env.reset()
@@ -39,6 +40,7 @@ def gym_mirror(steps=300):
     dt = time.perf_counter() - t0
     return {"env_steps_per_s": round(n / dt, 1), "ms_per_step": round(dt / n * 1e3, 4),
             "reset_ms": round(t_reset * 1e3, 2), "action_repeats": opts.action_repeats,
+            "step_as_hipgraph": graph,
             "note": "B = 1, numpy action in, numpy obs copy out per step (resets inside the loop included)"}
 
 
@@ -68,4 +70,5 @@ def batched_pcie(B=65536, steps=400, warmup=20):
 
 
 if __name__ == "__main__":
-    print(json.dumps({"gym_mirror_B1": gym_mirror(), "batched_pcie_C3": batched_pcie()}), flush=True)
+    print(json.dumps({"gym_mirror_B1": gym_mirror(), "gym_mirror_B1_eager": gym_mirror(graph=False),
+                      "batched_pcie_C3": batched_pcie()}), flush=True)
