@@ -85,7 +85,7 @@ class cp_physics(C.Structure):
 CP_MODEL_SPLIT_ISLANDS = 0x1
 CP_MODEL_VEL_FRICTION = 0x2
 CP_MODEL_PERSISTENT = 0x4
-CP_MODEL_GPU_FLAGS = 0x0
+CP_MODEL_GPU_FLAGS = 0x4
 
 # kernel shapes (cp_set_kernel_shape)
 CP_SHAPE_AUTO = -1

@@ -15,6 +15,12 @@
 
 #define CP_DEV __device__ __forceinline__
 
+// CP_MODEL_PERSISTENT: per lane (island) and local pair, the persistent manifold: count, then for
+// the 4 cache slots the local point on A (3), on B (3), the normal (3), the separation (1) and the
+// applied normal impulse (1) -- buffer Bufs::pman, one column per lane (cp_physics.h PMan)
+#define CP_PM_PAIR_FIELDS 45
+#define CP_PM_FIELDS (CP_ISLAND_PAIRS * CP_PM_PAIR_FIELDS)
+
 namespace cpc {
 
 CP_DEV float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
@@ -113,6 +119,7 @@ struct Bufs {
     int32_t* rlist;    // [B] envs to render after the step kernel
     int32_t* rcount;   // [1]
     uint8_t* stepped;  // [B] 1 = simulated by the last cp_step (event log: done-before envs are not logged)
+    void* pman;        // [CP_PM_FIELDS][2B] real: persistent manifolds (CP_MODEL_PERSISTENT handles only)
 };
 
 }  // namespace cpc

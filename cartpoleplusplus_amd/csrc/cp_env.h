@@ -258,11 +258,11 @@ __global__ void __launch_bounds__(256) cp_init_kernel(cp_config cfg, Bufs b) {
 // (fixed-length episodes end together).  LAT = true: one wave per SIMD with 512 registers and
 // fast-form rows, for the short lists of desynchronised episodes (bounds termination), where
 // the 130 serial substeps of one wave are the whole latency of the step.
-template <bool LAT>
+template <bool LAT, bool PM = false>
 __global__ void __launch_bounds__(WAVE)
 __attribute__((amdgpu_waves_per_eu(LAT ? 1 : CP_WAVES_PER_EU, LAT ? 1 : CP_WAVES_PER_EU)))
 cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
-    __shared__ real lds_pool[POOL_FLOATS * WAVE];
+    __shared__ real lds_pool[(PM ? POOL_FLOATS_PM : POOL_FLOATS) * WAVE];
     const int B = cfg.num_envs;
     const int t = blockIdx.x * WAVE + threadIdx.x;
     if (t == 0 && b.count_next) *b.count_next = 0;  // the next cp_step's list starts empty
@@ -273,13 +273,15 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     const int i = b.list[t >> 1];
     real* pool = lds_pool + threadIdx.x;
     real* pool0 = lds_pool + (threadIdx.x & ~1u);
-    const Mem G = Mem::make(b.state, b.scratch, B, i, isl);
+    const Mem G = Mem::make(b.state, b.scratch, B, i, isl, b.pman);
     const Lane L = Lane::make(isl, cfg.phys);
     Stamps ST;
     CP_STAMP(k0);
     CP_RT(r0);
     Sim S;
     load_sim(S, G.st, G.off);  // pending forces survive the reset (pybullet keeps them)
+    if constexpr (PM)  // resetBasePositionAndOrientation: no cached contact survives the teleport
+        for (int j = 0; j < CP_ISLAND_PAIRS; ++j) G.sp(pmf(j, 0), bits_to<real>(0u));
     const int episode = ldi(G.st, CP_SF_EPISODE, G.off);
 #pragma unroll
     for (int d = 0; d < CP_NUM_DYN; ++d) {
@@ -297,7 +299,7 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     int ov = 0;
     const int nsub = cfg.settle_steps + cfg.initial_force_steps;
     for (int s = 0; s < nsub; ++s) {
-        substep<LAT && !kF64, true>(S, cfg.phys, L, pool, pool0, ov, G, ST);
+        substep<LAT && !kF64, true, true, PM>(S, cfg.phys, L, pool, pool0, ov, G, ST);
         const int k = s - cfg.settle_steps;
         if (k >= 0) {
             real fx, fy;
@@ -333,12 +335,12 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
 
 // LAT: the latency shape of cp_reset_kernel<true> (1 wave per SIMD, 512 registers, fast-form
 // rows) for batches whose waves all get a SIMD of their own (<= 32,768 envs)
-template <int KIND, bool LQR, bool LAT>
+template <int KIND, bool LQR, bool LAT, bool PM = false>
 __global__ void __launch_bounds__(WAVE)
 __attribute__((amdgpu_waves_per_eu(LAT ? 1 : CP_WAVES_PER_EU, LAT ? 1 : CP_WAVES_PER_EU)))
 cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float* reward_out, uint8_t* done_out,
                float* term_out, float* readback, int rb_bug, Lqr lq) {
-    __shared__ real lds_pool[POOL_FLOATS * WAVE];
+    __shared__ real lds_pool[(PM ? POOL_FLOATS_PM : POOL_FLOATS) * WAVE];
     const int B = cfg.num_envs;
     const int t = blockIdx.x * WAVE + threadIdx.x;
     const int i = t >> 1, isl = t & 1;
@@ -353,7 +355,7 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
     CP_STAMP(k0);
     CP_RT(r0);
     if (inb) {
-        const Mem G = Mem::make(b.state, b.scratch, B, i, isl);
+        const Mem G = Mem::make(b.state, b.scratch, B, i, isl, b.pman);
         const Lane L = Lane::make(isl, cfg.phys);
         const SoaF term = SoaF::make(b.term_obs, B, R * 14);
         const uint32_t toff = SoaF::eoff(i);
@@ -393,7 +395,7 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
             }
             for (int r = 0; r < R; ++r) {
                 for (int s = 0; s < SR; ++s) {
-                    substep<LAT && !kF64, false, kAllinStep>(S, cfg.phys, L, pool, pool0, ov, G, ST);
+                    substep<LAT && !kF64, false, kAllinStep, PM>(S, cfg.phys, L, pool, pool0, ov, G, ST);
                     if constexpr (LQR) {  // disturbance + control (:897-901), control from the pre-step state
                         apply_force_link<0>(S, f00 + u[0][0], f01 + u[0][1]);
                         apply_force_link<1>(S, f10 + u[1][0], f11 + u[1][1]);
@@ -513,12 +515,12 @@ enum : int { RC_K = 0, RC_SUB, RC_STEPS, RC_EPISODE, RC_FLAGS, RC_RET, RC_U0, RC
 enum : uint32_t { RF_DONE = 1u, RF_RESETTING = 2u, RF_LAST_SIM = 4u, RF_LQR_DONE = 8u };
 static_assert(RC_FIELDS <= 4 * CP_ISLAND_PAIRS, "rollout state must fit the scratch SoA's per-lane fields");
 
-template <int KIND, bool LQR, bool LAT>
+template <int KIND, bool LQR, bool LAT, bool PM = false>
 __global__ void __launch_bounds__(WAVE)
 __attribute__((amdgpu_waves_per_eu(LAT ? 1 : CP_WAVES_PER_EU, LAT ? 1 : CP_WAVES_PER_EU)))
 cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_out, float* reward_out,
                   uint8_t* done_out, float* term_out, Lqr lq) {
-    __shared__ real lds_pool[POOL_FLOATS * WAVE];
+    __shared__ real lds_pool[(PM ? POOL_FLOATS_PM : POOL_FLOATS) * WAVE];
     const int B = cfg.num_envs;
     const int t = blockIdx.x * WAVE + threadIdx.x;
     const int i = t >> 1, isl = t & 1;
@@ -528,7 +530,7 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
     const int nreset = cfg.settle_steps + cfg.initial_force_steps;
     real* pool = lds_pool + threadIdx.x;
     real* pool0 = lds_pool + (threadIdx.x & ~1u);
-    const Mem G = Mem::make(b.state, b.scratch, B, i, isl);
+    const Mem G = Mem::make(b.state, b.scratch, B, i, isl, b.pman);
     const Lane L = Lane::make(isl, cfg.phys);
     const SoaF term = SoaF::make(b.term_obs, B, R * 14);
     const size_t obs_step = (size_t)B * R * 14;
@@ -573,7 +575,7 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
                            ldi(G.st, CP_SF_DONE, G.off) != 0 ? RF_DONE : 0u, b.ret_acc[i]);
     while (__ballot(work) != 0ull) {
         if (!work) continue;
-        substep<LAT && !kF64, false, kAllinStep>(S, cfg.phys, L, pool, pool0, ov, G, ST);
+        substep<LAT && !kF64, false, kAllinStep, PM>(S, cfg.phys, L, pool, pool0, ov, G, ST);
         int k = ldc(RC_K), sub = ldc(RC_SUB);
         uint32_t flags = (uint32_t)ldc(RC_FLAGS);
         if (!(flags & RF_RESETTING)) {
@@ -640,6 +642,7 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
                         G.sw(CP_SF_WS_ID(0, j), bits_to<real>(0xFFFFFFFFu));
 #pragma unroll
                         for (int q = 0; q < 4; ++q) G.sl(CP_SF_WS_LAM(0, j, q), real(0.0));
+                        if constexpr (PM) G.sp(pmf(j, 0), bits_to<real>(0u));
                     }
                     stc(RC_SUB, 0);
                     stc(RC_STEPS, steps);
@@ -697,6 +700,10 @@ void launch_init(const cp_config& cfg, const Bufs& b, hipStream_t st) {
 
 void launch_reset(bool lat, const cp_config& cfg, const Bufs& b, float* obs_out, hipStream_t st) {
     const dim3 grid(env_grid(2 * cfg.num_envs, WAVE)), block(WAVE);  // two lanes per env
+    if (cfg.phys.model_flags & CP_MODEL_PERSISTENT) {  // the persistent-manifold model: latency shape only
+        hipLaunchKernelGGL((cp_reset_kernel<true, true>), grid, block, 0, st, cfg, b, obs_out);
+        return;
+    }
     if constexpr (kF64) {
         (void)lat;
         hipLaunchKernelGGL(cp_reset_kernel<true>, grid, block, 0, st, cfg, b, obs_out);
@@ -711,6 +718,11 @@ static void launch_step_t(bool lat, const cp_config& cfg, const Bufs& b, const v
                           float* reward_out, uint8_t* done_out, float* term_out, float* readback, int rb_bug,
                           const Lqr& lq, hipStream_t st) {
     const dim3 grid(env_grid(2 * cfg.num_envs, WAVE)), block(WAVE);  // two lanes per env
+    if (cfg.phys.model_flags & CP_MODEL_PERSISTENT) {  // the persistent-manifold model: latency shape only
+        hipLaunchKernelGGL((cp_step_kernel<K, Q, true, true>), grid, block, 0, st, cfg, b, actions, obs_out,
+                           reward_out, done_out, term_out, readback, rb_bug, lq);
+        return;
+    }
     if constexpr (kF64) {
         (void)lat;
         hipLaunchKernelGGL((cp_step_kernel<K, Q, true>), grid, block, 0, st, cfg, b, actions, obs_out, reward_out,
@@ -730,7 +742,10 @@ static void launch_rollout_t(bool lat, const cp_config& cfg, const Bufs& b, int 
                              float* obs_out, float* reward_out, uint8_t* done_out, float* term_out, const Lqr& lq,
                              hipStream_t st) {
     const dim3 grid(env_grid(2 * cfg.num_envs, WAVE)), block(WAVE);  // two lanes per env
-    if (lat || kF64)
+    if (cfg.phys.model_flags & CP_MODEL_PERSISTENT)
+        hipLaunchKernelGGL((cp_rollout_kernel<K, Q, true, true>), grid, block, 0, st, cfg, b, steps, actions, obs_out,
+                           reward_out, done_out, term_out, lq);
+    else if (lat || kF64)
         hipLaunchKernelGGL((cp_rollout_kernel<K, Q, true>), grid, block, 0, st, cfg, b, steps, actions, obs_out,
                            reward_out, done_out, term_out, lq);
     else

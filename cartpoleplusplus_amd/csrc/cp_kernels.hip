@@ -332,6 +332,11 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     CP_ALLOC(h->b.scratch, (size_t)4 * CP_ISLAND_PAIRS * 2 * B * rb);
     CP_ALLOC(h->b.stamps, CP_STAMP_SLOTS * sizeof(uint64_t));
     CP_ALLOC(h->b.stepped, B * sizeof(uint8_t));
+    if (cfg->phys.model_flags & CP_MODEL_PERSISTENT) {  // the persistent manifolds, empty
+        CP_ALLOC(h->b.pman, (size_t)CP_PM_FIELDS * 2 * B * rb);
+        e = hipMemset(h->b.pman, 0, (size_t)CP_PM_FIELDS * 2 * B * rb);
+        if (e != hipSuccess) return fail_free(e, "hipMemset");
+    }
 #undef CP_ALLOC
     e = hipMemset(h->count2, 0, 2 * sizeof(int32_t));
     if (e != hipSuccess) return fail_free(e, "hipMemset");
@@ -371,6 +376,7 @@ void cp_destroy(cp_handle* h) {
     (void)hipFree(h->b.scratch);
     (void)hipFree(h->b.stamps);
     (void)hipFree(h->b.stepped);
+    (void)hipFree(h->b.pman);
     (void)hipFree(h->b.rposes);
     (void)hipFree(h->b.rlist);
     (void)hipFree(h->b.rcount);
@@ -425,6 +431,7 @@ static void choose_reset_shape(cp_handle* h) {
     if (h->reset_req != CP_SHAPE_AUTO) h->reset_lat = h->reset_req == CP_SHAPE_LATENCY;
     if (h->step_req != CP_SHAPE_AUTO) h->step_lat = h->step_req == CP_SHAPE_LATENCY;
     if (h->f64) h->reset_lat = h->step_lat = 1;  // fp64: the 512-register shape only
+    if (h->cfg.phys.model_flags & CP_MODEL_PERSISTENT) h->reset_lat = h->step_lat = 1;  // PM: latency shape only
 }
 
 static int launch_reset_from_list(cp_handle* h, float* obs_out, hipStream_t st, bool render) {
@@ -541,8 +548,9 @@ int cp_set_kernel_shape(cp_handle* h, int step_shape, int reset_shape) {
     auto ok = [](int v) { return v == CP_SHAPE_AUTO || v == CP_SHAPE_THROUGHPUT || v == CP_SHAPE_LATENCY; };
     if (!ok(step_shape) || !ok(reset_shape))
         return fail(h, "cp_set_kernel_shape: shapes must be CP_SHAPE_AUTO, CP_SHAPE_THROUGHPUT or CP_SHAPE_LATENCY");
-    if (h->f64 && (step_shape == CP_SHAPE_THROUGHPUT || reset_shape == CP_SHAPE_THROUGHPUT))
-        return fail(h, "cp_set_kernel_shape: fp64 handles have the latency shape only");
+    if ((h->f64 || (h->cfg.phys.model_flags & CP_MODEL_PERSISTENT)) &&
+        (step_shape == CP_SHAPE_THROUGHPUT || reset_shape == CP_SHAPE_THROUGHPUT))
+        return fail(h, "cp_set_kernel_shape: fp64 and persistent-manifold handles have the latency shape only");
     h->step_req = step_shape;
     h->reset_req = reset_shape;
     choose_reset_shape(h);

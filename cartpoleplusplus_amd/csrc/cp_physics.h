@@ -49,6 +49,11 @@ constexpr int POOL_FLOATS = NPF * MAXP + 4 * MAXF;  // 80 floats per lane = 20 K
 
 CP_DEV real& pool_n(real* pool, int field, int slot) { return pool[(field * MAXP + slot) * WAVE]; }
 CP_DEV real& pool_f(real* pool, int field, int slot) { return pool[(NPF * MAXP + field * MAXF + slot) * WAVE]; }
+// CP_MODEL_PERSISTENT (PM) kernels: each normal row's own normal (a cached point keeps the normal it
+// was added with), 3 more fields per row after the friction fields
+constexpr int POOL_FLOATS_PM = POOL_FLOATS + 3 * MAXP;
+CP_DEV real& pool_pn(real* pool, int c, int slot) { return pool[(POOL_FLOATS + c * MAXP + slot) * WAVE]; }
+CP_DEV V3 pool_normal(real* pool, int slot) { return mk(pool_pn(pool, 0, slot), pool_pn(pool, 1, slot), pool_pn(pool, 2, slot)); }
 
 // body pairs (a < b), Bullet-like order over the loadURDF ids
 __host__ __device__ constexpr int pair_a(int p) {
@@ -75,14 +80,16 @@ using Soa = SoaT<real>;
 struct Mem {
     Soa st;           // state SoA [CP_STATE_FIELDS][B]
     Soa scr;          // scratch SoA [4*CP_ISLAND_PAIRS][2B], one column per lane
+    Soa pm;           // CP_MODEL_PERSISTENT: the island's persistent manifolds [PM_FIELDS][2B], one column per lane
     uint32_t off;     // env index * sizeof(real)
     uint32_t woff;    // off + island * CP_ISLAND_PAIRS fields  (warm-start ids of the lane's island)
     uint32_t loff;    // off + island * 4*CP_ISLAND_PAIRS fields (warm-start impulses)
     uint32_t xoff;    // (2 * env + island) * sizeof(real)
-    CP_DEV static Mem make(void* state, void* scratch, int B, int env, int isl) {
+    CP_DEV static Mem make(void* state, void* scratch, int B, int env, int isl, void* pman = nullptr) {
         Mem m;
         m.st = Soa::make(state, B, CP_STATE_FIELDS);
         m.scr = Soa::make(scratch, 2 * B, 4 * CP_ISLAND_PAIRS);
+        m.pm = Soa::make(pman, pman ? 2 * B : 0, CP_PM_FIELDS);  // null: an empty resource (no PM kernel reads it)
         m.off = Soa::eoff(env);
         m.woff = m.off + (uint32_t)(isl * CP_ISLAND_PAIRS) * m.st.fstride;
         m.loff = m.off + (uint32_t)(isl * 4 * CP_ISLAND_PAIRS) * m.st.fstride;
@@ -97,6 +104,8 @@ struct Mem {
     CP_DEV void sl(int f, real v) const { st.st(f, loff, v); }
     CP_DEV real lx(int f) const { return scr.ld(f, xoff); }
     CP_DEV void sx(int f, real v) const { scr.st(f, xoff, v); }
+    CP_DEV real lp(int f) const { return pm.ld(f, xoff); }
+    CP_DEV void sp(int f, real v) const { pm.st(f, xoff, v); }
 };
 
 struct Box {
@@ -639,18 +648,18 @@ CP_DEV bool is_plus_z(V3 n) { return n.x == real(0.0) && n.y == real(0.0) && n.z
 template <int J> constexpr int loc_a() { return J == 2 ? 1 : 0; }
 template <int J> constexpr int loc_b() { return J == 0 ? 1 : 2; }
 
-template <int J>
+template <int J, bool PM = false>
 CP_DEV void isl_warmstart(Isl& I, const Step& T, real* pool) {
     const uint32_t pk = T.pk[J];
     const int cnt = pk_cnt(pk), base = pk_base(pk);
     for (int k = 0; k < cnt; ++k) {
         const int s = base + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
-        isl_impulse<loc_a<J>(), loc_b<J>()>(I, rb, T.n[J], pool_n(pool, F_LAM, s));
+        isl_impulse<loc_a<J>(), loc_b<J>()>(I, rb, PM ? pool_normal(pool, s) : T.n[J], pool_n(pool, F_LAM, s));
     }
 }
 
-template <int J>
+template <int J, bool PM = false>
 CP_DEV void isl_normal_rows(Isl& I, const Step& T, real* pool, real tol, bool& bad) {
     const uint32_t pk = T.pk[J];
     const int cnt = pk_cnt(pk), base = pk_base(pk);
@@ -658,13 +667,13 @@ CP_DEV void isl_normal_rows(Isl& I, const Step& T, real* pool, real tol, bool& b
         const int s = base + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
         real lam = pool_n(pool, F_LAM, s);
-        bad |= isl_row<loc_a<J>(), loc_b<J>(), false>(I, rb, T.n[J], pool_n(pool, F_IE, s),
+        bad |= isl_row<loc_a<J>(), loc_b<J>(), false>(I, rb, PM ? pool_normal(pool, s) : T.n[J], pool_n(pool, F_IE, s),
                                                       pool_n(pool, F_TG, s), lam, real(0.0), tol);
         pool_n(pool, F_LAM, s) = lam;
     }
 }
 
-template <int J, bool HOISTED = false>
+template <int J, bool HOISTED = false, bool PM = false>
 CP_DEV void isl_friction_rows(Isl& I, const Step& T, real mu, real* pool, real tol, bool& bad, V3 ht1 = V3{},
                               V3 ht2 = V3{}) {
     const uint32_t pk = T.pk[J];
@@ -675,7 +684,7 @@ CP_DEV void isl_friction_rows(Isl& I, const Step& T, real mu, real* pool, real t
     if constexpr (HOISTED) {
         t1 = ht1;
         t2 = ht2;
-    } else {
+    } else if constexpr (!PM) {
         // tangent basis inside the sweep (cross pairs: hoisted it would pin VGPRs for rare rows)
         V3 n = T.n[J];
         asm volatile("" : "+v"(n.x), "+v"(n.y), "+v"(n.z));
@@ -683,6 +692,7 @@ CP_DEV void isl_friction_rows(Isl& I, const Step& T, real mu, real* pool, real t
     }
     for (int k = 0; k < fcnt; ++k) {
         const int s = base + k, fs = fbase + k;
+        if constexpr (PM) plane_space(pool_normal(pool, s), t1, t2);  // the point's own normal
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
         real bound = mu * pool_n(pool, F_LAM, s);
         real l1 = pool_f(pool, FF_L1, fs), l2 = pool_f(pool, FF_L2, fs);
@@ -803,7 +813,7 @@ CP_DEV bool solve_row(Sim& S, const Step& T, const cp_physics& P, V3 rb, V3 t, r
     return abs_(dl) > tol * inv_eff;  // Bullet residual test (oracle: solve_row)
 }
 
-template <int PAIR>
+template <int PAIR, bool PM = false>
 CP_DEV void pair_warmstart(Sim& S, const Step& T, bool second, const cp_physics& P, real* pool0) {
     constexpr int A = pair_a(PAIR), B = pair_b(PAIR);
     real* pool = pool0 + island_of(PAIR);
@@ -813,11 +823,11 @@ CP_DEV void pair_warmstart(Sim& S, const Step& T, bool second, const cp_physics&
     for (int k = 0; k < cnt; ++k) {
         const int s = base + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
-        apply_impulse<A, B>(S, T, P, rb, H.n, pool_n(pool, F_LAM, s));
+        apply_impulse<A, B>(S, T, P, rb, PM ? pool_normal(pool, s) : H.n, pool_n(pool, F_LAM, s));
     }
 }
 
-template <int PAIR>
+template <int PAIR, bool PM = false>
 CP_DEV void pair_normal_rows(Sim& S, const Step& T, bool second, const cp_physics& P, real* pool0,
                              real tol, bool& bad) {
     constexpr int A = pair_a(PAIR), B = pair_b(PAIR);
@@ -829,13 +839,13 @@ CP_DEV void pair_normal_rows(Sim& S, const Step& T, bool second, const cp_physic
         const int s = base + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
         real lam = pool_n(pool, F_LAM, s);
-        bad |= solve_row<A, B, false>(S, T, P, rb, H.n, pool_n(pool, F_IE, s), pool_n(pool, F_TG, s),
-                                      lam, real(0.0), tol);
+        bad |= solve_row<A, B, false>(S, T, P, rb, PM ? pool_normal(pool, s) : H.n, pool_n(pool, F_IE, s),
+                                      pool_n(pool, F_TG, s), lam, real(0.0), tol);
         pool_n(pool, F_LAM, s) = lam;
     }
 }
 
-template <int PAIR>
+template <int PAIR, bool PM = false>
 CP_DEV void pair_friction_rows(Sim& S, const Step& T, bool second, const cp_physics& P, real* pool0,
                                real tol, bool& bad) {
     constexpr int A = pair_a(PAIR), B = pair_b(PAIR);
@@ -846,12 +856,15 @@ CP_DEV void pair_friction_rows(Sim& S, const Step& T, bool second, const cp_phys
     if (fcnt == 0) return;
     const int base = pk_base(pk), fbase = pk_fbase(pk);
     const real mu = real(P.friction[A]) * real(P.friction[B]);  // oracle: (real) * (real)
-    V3 n = H.n;
-    asm volatile("" : "+v"(n.x), "+v"(n.y), "+v"(n.z));
     V3 t1, t2;
-    plane_space(n, t1, t2);
+    if constexpr (!PM) {
+        V3 n = H.n;
+        asm volatile("" : "+v"(n.x), "+v"(n.y), "+v"(n.z));
+        plane_space(n, t1, t2);
+    }
     for (int k = 0; k < fcnt; ++k) {
         const int s = base + k, fs = fbase + k;
+        if constexpr (PM) plane_space(pool_normal(pool, s), t1, t2);
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
         real bound = mu * pool_n(pool, F_LAM, s);
         real l1 = pool_f(pool, FF_L1, fs), l2 = pool_f(pool, FF_L2, fs);
@@ -1013,29 +1026,30 @@ struct Ctx {
 // Bullet solves the two islands as one group (oracle: substep, step 4).
 CP_DEV bool c44_ok(const Ctx& c);
 CP_DEV void sweeps_c44_slow(Ctx& c, real* pool, real tol, int it0, int it1, Stamps& ST);
-template <bool C44 = false>
+template <bool C44 = false, bool PM = false>
 CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0, bool second, int it0, int it1,
                    Stamps& ST) {
     const real tol = sqrt_(real(P.residual_threshold));  // oracle: SQRT((real)threshold)
     // the ground-pole pair's tangent basis (with the URDF frictions the only island pair with
     // friction rows: the carts' friction is 0), once per substep instead of once per sweep:
     // step kernel 0.772 -> 0.753 ms
-    V3 h1, h2;
-    plane_space(c.T.n[1], h1, h2);
+    V3 h1 = mk(real(0.0), real(0.0), real(0.0)), h2 = h1;
+    if constexpr (!PM) plane_space(c.T.n[1], h1, h2);
     // ground pairs whose rows all have a +z normal in this wave run isl_row_ez (wave-uniform):
-    // the ground-pole pair in every measured wave, the ground-cart pair in ~3 of 4
+    // the ground-pole pair in every measured wave, the ground-cart pair in ~3 of 4 (PM: every row
+    // has its own normal, the generic rows)
 #ifdef CP_NO_EZ
     const bool ez0 = false, ez1 = false;
 #else
-    const bool ez0 = __ballot(pk_cnt(c.T.pk[0]) > 0 && !is_plus_z(c.T.n[0])) == 0ull;
-    const bool ez1 = __ballot(pk_cnt(c.T.pk[1]) > 0 && !is_plus_z(c.T.n[1])) == 0ull;
+    const bool ez0 = !PM && __ballot(pk_cnt(c.T.pk[0]) > 0 && !is_plus_z(c.T.n[0])) == 0ull;
+    const bool ez1 = !PM && __ballot(pk_cnt(c.T.pk[1]) > 0 && !is_plus_z(c.T.n[1])) == 0ull;
 #endif
 #ifdef CP_STAMPS
     ST.flags |= (ez0 ? 0u : 2u) | (ez1 ? 0u : 4u);
 #endif
     for (int it = it0; it < it1; ++it) {
         if (__ballot(c.active) == 0ull) break;
-        if constexpr (C44) {  // every still-active lane in the settle structure (the reset kernels)
+        if constexpr (C44 && !PM) {  // every still-active lane in the settle structure (the reset kernels)
             if ((it - it0) % 8 == 0 && __ballot(c.active && !c44_ok(c)) == 0ull) {
                 sweeps_c44_slow(c, pool, tol, it, it1, ST);
                 return;
@@ -1047,33 +1061,34 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0,
         bool bad = false, badc = false;
         if (c.active) {
             if (ez0) isl_normal_rows_ez<0>(c.I, c.T, pool, tol, bad);
-            else isl_normal_rows<0>(c.I, c.T, pool, tol, bad);
+            else isl_normal_rows<0, PM>(c.I, c.T, pool, tol, bad);
             if (ez1) isl_normal_rows_ez<1>(c.I, c.T, pool, tol, bad);
-            else isl_normal_rows<1>(c.I, c.T, pool, tol, bad);
-            isl_normal_rows<2>(c.I, c.T, pool, tol, bad);
+            else isl_normal_rows<1, PM>(c.I, c.T, pool, tol, bad);
+            isl_normal_rows<2, PM>(c.I, c.T, pool, tol, bad);
         }
         const bool cross = c.active && c.merged;  // same on both lanes of an env
         if (__ballot(cross) != 0ull && cross) {
             cross_view(S, c.T, c.I, second);
-            pair_normal_rows<5>(S, c.T, second, P, pool0, tol, badc);
-            pair_normal_rows<6>(S, c.T, second, P, pool0, tol, badc);
-            pair_normal_rows<7>(S, c.T, second, P, pool0, tol, badc);
-            pair_normal_rows<8>(S, c.T, second, P, pool0, tol, badc);
+            pair_normal_rows<5, PM>(S, c.T, second, P, pool0, tol, badc);
+            pair_normal_rows<6, PM>(S, c.T, second, P, pool0, tol, badc);
+            pair_normal_rows<7, PM>(S, c.T, second, P, pool0, tol, badc);
+            pair_normal_rows<8, PM>(S, c.T, second, P, pool0, tol, badc);
             cross_back(c.I, S, second);
         }
         if (c.active) {
             if (ez0) isl_friction_rows_ez<0>(c.I, c.T, c.mu0, pool, tol, bad);
-            else isl_friction_rows<0>(c.I, c.T, c.mu0, pool, tol, bad);
+            else isl_friction_rows<0, false, PM>(c.I, c.T, c.mu0, pool, tol, bad);
             if (ez1) isl_friction_rows_ez<1>(c.I, c.T, c.mu1, pool, tol, bad);
+            else if (PM) isl_friction_rows<1, false, PM>(c.I, c.T, c.mu1, pool, tol, bad);
             else isl_friction_rows<1, true>(c.I, c.T, c.mu1, pool, tol, bad, h1, h2);
-            isl_friction_rows<2>(c.I, c.T, c.mu2, pool, tol, bad);
+            isl_friction_rows<2, false, PM>(c.I, c.T, c.mu2, pool, tol, bad);
         }
         if (__ballot(cross) != 0ull && cross) {
             cross_view(S, c.T, c.I, second);
-            pair_friction_rows<5>(S, c.T, second, P, pool0, tol, badc);
-            pair_friction_rows<6>(S, c.T, second, P, pool0, tol, badc);
-            pair_friction_rows<7>(S, c.T, second, P, pool0, tol, badc);
-            pair_friction_rows<8>(S, c.T, second, P, pool0, tol, badc);
+            pair_friction_rows<5, PM>(S, c.T, second, P, pool0, tol, badc);
+            pair_friction_rows<6, PM>(S, c.T, second, P, pool0, tol, badc);
+            pair_friction_rows<7, PM>(S, c.T, second, P, pool0, tol, badc);
+            pair_friction_rows<8, PM>(S, c.T, second, P, pool0, tol, badc);
             cross_back(c.I, S, second);
         }
         // every lane that entered the loop is here (pairs together): the env's joint decision
@@ -1434,9 +1449,13 @@ CP_DEV void fast_store(const FastIsl& F, const Ctx& c, real* pool) {
 // PGS sweeps [it0, it1) of the lane's island.  FAST: fast-form island rows when no
 // lane of the wave has friction rows on local pairs 0 / 2 (wave-uniform choice; the
 // fast form needs the register budget of the 1-wave-per-SIMD latency kernels).
-template <bool FAST, bool C44 = false>
+template <bool FAST, bool C44 = false, bool PM = false>
 CP_DEV void solve_range(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0, bool second, int it0, int it1,
                         Stamps& ST) {
+    if constexpr (PM) {  // per-row normals: the generic rows (no fast form, no +z form, no settle loop)
+        sweeps<false, true>(c, S, P, pool, pool0, second, it0, it1, ST);
+        return;
+    }
 #ifndef CP_NO_FAST_ROWS
     if constexpr (FAST) {
         if (__ballot(!fast_ok(c)) == 0ull) {
@@ -1481,11 +1500,134 @@ CP_DEV void island_view(const Sim& S, const cp_physics& P, int isl_, Ctx& c) {
     c.mu2 = L.mu2;
 }
 
+// ---- CP_MODEL_PERSISTENT: Bullet's persistent contact manifold of one local pair (oracle:
+// persistent_manifold, pm_sort_cached).  The cache slots are registers with compile-time indices
+// (every slot choice is a select), loaded from and stored to the lane's column of Bufs::pman.
+struct PMan {
+    int cnt;
+    V3 la[4], lb[4], n[4];
+    real d[4], lam[4];
+};
+CP_DEV int pmf(int j, int off) { return j * CP_PM_PAIR_FIELDS + off; }
+// field offsets in a pair's block: count 0, la 1 + 3c, lb 13 + 3c, n 25 + 3c, d 37 + c, lam 41 + c
+CP_DEV void pm_load(const Mem& G, int j, PMan& M) {
+    M.cnt = (int)to_bits(G.lp(pmf(j, 0)));
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        M.la[c] = mk(G.lp(pmf(j, 1 + 3 * c)), G.lp(pmf(j, 2 + 3 * c)), G.lp(pmf(j, 3 + 3 * c)));
+        M.lb[c] = mk(G.lp(pmf(j, 13 + 3 * c)), G.lp(pmf(j, 14 + 3 * c)), G.lp(pmf(j, 15 + 3 * c)));
+        M.n[c] = mk(G.lp(pmf(j, 25 + 3 * c)), G.lp(pmf(j, 26 + 3 * c)), G.lp(pmf(j, 27 + 3 * c)));
+        M.d[c] = G.lp(pmf(j, 37 + c));
+        M.lam[c] = G.lp(pmf(j, 41 + c));
+    }
+}
+CP_DEV void pm_store(const Mem& G, int j, const PMan& M) {
+    G.sp(pmf(j, 0), bits_to<real>((uint32_t)M.cnt));
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        if (c < M.cnt) {
+            G.sp(pmf(j, 1 + 3 * c), M.la[c].x); G.sp(pmf(j, 2 + 3 * c), M.la[c].y); G.sp(pmf(j, 3 + 3 * c), M.la[c].z);
+            G.sp(pmf(j, 13 + 3 * c), M.lb[c].x); G.sp(pmf(j, 14 + 3 * c), M.lb[c].y); G.sp(pmf(j, 15 + 3 * c), M.lb[c].z);
+            G.sp(pmf(j, 25 + 3 * c), M.n[c].x); G.sp(pmf(j, 26 + 3 * c), M.n[c].y); G.sp(pmf(j, 27 + 3 * c), M.n[c].z);
+            G.sp(pmf(j, 37 + c), M.d[c]);
+            G.sp(pmf(j, 41 + c), M.lam[c]);
+        }
+    }
+}
+CP_DEV V3 box_local(const Box& B, V3 w) { return rot_t(B.ax, sub(w, B.c)); }
+CP_DEV V3 box_world(const Box& B, V3 l) { return add(B.c, rot(B.ax, l)); }
+CP_DEV real box_radius(const Box& B) { return sqrt_(dot(mk(B.h0, B.h1, B.h2), mk(B.h0, B.h1, B.h2))); }
+
+// btPersistentManifold::sortCachedPoints (KEEP_DEEPEST_POINT, gContactCalcArea3Points): the slot a
+// 5th point replaces (M.cnt == 4)
+CP_DEV int pm_sort_cached(const PMan& M, V3 la, real d) {
+    int deepest = -1;
+    real maxpen = d;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (M.d[i] < maxpen) { deepest = i; maxpen = M.d[i]; }
+    real res[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        // a = new - [o0], b = [o1] - [o2]: (1,3,2) (0,3,2) (0,3,1) (0,2,1)
+        const int o0 = i == 0 ? 1 : 0, o1 = i == 3 ? 2 : 3, o2 = i < 2 ? 2 : 1;
+        const V3 cr = cross(sub(la, M.la[o0]), sub(M.la[o1], M.la[o2]));
+        res[i] = i == deepest ? real(0.0) : dot(cr, cr);
+    }
+    int best = -1;
+    real bv = real(-1e30);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (abs_(res[i]) > bv) { bv = abs_(res[i]); best = i; }
+    return best;
+}
+
+// btManifoldResult::addContactPoint: the new point (world midpoint p, A->B normal n, separation d)
+// replaces the nearest cached point in A's frame within thr (keeping its impulse), or is added
+CP_DEV void pm_add(PMan& M, const Box& A, const Box& B, V3 p, V3 n, real d, real thr) {
+    const V3 pa = madd(p, n, -(d * real(0.5))), pb = madd(p, n, d * real(0.5));
+    const V3 la = box_local(A, pa), lb = box_local(B, pb);
+    real best = thr * thr;
+    int idx = -1;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        if (c < M.cnt) {
+            const V3 df = sub(M.la[c], la);
+            const real d2 = dot(df, df);
+            if (d2 < best) { best = d2; idx = c; }
+        }
+    }
+    real lam = real(0.0);
+    if (idx >= 0) {
+        lam = idx == 0 ? M.lam[0] : idx == 1 ? M.lam[1] : idx == 2 ? M.lam[2] : M.lam[3];
+    } else if (M.cnt == 4) {
+        idx = pm_sort_cached(M, la, d);
+    } else {
+        idx = M.cnt;
+        M.cnt += 1;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (q == idx) {
+            M.la[q] = la; M.lb[q] = lb; M.n[q] = n; M.d[q] = d; M.lam[q] = lam;
+        }
+    }
+}
+
+// btPersistentManifold::refreshContactPoints: separations from the current poses; a point separated
+// by more than thr, or drifted sideways by more than thr, is removed (the last slot moved in)
+CP_DEV void pm_refresh(PMan& M, const Box& A, const Box& B, real thr) {
+#pragma unroll
+    for (int c = 3; c >= 0; --c) {
+        if (c < M.cnt) {
+            const V3 pa = box_world(A, M.la[c]), pb = box_world(B, M.lb[c]);
+            const real d = dot(sub(pb, pa), M.n[c]);
+            bool keep = d <= thr;
+            if (keep) {
+                const V3 df = sub(pb, madd(pa, M.n[c], d));
+                keep = dot(df, df) <= thr * thr;
+            }
+            if (keep) {
+                M.d[c] = d;
+            } else {
+                const int last = M.cnt - 1;
+#pragma unroll
+                for (int q = c + 1; q < 4; ++q) {
+                    if (q == last) {
+                        M.la[c] = M.la[q]; M.lb[c] = M.lb[q]; M.n[c] = M.n[q]; M.d[c] = M.d[q]; M.lam[c] = M.lam[q];
+                    }
+                }
+                M.cnt = last;
+            }
+        }
+    }
+}
+
 // Phase 1 of one p.stepSimulation() (DESIGN.md §Physics model 1-5a): narrowphase and
 // row setup of the lane's island, unconstrained velocity update of the whole env,
 // the island view and the warm start.  A lane with live == false (done env, padding)
 // makes no contacts and writes nothing.
-template <bool ALLIN = false>
+template <bool ALLIN = false, bool PM = false>
 CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool, real* pool0, int& overflow,
                          const Mem& G, Stamps& ST, bool live, Ctx& c) {
     const real dt = P.dt, inv_dt = P.inv_dt;
@@ -1502,9 +1644,13 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
         const int a = GROUND ? 0 : pair_a(g);
         CP_STAMP(n0);
         // warm-start cache of the pair, loaded first: its latency overlaps the narrowphase
-        const uint32_t oid = to_bits(G.lw(CP_SF_WS_ID(0, j)));
-        const real ol0 = G.ll(CP_SF_WS_LAM(0, j, 0)), ol1 = G.ll(CP_SF_WS_LAM(0, j, 1));
-        const real ol2 = G.ll(CP_SF_WS_LAM(0, j, 2)), ol3 = G.ll(CP_SF_WS_LAM(0, j, 3));
+        uint32_t oid = 0xFFFFFFFFu;
+        real ol0 = real(0.0), ol1 = real(0.0), ol2 = real(0.0), ol3 = real(0.0);
+        if constexpr (!PM) {
+            oid = to_bits(G.lw(CP_SF_WS_ID(0, j)));
+            ol0 = G.ll(CP_SF_WS_LAM(0, j, 0)); ol1 = G.ll(CP_SF_WS_LAM(0, j, 1));
+            ol2 = G.ll(CP_SF_WS_LAM(0, j, 2)); ol3 = G.ll(CP_SF_WS_LAM(0, j, 3));
+        }
         // the island flag through a volatile empty asm per pair: the box selections below are
         // otherwise loop-invariant per branch, and hoisting all of them out of the pair loop
         // keeps every body's axes live across the narrowphase (spills)
@@ -1532,14 +1678,32 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
         C.m = 0;
         C.n = mk(real(0.0), real(0.0), real(1.0));
         CP_STAMP(n1);
-        if (live && !face_separated(A, Bx, P.contact_margin)) box_box<ALLIN>(A, Bx, P.contact_margin, P.edge_bias, C);
+        // PM: Bullet's box-box detector reports overlapping boxes only (margin 0); the manifold keeps
+        // the points within the pair's relative breaking threshold
+        const real newmargin = PM ? real(0.0) : real(P.contact_margin);
+        if (live && !face_separated(A, Bx, newmargin)) box_box<ALLIN>(A, Bx, newmargin, P.edge_bias, C);
+        PMan M;
+        M.cnt = 0;
+        if constexpr (PM) {
+            if (live) {
+                pm_load(G, j, M);
+                const real ra = box_radius(A), rb_ = box_radius(Bx);
+                const real thr = real(P.contact_margin) * (ra < rb_ ? ra : rb_);
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (k < C.m) pm_add(M, A, Bx, C.p[k], C.n, C.d[k], thr);
+                pm_refresh(M, A, Bx, thr);
+                pm_store(G, j, M);
+            }
+        }
         CP_STAMP(n2);
         CP_ACC(sel, n0, n1);
         CP_ACC(bb, n1, n2);
         const int base = used, fbase = fused;
         int m = 0, fm = 0;
         uint32_t nid = 0xFFFFFFFFu;
-        if (__ballot(C.m > 0) != 0ull) {  // row setup, skipped when no lane of the wave has a contact
+        const int npts = PM ? M.cnt : C.m;
+        if (__ballot(npts > 0) != 0ull) {  // row setup, skipped when no lane of the wave has a contact
         real mu, ima, imb;
         Sym Ma, Mb;
         pair_dispatch<GROUND>(j, [&](auto jt) {
@@ -1554,24 +1718,34 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
         });
         const V3 xa = A.c, xb = Bx.c;
         V3 t1 = mk(real(0.0), real(0.0), real(0.0)), t2 = t1;
-        if (mu > real(0.0)) plane_space(C.n, t1, t2);
+        if (!PM && mu > real(0.0)) plane_space(C.n, t1, t2);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            if (k < C.m) {
+            if (k < npts) {
                 if (base + m >= MAXP) {
                     overflow += 1;  // dropped by the island pool cap (oracle: same count)
                 } else {
                     const int s = base + m;
-                    V3 rb = sub(C.p[k], xb);
-                    real K = row_k_dyn(a, ima, imb, xa, xb, Ma, Mb, rb, C.n);
-                    real dist = C.d[k];
+                    // PM: the cached point's own point on B, normal, separation and applied impulse
+                    const V3 nk = PM ? M.n[k] : C.n;
+                    V3 rb = sub(PM ? box_world(Bx, M.lb[k]) : C.p[k], xb);
+                    real K = row_k_dyn(a, ima, imb, xa, xb, Ma, Mb, rb, nk);
+                    real dist = PM ? M.d[k] : C.d[k];
                     real tg = dist > real(0.0) ? -(dist * inv_dt) : -((P.erp * dist) * inv_dt);
                     const int id = (int)((C.ids >> (8 * k)) & 0xFFu);
                     real l0 = real(0.0);
-                    if ((int)(oid & 0xFFu) == id) l0 = ol0;
-                    else if ((int)((oid >> 8) & 0xFFu) == id) l0 = ol1;
-                    else if ((int)((oid >> 16) & 0xFFu) == id) l0 = ol2;
-                    else if ((int)((oid >> 24) & 0xFFu) == id) l0 = ol3;
+                    if constexpr (PM) {
+                        l0 = M.lam[k];
+                        pool_pn(pool, 0, s) = nk.x;
+                        pool_pn(pool, 1, s) = nk.y;
+                        pool_pn(pool, 2, s) = nk.z;
+                        if (mu > real(0.0)) plane_space(nk, t1, t2);
+                    } else {
+                        if ((int)(oid & 0xFFu) == id) l0 = ol0;
+                        else if ((int)((oid >> 8) & 0xFFu) == id) l0 = ol1;
+                        else if ((int)((oid >> 16) & 0xFFu) == id) l0 = ol2;
+                        else if ((int)((oid >> 24) & 0xFFu) == id) l0 = ol3;
+                    }
                     pool_n(pool, F_RBX, s) = rb.x;
                     pool_n(pool, F_RBY, s) = rb.y;
                     pool_n(pool, F_RBZ, s) = rb.z;
@@ -1620,7 +1794,7 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
             T.pk[q] = h ? pk : T.pk[q];
         }
 #endif
-        if (live && nid != oid) G.sw(CP_SF_WS_ID(0, j), bits_to<real>(nid));  // unchanged: no write
+        if (!PM && live && nid != oid) G.sw(CP_SF_WS_ID(0, j), bits_to<real>(nid));  // unchanged: no write
     };
 #ifdef CP_NO_GROUND_PEEL
 #pragma unroll 1
@@ -1688,13 +1862,13 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
     // rows (merged env) run on both lanes on the whole-env view after the island
     // rows of the same kind, as in the oracle.  Both lanes sweep until the env's joint
     // stopping test passes (one solver group, oracle: substep step 4).
-    isl_warmstart<0>(I, T, pool);
-    isl_warmstart<1>(I, T, pool);
-    isl_warmstart<2>(I, T, pool);
+    isl_warmstart<0, PM>(I, T, pool);
+    isl_warmstart<1, PM>(I, T, pool);
+    isl_warmstart<2, PM>(I, T, pool);
     if (__ballot(c.merged) != 0ull && c.merged) {
         cross_view(S, T, I, second);
-        pair_warmstart<5>(S, T, second, P, pool0); pair_warmstart<6>(S, T, second, P, pool0);
-        pair_warmstart<7>(S, T, second, P, pool0); pair_warmstart<8>(S, T, second, P, pool0);
+        pair_warmstart<5, PM>(S, T, second, P, pool0); pair_warmstart<6, PM>(S, T, second, P, pool0);
+        pair_warmstart<7, PM>(S, T, second, P, pool0); pair_warmstart<8, PM>(S, T, second, P, pool0);
         cross_back(I, S, second);
     }
     c.active = c.tot > 0;  // same on both lanes of the env
@@ -1703,6 +1877,7 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
 // Phase 3: whole-env velocities from the two lanes' islands (both lanes of every
 // env active), the warm-start cache refresh and the integration (DESIGN.md
 // §Physics model 5b-7).
+template <bool PM = false>
 CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx& c, real* pool, const Mem& G,
                            Stamps& ST, bool live) {
     const real dt = P.dt, inv_dt = P.inv_dt;
@@ -1724,7 +1899,7 @@ CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx
     // the substep holds 0 impulses and keeps them: it is not rewritten (the id word is a 0xFF-padded prefix,
     // the impulses past it 0, in every state the kernels and cp_init write; oracle: every slot
     // rewritten, same values)
-    if (live) {
+    if (live && !PM) {
 #pragma unroll
         for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
             const int cnt = pk_cnt(c.T.pk[j]), base = pk_base(c.T.pk[j]);
@@ -1733,6 +1908,15 @@ CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx
                 for (int k = 0; k < 4; ++k)
                     G.sl(CP_SF_WS_LAM(0, j, k), (k < cnt) ? pool_n(pool, F_LAM, base + k) : real(0.0));
             }
+        }
+    }
+    if (live && PM) {  // the solved impulses of the cached points that got a row (oracle: q->pm)
+#pragma unroll
+        for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
+            const int cnt = pk_cnt(c.T.pk[j]), base = pk_base(c.T.pk[j]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < cnt) G.sp(pmf(j, 41 + k), pool_n(pool, F_LAM, base + k));
         }
     }
     // 5. integrate positions and orientations (both lanes, whole env)
@@ -1775,16 +1959,17 @@ CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx
 // FAST: fast-form island rows where the wave allows them (the 512-register kernels);
 // C44: the latency-shaped reset kernel's options: the guard-free settle-structure loop
 // (sweeps_c44) and the all-inside face-contact exit (face_contact<ALLIN>).
-template <bool FAST = false, bool C44 = false, bool ALLIN = C44>
+// PM: CP_MODEL_PERSISTENT (Bullet's persistent manifold, per-row normals in the pool).
+template <bool FAST = false, bool C44 = false, bool ALLIN = C44, bool PM = false>
 CP_DEV void substep(Sim& S, const cp_physics& P, const Lane& L, real* pool, real* pool0, int& overflow,
                     const Mem& G, Stamps& ST, bool live = true) {
     Ctx c;
-    substep_prep<ALLIN>(S, P, L, pool, pool0, overflow, G, ST, live, c);
+    substep_prep<ALLIN, PM>(S, P, L, pool, pool0, overflow, G, ST, live, c);
     CP_STAMP(t2);
-    solve_range<FAST, C44>(c, S, P, pool, pool0, L.isl != 0, 0, P.solver_iterations, ST);
+    solve_range<FAST, C44, PM>(c, S, P, pool, pool0, L.isl != 0, 0, P.solver_iterations, ST);
     CP_STAMP(t3);
     CP_ACC(solve, t2, t3);
-    substep_finish(S, P, L, c, pool, G, ST, live);
+    substep_finish<PM>(S, P, L, c, pool, G, ST, live);
 }
 
 // LINK_FRAME force at the COM on cart (C = 0) or cart2 (C = 1): world = R(q) f

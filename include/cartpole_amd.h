@@ -118,7 +118,8 @@ typedef struct cp_physics {
 #define CP_MODEL_PERSISTENT      0x4  /* Bullet's persistent manifold (getCacheEntry matching,
                                          replaceContactPoint, sortCachedPoints,
                                          refreshContactPoints) instead of feature-id matching   */
-#define CP_MODEL_GPU_FLAGS       0x0  /* the flags the HIP kernels implement                     */
+#define CP_MODEL_GPU_FLAGS       0x4  /* the flags the HIP kernels implement (PERSISTENT: latency-shaped
+                                         kernels only; its manifolds are not part of the state SoA) */
 
 typedef struct cp_config {
     int32_t num_envs;            /* B                                          */
