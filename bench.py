@@ -181,6 +181,8 @@ def workload(args, world):
         s += ", bounds termination on (bullet_cartpole.py:243-253)"
     if args.solver_iterations is not None:
         s += f", solver_iterations={args.solver_iterations} (diagnostic)"
+    if getattr(args, "persistent", False):
+        s += ", CP_MODEL_PERSISTENT contact model (Bullet's persistent manifold; model-fidelity variant)"
     if getattr(args, "rollout", 0):
         s += f", cp_rollout launches of up to {args.rollout} steps (not the per-step cp_step headline)"
     if idx is not None:
@@ -485,6 +487,9 @@ def main():
     ap.add_argument("--rollout", type=int, default=0, metavar="K",
                     help="run the steps as cp_rollout launches of up to K steps (one launch advances every env "
                          "through K steps; a separately labelled line, not the per-step headline)")
+    ap.add_argument("--persistent", action="store_true",
+                    help="the CP_MODEL_PERSISTENT contact model (Bullet's persistent manifold; latency-shaped "
+                         "kernels; a model-fidelity variant, not the headline)")
     ap.add_argument("--solver-iterations", type=int, default=None,
                     help="override the PGS sweep cap (default: the model's 50; non-default runs are diagnostics)")
     args = ap.parse_args()
@@ -507,7 +512,8 @@ def main():
     env = BatchedCartpole(B, local, action_repeats=R, steps_per_repeat=1, max_episode_len=WINDOW,
                           initial_force=55.0, autoreset=True, seed=spec["seed"], done_on_bounds=args.done_on_bounds,
                           env_id_offset=spec["env_id_offset"], precision=args.dtype,
-                          **({} if args.solver_iterations is None else {"solver_iterations": args.solver_iterations}))
+                          **({} if args.solver_iterations is None else {"solver_iterations": args.solver_iterations}),
+                          **({"model_flags": abi.CP_MODEL_PERSISTENT} if args.persistent else {}))
     if args.raster:
         env.enable_raster(True, num_cameras=args.cameras)
     ss_steps = 0 if args.no_steady_state else WINDOW

@@ -1580,17 +1580,23 @@ CP_DEV void pm_add(PMan& M, const Box& A, const Box& B, V3 p, V3 n, real d, real
     real lam = real(0.0);
     if (idx >= 0) {
         lam = idx == 0 ? M.lam[0] : idx == 1 ? M.lam[1] : idx == 2 ? M.lam[2] : M.lam[3];
+        asm volatile("" : "+v"(lam));
     } else if (M.cnt == 4) {
         idx = pm_sort_cached(M, la, d);
     } else {
         idx = M.cnt;
         M.cnt += 1;
     }
+    // slot writes as selects per compile-time slot (a guarded write is merged into one indexed store,
+    // which puts the manifold in private memory)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        if (q == idx) {
-            M.la[q] = la; M.lb[q] = lb; M.n[q] = n; M.d[q] = d; M.lam[q] = lam;
-        }
+        const bool h = q == idx;
+        M.la[q] = selv(h, la, M.la[q]);
+        M.lb[q] = selv(h, lb, M.lb[q]);
+        M.n[q] = selv(h, n, M.n[q]);
+        M.d[q] = h ? d : M.d[q];
+        M.lam[q] = h ? lam : M.lam[q];
     }
 }
 
@@ -1607,18 +1613,18 @@ CP_DEV void pm_refresh(PMan& M, const Box& A, const Box& B, real thr) {
                 const V3 df = sub(pb, madd(pa, M.n[c], d));
                 keep = dot(df, df) <= thr * thr;
             }
-            if (keep) {
-                M.d[c] = d;
-            } else {
-                const int last = M.cnt - 1;
+            const int last = M.cnt - 1;
+            M.d[c] = keep ? d : M.d[c];
 #pragma unroll
-                for (int q = c + 1; q < 4; ++q) {
-                    if (q == last) {
-                        M.la[c] = M.la[q]; M.lb[c] = M.lb[q]; M.n[c] = M.n[q]; M.d[c] = M.d[q]; M.lam[c] = M.lam[q];
-                    }
-                }
-                M.cnt = last;
+            for (int q = c + 1; q < 4; ++q) {  // removal: the last slot moves into slot c (selects)
+                const bool h = !keep && q == last;
+                M.la[c] = selv(h, M.la[q], M.la[c]);
+                M.lb[c] = selv(h, M.lb[q], M.lb[c]);
+                M.n[c] = selv(h, M.n[q], M.n[c]);
+                M.d[c] = h ? M.d[q] : M.d[c];
+                M.lam[c] = h ? M.lam[q] : M.lam[c];
             }
+            M.cnt = keep ? M.cnt : last;
         }
     }
 }

@@ -1084,7 +1084,7 @@ static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* i
                 if (q->pm >= 0) S->pm[p][j].lam[q->pm] = q->lam;
             }
         }
-    for (int p = 0; p < CP_NUM_ISLANDS; ++p) {
+    for (int p = 0; p < CP_NUM_ISLANDS && !persistent; ++p) {   /* feature-id cache: default model only */
         for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
             manifold_t* m = &isl[p].man[j];
             uint32_t idw = 0xFFFFFFFFu;

@@ -43,18 +43,27 @@ def _np(t):
 
 
 def _assert_same(a, b, what):
-    """Bit-exact: float32 arrays are compared as their uint32 bits (-0.0 != +0.0, NaN bits)."""
+    """Bit-exact: float32 arrays are compared as their uint32 bits (-0.0 != +0.0); a NaN must be a
+    NaN on both sides (its payload is the hardware's default NaN: gfx950 and x86 differ)."""
     a, b = np.asarray(a), np.asarray(b)
     if a.dtype == np.float32 and b.dtype == np.float32:
-        same = np.array_equal(np.ascontiguousarray(a).view(np.uint32), np.ascontiguousarray(b).view(np.uint32))
+        na, nb = np.isnan(a), np.isnan(b)
+        ua = np.where(na, np.uint32(0x7FC00000), np.ascontiguousarray(a).view(np.uint32))
+        ub = np.where(nb, np.uint32(0x7FC00000), np.ascontiguousarray(b).view(np.uint32))
+        same = np.array_equal(ua, ub)
     else:
         same = np.array_equal(a, b, equal_nan=True)
     if not same:
         d = np.abs(a.astype(np.float64) - b.astype(np.float64))
         idx = np.unravel_index(np.nanargmax(d), d.shape)
-        nbits = np.count_nonzero(np.ascontiguousarray(a).view(np.uint32) != np.ascontiguousarray(b).view(np.uint32)) \
-            if a.dtype == b.dtype == np.float32 else np.count_nonzero(d)
-        raise AssertionError(f"{what}: {nbits} elements differ, max |diff| {np.nanmax(d):.3e} at {idx}")
+        if a.dtype == b.dtype == np.float32:
+            diff = ua != ub
+        else:
+            diff = d != 0
+        where = [tuple(int(x) for x in w) for w in np.argwhere(diff)[:6]]
+        vals = [(float(a[w]), float(b[w])) for w in where]
+        raise AssertionError(f"{what}: {int(diff.sum())} elements differ, max |diff| {np.nanmax(d):.3e} at {idx}; "
+                             f"first {where} (gpu, oracle) {vals}")
 
 
 def _compare_state(gpu, orc, what):
