@@ -234,13 +234,50 @@ def timed(env, actions, t0, K, world, dev, gather_at_end, rollout=0):
 
 
 # ----------------------------------------------------------------- CPU legs
+def host_cpus():
+    """The CPUs this process may actually use: the affinity mask, capped by the cgroup CPU quota
+    (cgroup v2 cpu.max or v1 cfs_quota_us) and by OMP_NUM_THREADS when the launcher sets it to the
+    process's CPU share.  On the GPU box the mask lists the whole machine (256) while the share is
+    16: 256 OpenMP threads on 16 CPUs time-slice through every per-step barrier (16 k env-steps/s
+    measured, rd3f) instead of using the 16 CPUs."""
+    import math
+    info = {"nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)), "cgroup_quota_cpus": None,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                info["cgroup_quota_cpus"] = math.ceil(int(q) / int(per))
+        except (OSError, ValueError):
+            pass
+    if info["cgroup_quota_cpus"] is None:
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                info["cgroup_quota_cpus"] = math.ceil(q / per)
+        except (OSError, ValueError):
+            pass
+    n = info["affinity_cpus"]
+    if info["cgroup_quota_cpus"]:
+        n = min(n, info["cgroup_quota_cpus"])
+    try:
+        if info["omp_num_threads"]:
+            n = min(n, int(info["omp_num_threads"]))
+    except ValueError:
+        pass
+    info["usable_cpus"] = max(1, n)
+    return info
+
+
 def cpu_baseline(R, budget_s):
     """The oracle (port) on the host, -O3 -march=native: C3 on all cores, C3 on one core,
     C1 (B = 1, R = 2) on one core; each a bounded sample of about budget_s seconds."""
     import numpy as np
 
     from oracle import oracle as O
-    all_cpus = len(os.sched_getaffinity(0))
+    cpus = host_cpus()
+    all_cpus = cpus["usable_cpus"]
     lib = O.load("native")
 
     def run(B, steps, threads_, R_, seed):
@@ -281,7 +318,7 @@ def cpu_baseline(R, budget_s):
                 "sample": f"{max(B, 64)} envs x {steps} steps ({dt:.1f} s)"}
 
     omp = sized(all_cpus, budget_s)
-    t16 = sized(min(16, all_cpus), budget_s / 2)
+    t16 = sized(16, budget_s / 2) if all_cpus > 16 else omp
     one = sized(1, budget_s / 2)
     # C1: B = 1, R = 2 (reference default), discrete random actions, seeds 0..9, autoreset
     c1_steps, c1_t = 0, 0.0
@@ -294,7 +331,8 @@ def cpu_baseline(R, budget_s):
     return {"value": omp["value"], "unit": "env-steps/s", "cores": omp["cores"], "kind": "port",
             "sample": (f"oracle/cp_oracle.c fp32 built gcc -O3 -march=native (same algorithm; bit-identical "
                        f"to the parity build: {same}), C3 workload (R={R}, discrete random actions, autoreset "
-                       f"incl.), OpenMP on {omp['cores']} threads (every CPU of the affinity mask): "
+                       f"incl.), OpenMP on {omp['cores']} threads (every CPU the process may use: the "
+                       f"affinity mask capped by the cgroup quota and the launcher's OMP_NUM_THREADS share): "
                        f"{omp['sample']}"),
             "threads_16": {"value": t16["value"], "unit": "env-steps/s", "cores": t16["cores"],
                            "sample": "C3 workload, " + t16["sample"]},
@@ -303,7 +341,7 @@ def cpu_baseline(R, budget_s):
             "c1_single_thread": {"value": round(c1_steps / c1_t, 1), "unit": "env-steps/s", "cores": 1,
                                  "sample": f"C1: B=1, R=2, discrete random actions, seeds 0..{seed}, "
                                            f"{c1_steps} steps incl. {c1_steps // WINDOW} resets ({c1_t:.1f} s)"},
-            "nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            **cpus,
             "pybullet": "not importable (SURVEY.md §8c): the reference's own CPU path cannot be timed here"}
 
 

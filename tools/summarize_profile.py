@@ -21,6 +21,9 @@ def kernel_key(name):
         kind = "discrete" if ("<1>" in name or "<1," in name) else "continuous"
         lqr = ",lqr" if ("<1, true" in name or "<0, true" in name) else ""
         return f"{ns}cp_step_kernel<{kind}{lqr}>"
+    if "cp_rollout_kernel" in name:
+        kind = "discrete" if ("<1>" in name or "<1," in name) else "continuous"
+        return f"{ns}cp_rollout_kernel<{kind}>"
     if "cp_reset_kernel" in name:
         return f"{ns}cp_reset_kernel"
     for k in ("cp_init_kernel", "cp_mask_to_list_kernel", "cp_render_small_kernel",
