@@ -181,6 +181,10 @@ def workload(args, world):
         s += ", bounds termination on (bullet_cartpole.py:243-253)"
     if args.solver_iterations is not None:
         s += f", solver_iterations={args.solver_iterations} (diagnostic)"
+    if getattr(args, "streams", 1) > 1:
+        s += f", as {args.streams} shard handles of {B // args.streams:,} envs on {args.streams} HIP streams"
+    if getattr(args, "shape", "auto") != "auto":
+        s += f", kernel shape {args.shape}"
     if getattr(args, "persistent", False):
         s += ", CP_MODEL_PERSISTENT contact model (Bullet's persistent manifold; model-fidelity variant)"
     if getattr(args, "rollout", 0):
@@ -188,6 +192,80 @@ def workload(args, world):
     if idx is not None:
         s += f" (BASELINE.json configs[{idx}])"
     return name, s
+
+
+class StreamShards:
+    """`--streams S`: the GPU's batch as S shard handles of B/S envs (the C4 shard rule inside one
+    GPU: one seed, env_id_offset = global id of the shard's first env, actions keyed by global env
+    id, so every env computes exactly what it computes in one B-env handle), each stepped on its
+    own HIP stream.  One cp_step per shard per step; a shard's next step starts as soon as ITS
+    previous step is done, so the tail of one shard's launch overlaps the other shards' waves.
+    Exposes the subset of BatchedCartpole that main() uses."""
+
+    def __init__(self, S, B, device, env_id_offset, **kw):
+        assert B % S == 0, "--streams must divide the batch"
+        self.S, self.b = S, B // S
+        self.envs = [BatchedCartpole(self.b, device, env_id_offset=env_id_offset + k * self.b, **kw) for k in range(S)]
+        self.streams = [torch.cuda.Stream(self.envs[0].device) for _ in range(S)]
+        self.cfg = self.envs[0].cfg
+        self.device = self.envs[0].device
+
+    def _each(self, fn):
+        cur = torch.cuda.current_stream(self.device)
+        out = []
+        for e, st in zip(self.envs, self.streams):
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                out.append(fn(e))
+        for st in self.streams:
+            cur.wait_stream(st)
+        return out
+
+    def set_kernel_shape(self, step, reset):
+        for e in self.envs:
+            e.set_kernel_shape(step, reset)
+
+    def kernel_shape(self):
+        return self.envs[0].kernel_shape()
+
+    def reset(self):
+        self._each(lambda e: e.reset())
+
+    def step(self, actions):
+        # no cross-stream waits between steps: each shard's stream orders its own steps
+        for k, (e, st) in enumerate(zip(self.envs, self.streams)):
+            with torch.cuda.stream(st):
+                e.step(actions[k * self.b:(k + 1) * self.b])
+
+    def rollout(self, actions):
+        for k, (e, st) in enumerate(zip(self.envs, self.streams)):
+            with torch.cuda.stream(st):
+                e.rollout(actions[:, k * self.b:(k + 1) * self.b])
+
+    def episode_returns(self):
+        rs = self._each(lambda e: e.episode_returns())
+        return torch.cat([r for r, _ in rs]), torch.cat([n for _, n in rs])
+
+    def get_state(self):
+        return torch.cat(self._each(lambda e: e.get_state()), dim=1)
+
+    def timing_begin(self, n):
+        for e in self.envs:
+            e.timing_begin(n)
+
+    def timing_stride(self, a, b):
+        for e in self.envs:
+            e.timing_stride(a, b)
+
+    def timing_end(self):
+        ts = [e.timing_end() for e in self.envs]
+        out = {k: sum(t[k] for t in ts) / len(ts) for k in ("step_ms", "reset_ms", "render_ms")}
+        out.update({k: ts[0][k] for k in ("step_launches", "reset_launches", "render_launches")})
+        return out
+
+    def close(self):
+        for e in self.envs:
+            e.close()
 
 
 def episodes(env):
@@ -525,6 +603,11 @@ def main():
     ap.add_argument("--rollout", type=int, default=0, metavar="K",
                     help="run the steps as cp_rollout launches of up to K steps (one launch advances every env "
                          "through K steps; a separately labelled line, not the per-step headline)")
+    ap.add_argument("--streams", type=int, default=1, metavar="S",
+                    help="run the GPU's batch as S shard handles on S HIP streams (the C4 shard rule inside one "
+                         "GPU; each env computes what it computes in one handle)")
+    ap.add_argument("--shape", choices=("auto", "throughput", "latency"), default="auto",
+                    help="kernel shapes (cp_set_kernel_shape) of the step and autoreset kernels")
     ap.add_argument("--persistent", action="store_true",
                     help="the CP_MODEL_PERSISTENT contact model (Bullet's persistent manifold; latency-shaped "
                          "kernels; a model-fidelity variant, not the headline)")
@@ -547,11 +630,16 @@ def main():
 
     B, R, K, W = args.batch, args.repeats, args.steps, args.warmup
     spec = shard_spec(B, rank, world, seed=SEED)
-    env = BatchedCartpole(B, local, action_repeats=R, steps_per_repeat=1, max_episode_len=WINDOW,
-                          initial_force=55.0, autoreset=True, seed=spec["seed"], done_on_bounds=args.done_on_bounds,
-                          env_id_offset=spec["env_id_offset"], precision=args.dtype,
-                          **({} if args.solver_iterations is None else {"solver_iterations": args.solver_iterations}),
-                          **({"model_flags": abi.CP_MODEL_PERSISTENT} if args.persistent else {}))
+    env_kw = dict(action_repeats=R, steps_per_repeat=1, max_episode_len=WINDOW, initial_force=55.0, autoreset=True,
+                  seed=spec["seed"], done_on_bounds=args.done_on_bounds, precision=args.dtype,
+                  **({} if args.solver_iterations is None else {"solver_iterations": args.solver_iterations}),
+                  **({"model_flags": abi.CP_MODEL_PERSISTENT} if args.persistent else {}))
+    if args.streams > 1:
+        env = StreamShards(args.streams, B, local, spec["env_id_offset"], **env_kw)
+    else:
+        env = BatchedCartpole(B, local, env_id_offset=spec["env_id_offset"], **env_kw)
+    if args.shape != "auto":
+        env.set_kernel_shape(args.shape, args.shape)
     if args.raster:
         env.enable_raster(True, num_cameras=args.cameras)
     ss_steps = 0 if args.no_steady_state else WINDOW
