@@ -189,6 +189,10 @@ def workload(args, world):
         s += ", CP_MODEL_PERSISTENT contact model (Bullet's persistent manifold; model-fidelity variant)"
     if getattr(args, "rollout", 0):
         s += f", cp_rollout launches of up to {args.rollout} steps (not the per-step cp_step headline)"
+    if getattr(args, "autoreset", "same_step") == "next_step":
+        s += (", NEXT_STEP autoreset (gymnasium >= 1.0 / envpool semantics: a finishing env's reset is handed "
+              "out by the next call and runs on a library stream in between; value counts simulated env-steps "
+              "only, not those reset-only calls)")
     if idx is not None:
         s += f" (BASELINE.json configs[{idx}])"
     return name, s
@@ -274,6 +278,23 @@ def episodes(env):
     if st.dtype == torch.float64:
         return st.view(torch.int32)[0::2].to(torch.int64)
     return st.view(torch.int32).to(torch.int64)
+
+
+def pending(env):
+    """CP_AUTORESET_NEXT_STEP: envs whose reset ran (or is in flight) and is handed out by the next step."""
+    st = env.get_state()[abi.CP_SF_DONE]
+    d = st.view(torch.int32)[0::2] if st.dtype == torch.float64 else st.view(torch.int32)
+    return int((d >= 2).sum().item())
+
+
+def simulated_steps(env, B, K, ep0, p0, next_step):
+    """Env-steps simulated by K calls: B*K, less the calls that only hand out a NEXT_STEP reset (the
+    resets launched before the window's end, minus the ones still pending after it, plus the ones
+    pending at its start).  -> (env-steps, resets run in the window)."""
+    ran = int((episodes(env) - ep0).sum().item())
+    if not next_step:
+        return B * K, ran
+    return B * K - (ran + p0 - pending(env)), ran
 
 
 def timed(env, actions, t0, K, world, dev, gather_at_end, rollout=0):
@@ -611,11 +632,17 @@ def main():
     ap.add_argument("--persistent", action="store_true",
                     help="the CP_MODEL_PERSISTENT contact model (Bullet's persistent manifold; latency-shaped "
                          "kernels; a model-fidelity variant, not the headline)")
+    ap.add_argument("--autoreset", choices=("same_step", "next_step"), default="same_step",
+                    help="same_step: a finishing env is reset in its step (the headline); next_step: the reset is "
+                         "handed out by the next step (gymnasium >= 1.0 / envpool), overlapped with the steps")
     ap.add_argument("--solver-iterations", type=int, default=None,
                     help="override the PGS sweep cap (default: the model's 50; non-default runs are diagnostics)")
     args = ap.parse_args()
     if args.batch is None:
         args.batch = 4096 if args.continuous else 65536
+    next_step = args.autoreset == "next_step"
+    if next_step and (args.rollout or args.raster or args.streams > 1):
+        ap.error("--autoreset next_step steps through cp_step only (no --rollout / --raster / --streams)")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -630,8 +657,8 @@ def main():
 
     B, R, K, W = args.batch, args.repeats, args.steps, args.warmup
     spec = shard_spec(B, rank, world, seed=SEED)
-    env_kw = dict(action_repeats=R, steps_per_repeat=1, max_episode_len=WINDOW, initial_force=55.0, autoreset=True,
-                  seed=spec["seed"], done_on_bounds=args.done_on_bounds, precision=args.dtype,
+    env_kw = dict(action_repeats=R, steps_per_repeat=1, max_episode_len=WINDOW, initial_force=55.0,
+                  autoreset=args.autoreset, seed=spec["seed"], done_on_bounds=args.done_on_bounds, precision=args.dtype,
                   **({} if args.solver_iterations is None else {"solver_iterations": args.solver_iterations}),
                   **({"model_flags": abi.CP_MODEL_PERSISTENT} if args.persistent else {}))
     if args.streams > 1:
@@ -651,30 +678,33 @@ def main():
     log(f"rank {rank}: B={B} R={R} warmup {W} done; timing {K} steps")
 
     ep0 = episodes(env)
+    p0 = pending(env) if next_step else 0
     env.timing_begin(K)
     env.timing_stride(1 if args.rollout else STEP_EVENT_STRIDE, 1)
     elapsed, hist, gathers = timed(env, actions, W, K, world, dev, gather_at_end=world > 1, rollout=args.rollout)
     tm = env.timing_end()
-    resets = int((episodes(env) - ep0).sum().item())
+    simulated, resets = simulated_steps(env, B, K, ep0, p0, next_step)
 
     steady = None
     if ss_steps:
         ep1 = episodes(env)
+        p1 = pending(env) if next_step else 0
         el2, hist2, g2 = timed(env, actions, W + K, ss_steps, world, dev, gather_at_end=world > 1,
                                rollout=args.rollout)
-        r2 = torch.tensor([int((episodes(env) - ep1).sum().item())], device=dev, dtype=torch.int64)
+        sim2, ran2 = simulated_steps(env, B, ss_steps, ep1, p1, next_step)
+        r2 = torch.tensor([ran2, sim2], device=dev, dtype=torch.int64)
         if world > 1:
             dist.all_reduce(r2)
         steady = {"steps": ss_steps, "ms_per_step": round(el2 / ss_steps * 1e3, 4),
-                  "value": round(world * B * ss_steps / el2, 1), "resets": int(r2.item()), "collectives": g2,
+                  "value": round(int(r2[1].item()) / el2, 1), "resets": int(r2[0].item()), "collectives": g2,
                   "note": "one full 200-step episode cycle (its autoreset burst included) right after the timed "
                           "window, timed the same way"}
         hist = hist2 if hist2 is not None else hist
 
-    rt = torch.tensor([resets], device=dev, dtype=torch.int64)
+    rt = torch.tensor([resets, simulated], device=dev, dtype=torch.int64)
     if world > 1:
         dist.all_reduce(rt)
-    value = world * B * K / elapsed
+    value = int(rt[1].item()) / elapsed   # = world * B * K / elapsed except for NEXT_STEP's reset-only calls
     kind = "continuous" if args.continuous else "discrete"
     per_launch_s = tm["step_ms"] / max(1, tm["step_launches"]) / 1e3
     bytes_launch = B * step_kernel_bytes(R, 16 if args.continuous else 2, 8 if args.dtype == "f64" else 4)
@@ -722,7 +752,9 @@ def main():
                    "parallelism": f"dp{world} (independent env shards, no per-step collective)",
                    "solver_iterations": env.cfg.phys.solver_iterations,
                    "residual_threshold": env.cfg.phys.residual_threshold},
-        "resets_in_window": int(rt.item()),
+        "resets_in_window": int(rt[0].item()),
+        "autoreset": args.autoreset,
+        **({"simulated_env_steps": int(rt[1].item()), "calls_x_envs": world * B * K} if next_step else {}),
         "collectives_in_window": gathers if world > 1 else 0,
         "rccl_world_size": rccl_world,
         "steady_state": steady,

@@ -5,7 +5,7 @@ library's entry points with these types.
 """
 import ctypes as C
 
-CP_ABI_VERSION = 3
+CP_ABI_VERSION = 4
 
 CP_BODY_GROUND, CP_BODY_CART, CP_BODY_POLE, CP_BODY_CART2, CP_BODY_POLE2 = range(5)
 CP_NUM_BODIES = 5
@@ -43,6 +43,8 @@ def CP_SF_WS_LAM(isl, j, k):
 
 
 CP_STATE_FIELDS = CP_SF_STEPS + 3 + CP_NUM_PAIRS * 5
+
+CP_AUTORESET_OFF, CP_AUTORESET_SAME_STEP, CP_AUTORESET_NEXT_STEP = 0, 1, 2
 
 CP_BUMP_PHILOX = 0
 CP_BUMP_HOST = 1

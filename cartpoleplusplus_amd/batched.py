@@ -8,12 +8,30 @@ outputs as PyTorch-ROCm tensors resident in HBM.
 
 One call of `step` is one env-step for every env: R x S physics substeps fused in
 one kernel launch (plus one compacted reset launch when autoreset is on).
+
+autoreset: False / "off"; True / "same_step" (a finishing env is reset in its step: obs holds
+the new episode's first obs, terminal_obs the finishing obs); "next_step" (gymnasium >= 1.0 /
+envpool: the step returns the finishing obs with done; the next step returns the new episode's
+first obs with reward 0, done 0 and ignores that env's action; the reset itself runs on a
+library stream in between, overlapped with the other envs' steps).
 """
 import ctypes as C
 
 import torch
 
 from . import abi, native
+
+AUTORESET = {False: abi.CP_AUTORESET_OFF, "off": abi.CP_AUTORESET_OFF, True: abi.CP_AUTORESET_SAME_STEP,
+             "same_step": abi.CP_AUTORESET_SAME_STEP, "next_step": abi.CP_AUTORESET_NEXT_STEP}
+
+
+def autoreset_mode(x):
+    """cp_config.autoreset for False / True / "off" / "same_step" / "next_step" (or the int itself)."""
+    if isinstance(x, int) and not isinstance(x, bool) and x in AUTORESET.values():
+        return x
+    if x not in AUTORESET:
+        raise ValueError(f"autoreset must be one of {sorted(map(str, AUTORESET))}, got {x!r}")
+    return AUTORESET[x]
 
 
 def _ptr(t):
@@ -51,7 +69,7 @@ class BatchedCartpole:
                 steps_per_repeat=int(steps_per_repeat), max_episode_len=int(max_episode_len),
                 action_force=float(action_force), initial_force=float(initial_force),
                 random_theta=int(bool(random_theta)), done_on_bounds=int(bool(done_on_bounds)),
-                autoreset=int(bool(autoreset)), seed=int(seed), env_id_offset=int(env_id_offset),
+                autoreset=autoreset_mode(autoreset), seed=int(seed), env_id_offset=int(env_id_offset),
                 bump_mode=abi.CP_BUMP_HOST if bump_mode == "host" else abi.CP_BUMP_PHILOX)
             if precision not in ("f32", "f64"):
                 raise ValueError(f"precision must be 'f32' or 'f64', got {precision!r}")

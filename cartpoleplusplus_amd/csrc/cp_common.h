@@ -120,6 +120,9 @@ struct Bufs {
     int32_t* rcount;   // [1]
     uint8_t* stepped;  // [B] 1 = simulated by the last cp_step (event log: done-before envs are not logged)
     void* pman;        // [CP_PM_FIELDS][2B] real: persistent manifolds (CP_MODEL_PERSISTENT handles only)
+    int32_t npar;      // CP_AUTORESET_NEXT_STEP: the reset list this call appends to (0 / 1); a finishing
+                       // env's done field becomes 2 + npar until the next call returns its reset obs
+    int32_t keep_done; // reset kernel: leave the done field (NEXT_STEP's in-flight reset; the fixup clears it)
 };
 
 }  // namespace cpc
@@ -130,6 +133,11 @@ struct Bufs {
     namespace NS {                                                                                               \
     void launch_init(const cp_config& cfg, const cpc::Bufs& b, hipStream_t st);                                  \
     void launch_reset(bool lat, const cp_config& cfg, const cpc::Bufs& b, float* obs_out, hipStream_t st);      \
+    void launch_nextstep_fixup(const cp_config& cfg, const cpc::Bufs& b, const int32_t* list, const int32_t* count, \
+                               int q, const float* nobs, float* obs_out, float* reward_out, uint8_t* done_out,    \
+                               hipStream_t st);                                                                    \
+    void launch_nextstep_resolve(const cp_config& cfg, const cpc::Bufs& b, const uint8_t* mask, const float* nobs, \
+                                 float* obs_out, hipStream_t st);                                                  \
     void launch_step(bool lat, int kind, const cp_config& cfg, const cpc::Bufs& b, const void* actions,          \
                      float* obs_out, float* reward_out, uint8_t* done_out, float* term_out, float* readback,    \
                      int rb_bug, const cpc::Lqr& lq, hipStream_t st);                                            \

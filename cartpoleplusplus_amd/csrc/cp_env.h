@@ -328,7 +328,7 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
 #pragma unroll
         for (int f = 0; f < 14; ++f) o[r * 14 + f] = row[f];
     sti(G.st, CP_SF_STEPS, G.off, 0);
-    sti(G.st, CP_SF_DONE, G.off, 0);
+    if (!b.keep_done) sti(G.st, CP_SF_DONE, G.off, 0);  // NEXT_STEP in flight: the fixup kernel clears it
     sti(G.st, CP_SF_EPISODE, G.off, episode + 1);
     b.ret_acc[i] = 0.0f;
 }
@@ -360,9 +360,13 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
         const SoaF term = SoaF::make(b.term_obs, B, R * 14);
         const uint32_t toff = SoaF::eoff(i);
         float* obs = obs_out + (size_t)i * R * 14;
-        const bool was_done = ldi(G.st, CP_SF_DONE, G.off) != 0;
+        const int done_field = ldi(G.st, CP_SF_DONE, G.off);
+        const bool was_done = done_field != 0;
         if (lead) b.stepped[i] = was_done ? 0 : 1;
-        if (was_done) {  // step after done (bullet_cartpole.py:179-181)
+        if (cfg.autoreset == CP_AUTORESET_NEXT_STEP && done_field >= 2) {
+            // finished in the previous call, reset on the library's second stream: this call's
+            // outputs for it come from cp_nextstep_fixup_kernel, its action is ignored
+        } else if (was_done) {  // step after done (bullet_cartpole.py:179-181)
             if (lead) {
                 for (int f = 0; f < R * 14; ++f) obs[f] = term.ld(f, toff);
                 reward_out[i] = 0.0f;
@@ -440,7 +444,7 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
                     for (int f = 0; f < R * 14; ++f) term.st(f, toff, obs[f]);
                     if (term_out)
                         for (int f = 0; f < R * 14; ++f) term_out[(size_t)i * R * 14 + f] = obs[f];
-                    sti(G.st, CP_SF_DONE, G.off, 1);
+                    sti(G.st, CP_SF_DONE, G.off, cfg.autoreset == CP_AUTORESET_NEXT_STEP ? 2 + b.npar : 1);
                     want_reset = cfg.autoreset != 0;
                 } else {
                     b.ret_acc[i] = ret;
@@ -691,11 +695,72 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
     if (ov) b.overflow[i] += ov;
 }
 
+// CP_AUTORESET_NEXT_STEP, in the call after an env finished (list q = the previous call's reset
+// list, whose reset kernel ran on the library's second stream and has completed): the new episode's
+// first obs (written by that reset kernel into nobs), reward 0, done 0; the done field is cleared,
+// so the env steps again from the next call.  An env whose done field is no longer 2 + q was
+// resolved by a cp_reset in between and is skipped.
+__global__ void __launch_bounds__(256) cp_nextstep_fixup_kernel(cp_config cfg, Bufs b, const int32_t* list,
+                                                                 const int32_t* count, int q, const float* nobs,
+                                                                 float* obs_out, float* reward_out, uint8_t* done_out) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= *count) return;
+    const int i = list[t];
+    const Soa st = Soa::make(b.state, cfg.num_envs, CP_STATE_FIELDS);
+    const uint32_t o = Soa::eoff(i);
+    if (ldi(st, CP_SF_DONE, o) != 2 + q) return;
+    const size_t n = (size_t)cfg.action_repeats * 14;
+    for (size_t f = 0; f < n; ++f) obs_out[(size_t)i * n + f] = nobs[(size_t)i * n + f];
+    reward_out[i] = 0.0f;
+    done_out[i] = 0;
+    sti(st, CP_SF_DONE, o, 0);
+}
+
+// cp_reset of a NEXT_STEP handle: a masked env whose reset is already done (done field >= 2)
+// returns that reset's obs and is not reset again (one reset from its terminal state, as a lazy
+// reset would give); the other masked envs go to the reset list (wave ballot compaction).
+__global__ void __launch_bounds__(256) cp_nextstep_resolve_kernel(cp_config cfg, Bufs b, const uint8_t* mask,
+                                                                   const float* nobs, float* obs_out) {
+    const int B = cfg.num_envs;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool want = false;
+    if (i < B && (mask == nullptr || mask[i] != 0)) {
+        const Soa st = Soa::make(b.state, B, CP_STATE_FIELDS);
+        const uint32_t o = Soa::eoff(i);
+        if (ldi(st, CP_SF_DONE, o) >= 2) {
+            const size_t n = (size_t)cfg.action_repeats * 14;
+            for (size_t f = 0; f < n; ++f) obs_out[(size_t)i * n + f] = nobs[(size_t)i * n + f];
+            sti(st, CP_SF_DONE, o, 0);
+        } else {
+            want = true;
+        }
+    }
+    const uint64_t bal = __ballot(want);
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int n = __popcll(bal);
+    int base = 0;
+    if (lane == 0 && n) base = atomicAdd(b.count, n);
+    base = __shfl(base, 0);
+    if (want) b.list[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
+}
+
 // ---------------------------------------------------------------- host launchers
 static inline unsigned env_grid(int n, int block) { return (unsigned)((n + block - 1) / block); }
 
 void launch_init(const cp_config& cfg, const Bufs& b, hipStream_t st) {
     hipLaunchKernelGGL(cp_init_kernel, dim3(env_grid(cfg.num_envs, 256)), dim3(256), 0, st, cfg, b);
+}
+
+void launch_nextstep_fixup(const cp_config& cfg, const Bufs& b, const int32_t* list, const int32_t* count, int q,
+                           const float* nobs, float* obs_out, float* reward_out, uint8_t* done_out, hipStream_t st) {
+    hipLaunchKernelGGL(cp_nextstep_fixup_kernel, dim3(env_grid(cfg.num_envs, 256)), dim3(256), 0, st, cfg, b, list,
+                       count, q, nobs, obs_out, reward_out, done_out);
+}
+
+void launch_nextstep_resolve(const cp_config& cfg, const Bufs& b, const uint8_t* mask, const float* nobs,
+                             float* obs_out, hipStream_t st) {
+    hipLaunchKernelGGL(cp_nextstep_resolve_kernel, dim3(env_grid(cfg.num_envs, 256)), dim3(256), 0, st, cfg, b, mask,
+                       nobs, obs_out);
 }
 
 void launch_reset(bool lat, const cp_config& cfg, const Bufs& b, float* obs_out, hipStream_t st) {

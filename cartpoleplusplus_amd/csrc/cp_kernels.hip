@@ -150,8 +150,18 @@ struct cp_handle {
     cp_timing timing;
     cp_raster_config raster;
     uint16_t* pixels;  // raster obs output (NULL: raster off)
-    int32_t* count2;   // [2] reset-list counters, alternating by call: each reset launch zeroes the other one
+    int32_t* count2;   // [3] reset-list counters: [0] [1] alternating by call (SAME_STEP: each reset launch
+                       // zeroes the other one; NEXT_STEP: one per reset list), [2] NEXT_STEP's cp_reset list
     int par;           // counter the next call appends to
+    // CP_AUTORESET_NEXT_STEP: the two reset lists (by call parity), the side stream each one's reset
+    // kernel runs on, the events that fork it after the step kernel and join it back, the reset obs
+    // the fixup kernel hands out, and the list whose reset is in flight (-1: none)
+    int32_t* nlist[2];
+    hipStream_t nstream[2];
+    hipEvent_t nfork[2], njoin[2];
+    float* nobs;
+    int npar;
+    int ninflight;
     int reset_lat;     // 1: latency-shaped autoreset kernel (episodes end at different steps)
     int step_lat;      // 1: latency-shaped step kernel (every wave gets a SIMD of its own)
     int reset_req;     // cp_set_kernel_shape request (CP_SHAPE_AUTO: choose_reset_shape decides)
@@ -289,6 +299,9 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
         return fail(nullptr, "cp_create: phys.model_flags names a model alternative the HIP kernels do not "
                              "implement (oracle-only, DESIGN.md §3)");
     if (!(cfg->phys.residual_threshold >= 0.0f)) return fail(nullptr, "cp_create: negative residual_threshold");
+    if (cfg->autoreset != CP_AUTORESET_OFF && cfg->autoreset != CP_AUTORESET_SAME_STEP &&
+        cfg->autoreset != CP_AUTORESET_NEXT_STEP)
+        return fail(nullptr, "cp_create: autoreset must be CP_AUTORESET_OFF, _SAME_STEP or _NEXT_STEP");
     if (cfg->precision != CP_PRECISION_F32 && cfg->precision != CP_PRECISION_F64)
         return fail(nullptr, "cp_create: precision must be CP_PRECISION_F32 or CP_PRECISION_F64");
     if ((unsigned long long)cfg->num_envs * CP_STATE_FIELDS * (cfg->precision == CP_PRECISION_F64 ? 8ull : 4ull) >= (1ull << 32) ||
@@ -303,6 +316,8 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     h->lqr = cpc::Lqr{nullptr, 0, nullptr, 0.0f, 0.0f};
     h->f64 = cfg->precision == CP_PRECISION_F64;
     h->pixels = nullptr;
+    h->npar = 0;
+    h->ninflight = -1;
     h->reset_req = h->step_req = CP_SHAPE_AUTO;
     choose_reset_shape(h);
     cp_default_raster_config(&h->raster);
@@ -328,7 +343,7 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     CP_ALLOC(h->b.last_len, B * sizeof(int32_t));
     CP_ALLOC(h->b.overflow, B * sizeof(int32_t));
     CP_ALLOC(h->b.list, B * sizeof(int32_t));
-    CP_ALLOC(h->count2, 2 * sizeof(int32_t));
+    CP_ALLOC(h->count2, 3 * sizeof(int32_t));
     CP_ALLOC(h->b.scratch, (size_t)4 * CP_ISLAND_PAIRS * 2 * B * rb);
     CP_ALLOC(h->b.stamps, CP_STAMP_SLOTS * sizeof(uint64_t));
     CP_ALLOC(h->b.stepped, B * sizeof(uint8_t));
@@ -337,8 +352,23 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
         e = hipMemset(h->b.pman, 0, (size_t)CP_PM_FIELDS * 2 * B * rb);
         if (e != hipSuccess) return fail_free(e, "hipMemset");
     }
+    if (cfg->autoreset == CP_AUTORESET_NEXT_STEP) {
+        for (int k = 0; k < 2; ++k) {
+            CP_ALLOC(h->nlist[k], B * sizeof(int32_t));
+            // non-blocking: no implicit ordering against a caller's legacy default stream
+            e = hipStreamCreateWithFlags(&h->nstream[k], hipStreamNonBlocking);
+            if (e != hipSuccess) return fail_free(e, "hipStreamCreateWithFlags");
+            e = hipEventCreateWithFlags(&h->nfork[k], hipEventDisableTiming);
+            if (e != hipSuccess) return fail_free(e, "hipEventCreateWithFlags");
+            e = hipEventCreateWithFlags(&h->njoin[k], hipEventDisableTiming);
+            if (e != hipSuccess) return fail_free(e, "hipEventCreateWithFlags");
+        }
+        CP_ALLOC(h->nobs, (size_t)R * 14 * B * sizeof(float));
+        e = hipMemset(h->nobs, 0, (size_t)R * 14 * B * sizeof(float));
+        if (e != hipSuccess) return fail_free(e, "hipMemset");
+    }
 #undef CP_ALLOC
-    e = hipMemset(h->count2, 0, 2 * sizeof(int32_t));
+    e = hipMemset(h->count2, 0, 3 * sizeof(int32_t));
     if (e != hipSuccess) return fail_free(e, "hipMemset");
     h->b.count = h->count2;
     h->b.count_next = nullptr;
@@ -363,6 +393,16 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
 void cp_destroy(cp_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
+    for (int k = 0; k < 2; ++k) {  // NEXT_STEP: a reset may still be in flight on a side stream
+        if (h->nstream[k]) {
+            (void)hipStreamSynchronize(h->nstream[k]);
+            (void)hipStreamDestroy(h->nstream[k]);
+        }
+        if (h->nfork[k]) (void)hipEventDestroy(h->nfork[k]);
+        if (h->njoin[k]) (void)hipEventDestroy(h->njoin[k]);
+        (void)hipFree(h->nlist[k]);
+    }
+    (void)hipFree(h->nobs);
     timing_free(h->timing);
     (void)hipFree(h->b.state);
     (void)hipFree(h->b.term_obs);
@@ -434,15 +474,72 @@ static void choose_reset_shape(cp_handle* h) {
     if (h->cfg.phys.model_flags & CP_MODEL_PERSISTENT) h->reset_lat = h->step_lat = 1;  // PM: latency shape only
 }
 
-static int launch_reset_from_list(cp_handle* h, float* obs_out, hipStream_t st, bool render) {
-    const int B = h->cfg.num_envs;
+static int launch_reset_list(cp_handle* h, const cpc::Bufs& b, float* obs_out, hipStream_t st) {
     hipEvent_t* ev = timing_slot(h, 1);
     if (ev) CP_TRY(h, hipEventRecord(ev[0], st));
-    if (h->f64) cp64::launch_reset(true, h->cfg, h->b, obs_out, st);
-    else cp::launch_reset(h->reset_lat != 0, h->cfg, h->b, obs_out, st);
+    if (h->f64) cp64::launch_reset(true, h->cfg, b, obs_out, st);
+    else cp::launch_reset(h->reset_lat != 0, h->cfg, b, obs_out, st);
     if (check(h, hipGetLastError(), "cp_reset_kernel")) return -1;
     if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
+    return 0;
+}
+
+static int launch_reset_from_list(cp_handle* h, float* obs_out, hipStream_t st, bool render) {
+    if (launch_reset_list(h, h->b, obs_out, st)) return -1;
     if (render && h->pixels) return launch_render(h, h->b.list, h->b.count, st);
+    return 0;
+}
+
+// CP_AUTORESET_NEXT_STEP: make `st` wait for the reset in flight on a side stream (every entry point
+// that reads or writes the state or the per-env outputs of the last call does this first)
+static int join_next_step(cp_handle* h, hipStream_t st) {
+    if (h->cfg.autoreset == CP_AUTORESET_NEXT_STEP && h->ninflight >= 0)
+        CP_TRY(h, hipStreamWaitEvent(st, h->njoin[h->ninflight], 0));
+    return 0;
+}
+
+// cp_step of a NEXT_STEP handle.  Call n appends its finishing envs to list q = n % 2
+// (their done field becomes 2 + q) and starts their reset on side stream q as soon as its step kernel
+// is done; call n + 1 steps every other env meanwhile (the step kernel skips done fields >= 2), then
+// waits for that reset and hands out its obs (fixup kernel).  Two resets can be in flight at once:
+// list q's reset overlaps call n + 1's step kernel and the caller's work between the calls.
+static int step_next_step(cp_handle* h, const void* actions, int action_kind, float* obs_out, float* reward_out,
+                          uint8_t* done_out, float* terminal_obs_out, hipStream_t st) {
+    const int q = h->npar;
+    cpc::Bufs b = h->b;
+    b.list = h->nlist[q];
+    b.count = h->count2 + q;  // zeroed by the fixup of its previous use (or at cp_create)
+    b.count_next = nullptr;
+    b.npar = q;
+    b.keep_done = 1;
+    hipEvent_t* ev = timing_slot(h, 0);
+    if (ev) CP_TRY(h, hipEventRecord(ev[0], st));
+    if (h->f64)
+        cp64::launch_step(true, action_kind, h->cfg, b, actions, obs_out, reward_out, done_out, terminal_obs_out,
+                          h->readback, h->readback_bug, h->lqr, st);
+    else
+        cp::launch_step(h->step_lat != 0, action_kind, h->cfg, b, actions, obs_out, reward_out, done_out,
+                        terminal_obs_out, h->readback, h->readback_bug, h->lqr, st);
+    CP_TRY(h, hipGetLastError());
+    if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
+    CP_TRY(h, hipEventRecord(h->nfork[q], st));
+    if (h->ninflight >= 0) {  // the previous call's list: its reset obs are this call's obs
+        const int p = h->ninflight;
+        CP_TRY(h, hipStreamWaitEvent(st, h->njoin[p], 0));
+        if (h->f64)
+            cp64::launch_nextstep_fixup(h->cfg, h->b, h->nlist[p], h->count2 + p, p, h->nobs, obs_out, reward_out,
+                                        done_out, st);
+        else
+            cp::launch_nextstep_fixup(h->cfg, h->b, h->nlist[p], h->count2 + p, p, h->nobs, obs_out, reward_out,
+                                      done_out, st);
+        CP_TRY(h, hipGetLastError());
+        CP_TRY(h, hipMemsetAsync(h->count2 + p, 0, sizeof(int32_t), st));
+    }
+    CP_TRY(h, hipStreamWaitEvent(h->nstream[q], h->nfork[q], 0));
+    if (launch_reset_list(h, b, h->nobs, h->nstream[q])) return -1;
+    CP_TRY(h, hipEventRecord(h->njoin[q], h->nstream[q]));
+    h->ninflight = q;
+    h->npar = q ^ 1;
     return 0;
 }
 
@@ -451,6 +548,17 @@ int cp_reset(cp_handle* h, const uint8_t* env_mask, float* obs_out, void* stream
     hipStream_t st = (hipStream_t)stream;
     const int B = h->cfg.num_envs;
     CP_TRY(h, hipSetDevice(h->device));
+    if (h->cfg.autoreset == CP_AUTORESET_NEXT_STEP) {  // envs whose reset already ran keep it
+        if (join_next_step(h, st)) return -1;
+        cpc::Bufs b = h->b;
+        b.count = h->count2 + 2;
+        b.count_next = nullptr;
+        CP_TRY(h, hipMemsetAsync(b.count, 0, sizeof(int32_t), st));
+        if (h->f64) cp64::launch_nextstep_resolve(h->cfg, b, env_mask, h->nobs, obs_out, st);
+        else cp::launch_nextstep_resolve(h->cfg, b, env_mask, h->nobs, obs_out, st);
+        CP_TRY(h, hipGetLastError());
+        return launch_reset_list(h, b, obs_out, st);
+    }
     use_counter(h);
     CP_TRY(h, hipMemsetAsync(h->b.count, 0, sizeof(int32_t), st));
     hipLaunchKernelGGL(cp::cp_mask_to_list_kernel, dim3(grid_for(B, 256)), dim3(256), 0, st, B, env_mask, h->b.list,
@@ -465,8 +573,9 @@ int cp_step(cp_handle* h, const void* actions, int action_kind, float* obs_out, 
     if (action_kind != CP_ACTION_CONTINUOUS && action_kind != CP_ACTION_DISCRETE)
         return fail(h, "cp_step: action_kind must be CP_ACTION_CONTINUOUS or CP_ACTION_DISCRETE");
     hipStream_t st = (hipStream_t)stream;
-    const int B = h->cfg.num_envs;
     CP_TRY(h, hipSetDevice(h->device));
+    if (h->cfg.autoreset == CP_AUTORESET_NEXT_STEP)
+        return step_next_step(h, actions, action_kind, obs_out, reward_out, done_out, terminal_obs_out, st);
     if (h->cfg.autoreset) use_counter(h);  // zeroed by the previous call's reset launch
     if (h->pixels) CP_TRY(h, hipMemsetAsync(h->b.rcount, 0, sizeof(int32_t), st));
     hipEvent_t* ev = timing_slot(h, 0);
@@ -495,6 +604,8 @@ int cp_rollout(cp_handle* h, int steps, const void* actions, int action_kind, fl
     if (h->readback || h->lqr.state8 || h->pixels)
         return fail(h, "cp_rollout: the per-step side outputs (readback, LQR 8-states, raster obs) are cp_step-only; "
                        "disable them first");
+    if (h->cfg.autoreset == CP_AUTORESET_NEXT_STEP)
+        return fail(h, "cp_rollout: CP_AUTORESET_NEXT_STEP handles step through cp_step only");
     hipStream_t st = (hipStream_t)stream;
     CP_TRY(h, hipSetDevice(h->device));
     hipEvent_t* ev = timing_slot(h, 0);
@@ -533,6 +644,7 @@ int cp_set_lqr(cp_handle* h, const float* gains, int per_env, float* state8_out,
 int cp_set_bump_forces(cp_handle* h, const float* forces, void* stream) {
     if (!h || !forces) return fail(h, "cp_set_bump_forces: null argument");
     CP_TRY(h, hipSetDevice(h->device));
+    if (join_next_step(h, (hipStream_t)stream)) return -1;  // an in-flight reset reads the bumps
     size_t n = (size_t)h->cfg.num_envs * h->cfg.initial_force_steps * 4;
     CP_TRY(h, hipMemcpyAsync(h->b.bumps, forces, n * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
     return 0;
@@ -567,6 +679,7 @@ int cp_get_kernel_shape(const cp_handle* h, int* step_shape, int* reset_shape) {
 int cp_get_state(cp_handle* h, void* state_out, void* stream) {
     if (!h || !state_out) return fail(h, "cp_get_state: null argument");
     CP_TRY(h, hipSetDevice(h->device));
+    if (join_next_step(h, (hipStream_t)stream)) return -1;
     size_t n = (size_t)CP_STATE_FIELDS * h->cfg.num_envs;
     CP_TRY(h, hipMemcpyAsync(state_out, h->b.state, n * (h->f64 ? sizeof(double) : sizeof(float)), hipMemcpyDeviceToDevice,
                              (hipStream_t)stream));
@@ -576,6 +689,7 @@ int cp_get_state(cp_handle* h, void* state_out, void* stream) {
 int cp_set_state(cp_handle* h, const void* state_in, void* stream) {
     if (!h || !state_in) return fail(h, "cp_set_state: null argument");
     CP_TRY(h, hipSetDevice(h->device));
+    if (join_next_step(h, (hipStream_t)stream)) return -1;
     size_t n = (size_t)CP_STATE_FIELDS * h->cfg.num_envs;
     CP_TRY(h, hipMemcpyAsync(h->b.state, state_in, n * (h->f64 ? sizeof(double) : sizeof(float)), hipMemcpyDeviceToDevice,
                              (hipStream_t)stream));
@@ -585,6 +699,7 @@ int cp_set_state(cp_handle* h, const void* state_in, void* stream) {
 int cp_episode_returns(cp_handle* h, float* returns_out, int32_t* lengths_out, void* stream) {
     if (!h) return fail(h, "cp_episode_returns: null handle");
     CP_TRY(h, hipSetDevice(h->device));
+    if (join_next_step(h, (hipStream_t)stream)) return -1;
     size_t B = (size_t)h->cfg.num_envs;
     hipStream_t st = (hipStream_t)stream;
     if (returns_out) CP_TRY(h, hipMemcpyAsync(returns_out, h->b.last_ret, B * sizeof(float), hipMemcpyDeviceToDevice, st));
@@ -596,6 +711,7 @@ int cp_episode_returns(cp_handle* h, float* returns_out, int32_t* lengths_out, v
 int cp_overflow_counts(cp_handle* h, int32_t* out, void* stream) {
     if (!h || !out) return fail(h, "cp_overflow_counts: null argument");
     CP_TRY(h, hipSetDevice(h->device));
+    if (join_next_step(h, (hipStream_t)stream)) return -1;
     CP_TRY(h, hipMemcpyAsync(out, h->b.overflow, (size_t)h->cfg.num_envs * sizeof(int32_t), hipMemcpyDeviceToDevice,
                              (hipStream_t)stream));
     return 0;
@@ -672,6 +788,8 @@ int cp_encode_events(cp_handle* h, int mode, const void* actions, int action_kin
         return fail(h, "cp_encode_events: mode 0 needs actions, reward, done and step_records");
     if (mode == 1 && !reset_records) return fail(h, "cp_encode_events: mode 1 needs reset_records");
     if (mode != 0 && mode != 1) return fail(h, "cp_encode_events: mode must be 0 (step) or 1 (reset)");
+    if (h->cfg.autoreset == CP_AUTORESET_NEXT_STEP)
+        return fail(h, "cp_encode_events: not for CP_AUTORESET_NEXT_STEP handles");
     CP_TRY(h, hipSetDevice(h->device));
     const int B = h->cfg.num_envs;
     hipLaunchKernelGGL(cp::cp_event_kernel, dim3(grid_for(B, 256)), dim3(256), 0, (hipStream_t)stream, B,
@@ -730,6 +848,8 @@ int cp_set_raster(cp_handle* h, const cp_raster_config* rc, uint16_t* pixels_out
         return 0;
     }
     if (!rc) return fail(h, "cp_set_raster: null config");
+    if (h->cfg.autoreset == CP_AUTORESET_NEXT_STEP)
+        return fail(h, "cp_set_raster: not for CP_AUTORESET_NEXT_STEP handles");
     const int R = h->cfg.action_repeats;
     if (rc->width <= 0 || rc->height <= 0 || rc->width > 4096 || rc->height > 4096)
         return fail(h, "cp_set_raster: width and height must be in 1..4096");

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CP_ABI_VERSION 3
+#define CP_ABI_VERSION 4
 
 /* Bodies, in the reference's loadURDF order (bullet_cartpole.py:154-160). */
 #define CP_BODY_GROUND 0
@@ -136,7 +136,7 @@ typedef struct cp_config {
     float   angle_threshold;     /* 0.35, :62                                  */
     float   tan_angle_threshold; /* tan(angle_threshold), host-computed        */
     float   sin_angle_threshold; /* sin(angle_threshold), host-computed        */
-    int32_t autoreset;           /* reset done envs inside cp_step (0)         */
+    int32_t autoreset;           /* CP_AUTORESET_* (0: off)                    */
     int32_t bump_mode;           /* CP_BUMP_PHILOX or CP_BUMP_HOST             */
     uint64_t seed;               /* Philox key                                 */
     int64_t env_id_offset;       /* global id of env 0 (rank * B when sharded) */
@@ -152,6 +152,22 @@ typedef struct cp_config {
  * (bullet_cartpole.py:148).  The fp64 kernels run one 512-register wave per SIMD. */
 #define CP_PRECISION_F32 0
 #define CP_PRECISION_F64 1
+
+/* cp_config.autoreset: who resets an env whose episode ended, and when.
+ *   OFF        the caller (cp_reset); cp_step on a done env returns its last obs, reward 0,
+ *              done 1 (bullet_cartpole.py:179-181).
+ *   SAME_STEP  cp_step resets it in the call where it ends: obs_out holds the new episode's
+ *              first obs, terminal_obs_out the finishing obs (gym 0.x vector envs).
+ *   NEXT_STEP  cp_step returns the finishing obs in obs_out with done 1; the NEXT cp_step
+ *              returns the new episode's first obs for it, reward 0, done 0, and ignores its
+ *              action (gymnasium >= 1.0 vector envs, envpool).  The reset runs on a library
+ *              stream between the two calls, overlapped with the other envs' steps and the
+ *              caller's own work; every entry point that reads the state first
+ *              waits for it.  A cp_reset of a pending env returns that reset's obs.  Not for
+ *              hipGraph capture, cp_rollout, the raster obs or the event log. */
+#define CP_AUTORESET_OFF       0
+#define CP_AUTORESET_SAME_STEP 1
+#define CP_AUTORESET_NEXT_STEP 2
 
 #define CP_BUMP_PHILOX 0   /* theta = 2*pi*U, U from Philox4x32-10(seed; env, episode, k) */
 #define CP_BUMP_HOST   1   /* parity mode: host supplies the 60 bump forces per env      */

@@ -1293,6 +1293,7 @@ int orc_envs_create(const cp_config* cfg, orc_envs** out) {
     e->sweeps = (int32_t*)calloc((size_t)B * 2, sizeof(int32_t));
     e->merged = (int32_t*)calloc(B, sizeof(int32_t));
     e->pman = calloc(B * CP_NUM_PAIRS, sizeof(pman_t));
+    if (cfg->autoreset == CP_AUTORESET_NEXT_STEP) e->held_obs = (float*)calloc((size_t)R * 14 * B, sizeof(float));
     for (int i = 0; i < e->B; ++i) {
         for (int d = 0; d < CP_NUM_DYN; ++d) {
             for (int k = 0; k < 3; ++k) SF(e, CP_SF_BODY(d, k), i) = cfg->phys.spawn_pos[d + 1][k];
@@ -1311,6 +1312,7 @@ void orc_envs_destroy(orc_envs* e) {
     if (!e) return;
     free(e->state); free(e->term_obs); free(e->bump_forces); free(e->ret_acc);
     free(e->last_ret); free(e->last_len); free(e->overflow); free(e->sweeps); free(e->merged); free(e->pman);
+    free(e->held_obs);
     free(e);
 }
 void orc_envs_set_bump_forces(orc_envs* e, const float* f) {
@@ -1390,6 +1392,12 @@ void orc_envs_reset(orc_envs* e, const uint8_t* mask, float* obs_out) {
     int R = e->cfg.action_repeats;
     for (int i = 0; i < e->B; ++i) {
         if (mask && !mask[i]) continue;
+        if (e->cfg.autoreset == CP_AUTORESET_NEXT_STEP && get_i(e, CP_SF_DONE, i) >= 2) {
+            /* its reset already ran (in the step that ended it): hand out that reset's obs */
+            memcpy(obs_out + (size_t)i * R * 14, e->held_obs + (size_t)i * R * 14, (size_t)R * 14 * sizeof(float));
+            set_i(e, CP_SF_DONE, i, 0);
+            continue;
+        }
         reset_one(e, i, obs_out + (size_t)i * R * 14);
     }
 }
@@ -1460,10 +1468,18 @@ static int lqr_observe(const orc_envs* e, const sim_t* S, const float* K, real u
 }
 
 static void step_one(orc_envs* e, int i, const void* actions, int kind, float* obs_out, float* reward_out,
-                     uint8_t* done_out, float* term_out, float* readback, int rb_bug) {
+                     uint8_t* done_out, float* term_out, float* readback, int rb_bug, int par) {
     const cp_config* cfg = &e->cfg;
     const int R = cfg->action_repeats, Sn = cfg->steps_per_repeat;
     float* obs = obs_out + (size_t)i * R * 14;
+    if (cfg->autoreset == CP_AUTORESET_NEXT_STEP && get_i(e, CP_SF_DONE, i) >= 2) {
+        /* ended in the previous step: the new episode's first obs, reward 0, done 0; action ignored */
+        memcpy(obs, e->held_obs + (size_t)i * R * 14, (size_t)R * 14 * sizeof(float));
+        reward_out[i] = 0.0f;
+        done_out[i] = 0;
+        set_i(e, CP_SF_DONE, i, 0);
+        return;
+    }
     if (get_i(e, CP_SF_DONE, i)) {     /* bullet_cartpole.py:179-181 */
         for (int f = 0; f < R * 14; ++f) obs[f] = e->term_obs[(size_t)f * e->B + i];
         reward_out[i] = 0.0f;
@@ -1531,22 +1547,36 @@ static void step_one(orc_envs* e, int i, const void* actions, int kind, float* o
         for (int f = 0; f < R * 14; ++f) e->term_obs[(size_t)f * e->B + i] = obs[f];
         if (term_out) memcpy(term_out + (size_t)i * R * 14, obs, (size_t)R * 14 * sizeof(float));
         set_i(e, CP_SF_DONE, i, 1);
-        if (cfg->autoreset) reset_one(e, i, obs);
+        if (cfg->autoreset == CP_AUTORESET_NEXT_STEP) {
+            reset_one(e, i, e->held_obs + (size_t)i * R * 14);
+            set_i(e, CP_SF_DONE, i, 2 + par);
+        } else if (cfg->autoreset) {
+            reset_one(e, i, obs);
+        }
     }
 }
 
+/* the parity of this step (CP_AUTORESET_NEXT_STEP's done code); toggles per step call */
+static int next_par(orc_envs* e) {
+    const int q = e->npar;
+    e->npar ^= 1;
+    return q;
+}
 void orc_envs_step(orc_envs* e, const void* actions, int kind, float* obs_out, float* reward_out,
                    uint8_t* done_out, float* term_out, float* readback, int rb_bug) {
+    const int q = next_par(e);
     for (int i = 0; i < e->B; ++i)
-        step_one(e, i, actions, kind, obs_out, reward_out, done_out, term_out, readback, rb_bug);
+        step_one(e, i, actions, kind, obs_out, reward_out, done_out, term_out, readback, rb_bug, q);
 }
 void orc_envs_step_range(orc_envs* e, int lo, int hi, const void* actions, int kind, float* obs_out,
                          float* reward_out, uint8_t* done_out) {
-    for (int i = lo; i < hi; ++i) step_one(e, i, actions, kind, obs_out, reward_out, done_out, NULL, NULL, 0);
+    /* a shard of one step: NEXT_STEP handles step through orc_envs_step */
+    for (int i = lo; i < hi; ++i) step_one(e, i, actions, kind, obs_out, reward_out, done_out, NULL, NULL, 0, 0);
 }
 int orc_envs_step_omp(orc_envs* e, const void* actions, int kind, float* obs_out, float* reward_out,
                       uint8_t* done_out, int threads) {
     int used = 1;
+    const int q = next_par(e);
 #ifdef _OPENMP
     if (threads > 0) omp_set_num_threads(threads);
 #pragma omp parallel
@@ -1555,11 +1585,11 @@ int orc_envs_step_omp(orc_envs* e, const void* actions, int kind, float* obs_out
         used = omp_get_num_threads();
 #pragma omp for schedule(static)
         for (int i = 0; i < e->B; ++i)
-            step_one(e, i, actions, kind, obs_out, reward_out, done_out, NULL, NULL, 0);
+            step_one(e, i, actions, kind, obs_out, reward_out, done_out, NULL, NULL, 0, q);
     }
 #else
     (void)threads;
-    orc_envs_step(e, actions, kind, obs_out, reward_out, done_out, NULL, NULL, 0);
+    for (int i = 0; i < e->B; ++i) step_one(e, i, actions, kind, obs_out, reward_out, done_out, NULL, NULL, 0, q);
 #endif
     return used;
 }
