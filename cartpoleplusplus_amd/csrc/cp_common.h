@@ -60,6 +60,12 @@ CP_DEV uint32_t to_bits(double x) { return (uint32_t)(uint64_t)__double_as_longl
 // each env keeps one offset register instead of a 64-bit address per field (the flat form
 // made the compiler hoist and spill ~100 of them).  Limits one SoA array to 4 GiB:
 // B * fields * sizeof(T) < 2^32 (checked at cp_create).
+// cache policy bits of the SoA buffer accesses (gfx950 CPol: 1 sc0, 2 nt, 16 sc1); 0 = default.
+// Diagnostic builds (-DCP_SOA_AUX=2) stream the state past L2 so that the spill frame stays resident.
+#ifndef CP_SOA_AUX
+#define CP_SOA_AUX 0
+#endif
+
 template <typename T>
 struct SoaT {
     __amdgpu_buffer_rsrc_t r;
@@ -74,19 +80,19 @@ struct SoaT {
     CP_DEV static uint32_t eoff(int i) { return (uint32_t)i * (uint32_t)sizeof(T); }
     CP_DEV T ld(int f, uint32_t off) const {
         if constexpr (sizeof(T) == 4) {
-            return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, (int)((uint32_t)f * fstride), 0));
+            return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, (int)((uint32_t)f * fstride), CP_SOA_AUX));
         } else {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, (int)((uint32_t)f * fstride), 0);
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, (int)((uint32_t)f * fstride), CP_SOA_AUX);
             return __longlong_as_double((long long)(((uint64_t)(uint32_t)v[1] << 32) | (uint32_t)v[0]));
         }
     }
     CP_DEV void st(int f, uint32_t off, T x) const {
         if constexpr (sizeof(T) == 4) {
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, (int)off, (int)((uint32_t)f * fstride), 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, (int)off, (int)((uint32_t)f * fstride), CP_SOA_AUX);
         } else {
             const uint64_t u = (uint64_t)__double_as_longlong(x);
             __attribute__((ext_vector_type(2))) unsigned int v = {(unsigned int)u, (unsigned int)(u >> 32)};
-            __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, (int)((uint32_t)f * fstride), 0);
+            __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, (int)((uint32_t)f * fstride), CP_SOA_AUX);
         }
     }
 };

@@ -88,6 +88,17 @@ CP_DEV void flush_stamps(const Stamps& ST, uint64_t* dst, uint64_t total, uint64
 #endif
 }
 
+// per-step outputs (obs rows, reward, done): written once, read by the caller after the launch.
+// Diagnostic builds (-DCP_NT_OUT) store them non-temporally (past L2).
+template <typename T>
+CP_DEV void put_out(T* p, T v) {
+#ifdef CP_NT_OUT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 CP_DEV void load_sim(Sim& S, const Soa& st, uint32_t o) {
 #pragma unroll
     for (int d = 0; d < CP_NUM_DYN; ++d) {
@@ -420,7 +431,7 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
                     float row[14];
                     write_obs_row(S, row);
 #pragma unroll
-                    for (int f = 0; f < 14; ++f) obs[r * 14 + f] = row[f];
+                    for (int f = 0; f < 14; ++f) put_out(&obs[r * 14 + f], row[f]);
                     if (b.rposes) write_rposes(S, b.rposes + ((size_t)i * R + r) * CP_NUM_DYN * 7);
                 }
             }
@@ -434,8 +445,8 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
             if (lead) {
                 store_sim(S, G.st, G.off);
                 sti(G.st, CP_SF_STEPS, G.off, steps);
-                reward_out[i] = 1.0f;  // bullet_cartpole.py:260
-                done_out[i] = done ? 1 : 0;
+                put_out(&reward_out[i], 1.0f);  // bullet_cartpole.py:260
+                put_out(&done_out[i], (uint8_t)(done ? 1 : 0));
                 const float ret = b.ret_acc[i] + 1.0f;
                 if (done) {
                     b.last_ret[i] = ret;
@@ -604,7 +615,7 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
                 write_obs_row(S, row);
                 const int r = sub / SR - 1;
 #pragma unroll
-                for (int q = 0; q < 14; ++q) obs[r * 14 + q] = row[q];
+                for (int q = 0; q < 14; ++q) put_out(&obs[r * 14 + q], row[q]);
             }
             if (sub < RS) {
                 stc(RC_SUB, sub);
@@ -619,8 +630,8 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
             if (LQR && (flags & RF_LQR_DONE)) done = true;
             const float ret = __uint_as_float(to_bits(G.lx(RC_RET))) + 1.0f;
             if (lead) {
-                reward_out[(size_t)k * B + e] = 1.0f;
-                done_out[(size_t)k * B + e] = done ? 1 : 0;
+                put_out(&reward_out[(size_t)k * B + e], 1.0f);
+                put_out(&done_out[(size_t)k * B + e], (uint8_t)(done ? 1 : 0));
             }
             if (done) {
                 if (lead) {

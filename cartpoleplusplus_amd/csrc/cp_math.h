@@ -85,8 +85,29 @@ CP_DEV V3 symv(const Sym& M, V3 v) {
               fma_(M.m2, v.x, fma_(M.m4, v.y, M.m5 * v.z)));
 }
 
+// fp64: the Taylor series through x^17 / x^18 (remainder < 1e-19 at pi/4: double-accurate), with the
+// oracle's fp64 build's coefficients and Horner order (oracle/cp_oracle.c sincos_small)
+__constant__ const double kSin64[8] = {-0.16666666666666666, 0.008333333333333333, -0.0001984126984126984,
+                                       2.7557319223985893e-06, -2.505210838544172e-08, 1.6059043836821613e-10,
+                                       -7.647163731819816e-13, 2.8114572543455206e-15};
+__constant__ const double kCos64[9] = {-0.5, 0.041666666666666664, -0.001388888888888889, 2.48015873015873e-05,
+                                       -2.755731922398589e-07, 2.08767569878681e-09, -1.1470745597729725e-11,
+                                       4.779477332387385e-14, -1.5619206968586225e-16};
+
 // Taylor sin/cos for |x| <= pi/4 (constants rounded from double, as the oracle)
 CP_DEV void sincos_small(real x, real& s, real& c) {
+    if constexpr (sizeof(real) == 8) {
+        const real x2 = x * x;
+        real p = (real)kSin64[7];
+#pragma unroll
+        for (int k = 6; k >= 0; --k) p = fma_(x2, p, (real)kSin64[k]);
+        s = fma_(x * x2, p, x);
+        real q = (real)kCos64[8];
+#pragma unroll
+        for (int k = 7; k >= 0; --k) q = fma_(x2, q, (real)kCos64[k]);
+        c = fma_(x2, q, real(1.0));
+        return;
+    }
     real x2 = x * x;
     real p = fma_(x2, (real)2.7557319223985893e-6, (real)-1.9841269841269841e-4);
     p = fma_(x2, p, (real)8.3333333333333333e-3);
@@ -123,6 +144,15 @@ CP_DEV real atan_pos(real z) {
         z = (z - real(1.0)) / (z + real(1.0));
     }
     real z2 = z * z;
+    if constexpr (sizeof(real) == 8) {
+        // fp64: the odd Taylor series of atan through z^47 on |z| <= tan(pi/8) (remainder < 1e-18:
+        // double-accurate); coefficient k is (-1)^k / (2k + 1), folded at compile time (IEEE division,
+        // the oracle's fp64 build computes the same doubles)
+        real p = (real)(-1.0 / 47.0);
+#pragma unroll
+        for (int k = 22; k >= 1; --k) p = fma_(z2, p, (real)((k & 1 ? -1.0 : 1.0) / (double)(2 * k + 1)));
+        return base + fma_(z * z2, p, z);
+    }
     real p = fma_(z2, (real)8.05374449538e-2, (real)-1.38776856032e-1);
     p = fma_(z2, p, (real)1.99777106478e-1);
     p = fma_(z2, p, (real)-3.33329491539e-1);

@@ -95,8 +95,24 @@ static inline v3 symv(const real M[6], v3 v) {
 }
 
 /* --------------------------------------------------------- own transcendentals */
+#ifdef ORC_DOUBLE
+/* fp64: the Taylor series through x^17 / x^18 (remainder < 1e-19 at pi/4): double-accurate */
+static const double SIN64[8] = {-0.16666666666666666, 0.008333333333333333, -0.0001984126984126984,
+                                2.7557319223985893e-06, -2.505210838544172e-08, 1.6059043836821613e-10,
+                                -7.647163731819816e-13, 2.8114572543455206e-15};
+static const double COS64[9] = {-0.5, 0.041666666666666664, -0.001388888888888889, 2.48015873015873e-05,
+                                -2.755731922398589e-07, 2.08767569878681e-09, -1.1470745597729725e-11,
+                                4.779477332387385e-14, -1.5619206968586225e-16};
+#endif
 static inline void sincos_small(real x, real* s, real* c) {
-    /* Taylor through x^9 / x^8; used for |x| <= pi/4 */
+#ifdef ORC_DOUBLE
+    real x2 = x * x, p = SIN64[7], q = COS64[8];
+    for (int k = 6; k >= 0; --k) p = FMA(x2, p, SIN64[k]);
+    *s = FMA(x * x2, p, x);
+    for (int k = 7; k >= 0; --k) q = FMA(x2, q, COS64[k]);
+    *c = FMA(x2, q, RC(1.0));
+#else
+    /* Taylor through x^9 / x^8; used for |x| <= pi/4 (fp32: below the format's rounding) */
     real x2 = x * x;
     real p = FMA(x2, RC(2.7557319223985893e-6), RC(-1.9841269841269841e-4));
     p = FMA(x2, p, RC(8.3333333333333333e-3));
@@ -106,6 +122,7 @@ static inline void sincos_small(real x, real* s, real* c) {
     q = FMA(x2, q, RC(4.1666666666666667e-2));
     q = FMA(x2, q, RC(-0.5));
     *c = FMA(x2, q, RC(1.0));
+#endif
 }
 
 /* sin/cos of 2*pi*u for u in [0,1) (bump direction, bullet_cartpole.py:355) */
@@ -144,6 +161,13 @@ static real atan_pos(real z) {
         z = (z - RC(1.0)) / (z + RC(1.0));
     }
     real z2 = z * z;
+#ifdef ORC_DOUBLE
+    {   /* fp64: odd Taylor series through z^47 on |z| <= tan(pi/8) (remainder < 1e-18) */
+        real p = -1.0 / 47.0;
+        for (int k = 22; k >= 1; --k) p = FMA(z2, p, (k & 1 ? -1.0 : 1.0) / (double)(2 * k + 1));
+        return base + FMA(z * z2, p, z);
+    }
+#endif
     real p = FMA(z2, RC(8.05374449538e-2), RC(-1.38776856032e-1));
     p = FMA(z2, p, RC(1.99777106478e-1));
     p = FMA(z2, p, RC(-3.33329491539e-1));
@@ -157,6 +181,19 @@ static real atan2_own(real y, real x) {
     if (y < RC(0)) r = -r;
     return r;
 }
+/* test probe of the own transcendentals in the build's real type: sin, cos of x (|x| <= pi/4),
+   atan2(y, x), sin, cos of 2 pi u (u in [0, 1)) */
+void orc_probe_transcendentals(double x, double y, double u, double out[5]) {
+    real s, c;
+    sincos_small((real)x, &s, &c);
+    out[0] = (double)s;
+    out[1] = (double)c;
+    out[2] = (double)atan2_own((real)y, (real)x);
+    sincos_turns((real)u, &s, &c);
+    out[3] = (double)s;
+    out[4] = (double)c;
+}
+
 /* pybullet getEulerFromQuaternion (roll, pitch, yaw) [ext: recalled formula] */
 static void quat_euler(const real q[4], real rpy[3]) {
     real x = q[0], y = q[1], z = q[2], w = q[3];

@@ -91,6 +91,7 @@ def load(precision="f32"):
         "orc_render_frame": (None, [VP, VP, VP, C.c_int, VP]),
         "orc_philox4x32_10": (None, [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]),
         "orc_sincos_turns": (None, [C.c_float, P(C.c_float), P(C.c_float)]),
+        "orc_probe_transcendentals": (None, [C.c_double, C.c_double, C.c_double, P(C.c_double)]),
         "orc_sizeof_real": (C.c_int, []),
     }
     for fn, (res, args) in sig.items():

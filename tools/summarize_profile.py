@@ -62,7 +62,8 @@ def durations(path):
 def main(prof_dir, tag, out_dir):
     res = {"tag": tag, "source": os.path.relpath(prof_dir), "kernels": {}}
     dur = durations(os.path.join(prof_dir, "trace", "run_kernel_trace.csv"))
-    sq, n_sq = counters(os.path.join(prof_dir, "sq", "run_counter_collection.csv"))
+    p1 = os.path.join(prof_dir, "sq", "run_counter_collection.csv")   # absent in traffic-only runs
+    sq, n_sq = counters(p1) if os.path.exists(p1) else ({}, {})
     p2 = os.path.join(prof_dir, "sq2", "run_counter_collection.csv")
     if os.path.exists(p2):
         sq2, _ = counters(p2)
