@@ -1350,7 +1350,12 @@ CP_DEV void sweeps_fast(Ctx& c, FastIsl& F, Sim& S, const cp_physics& P, real* p
         // the periodic test cost more than it saved, 0.450 -> 0.480 ms at B = 4,096)
         if constexpr (C44) {
             if ((it - it0) % 8 == 0 && __ballot(c.active && !c44_ok(c)) == 0ull) {
+                CP_STAMP(q0);
                 sweeps_c44(c, F, tol, it, it1, ST);
+#ifdef CP_STAMP_C44  // diagnostic: the settle loop's own cycles in the row-setup slot
+                CP_STAMP(q1);
+                CP_ACC(rows, q0, q1);
+#endif
                 return;
             }
         }
@@ -1460,9 +1465,19 @@ CP_DEV void solve_range(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* p
     if constexpr (FAST) {
         if (__ballot(!fast_ok(c)) == 0ull) {
             FastIsl F;
+            CP_STAMP(b0);
             fast_build(F, c, pool);
+            CP_STAMP(b1);
             sweeps_fast<C44>(c, F, S, P, pool, pool0, second, it0, it1, ST);
+            CP_STAMP(b2);
             fast_store(F, c, pool);
+#ifdef CP_STAMP_C44  // diagnostic: fast_build in the box-selection slot, the rest of sweeps_fast outside the
+                     // settle loop in the box_box slot (fast_store is a few LDS writes)
+            CP_STAMP(b3);
+            CP_ACC(sel, b0, b1);
+            CP_ACC(bb, b1, b2);
+            (void)b3;
+#endif
             return;
         }
     }
@@ -1703,8 +1718,10 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
             }
         }
         CP_STAMP(n2);
+#ifndef CP_STAMP_C44
         CP_ACC(sel, n0, n1);
         CP_ACC(bb, n1, n2);
+#endif
         const int base = used, fbase = fused;
         int m = 0, fm = 0;
         uint32_t nid = 0xFFFFFFFFu;
@@ -1779,7 +1796,9 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
         used = base + m;
         fused = fbase + fm;
         CP_STAMP(n3);
+#ifndef CP_STAMP_C44
         CP_ACC(rows, n2, n3);
+#endif
         // old point count = the leading non-0xFF bytes of the old id word (written as a prefix)
         const int om = (oid & 0xFFu) == 0xFFu ? 0 : ((oid >> 8) & 0xFFu) == 0xFFu ? 1
                      : ((oid >> 16) & 0xFFu) == 0xFFu ? 2 : ((oid >> 24) & 0xFFu) == 0xFFu ? 3 : 4;
