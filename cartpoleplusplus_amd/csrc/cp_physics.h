@@ -1025,6 +1025,11 @@ struct Ctx {
 // the env (island 0, island 1, cross) has a squared residual above the threshold:
 // Bullet solves the two islands as one group (oracle: substep, step 4).
 CP_DEV bool c44_ok(const Ctx& c);
+// how often (in sweeps) the reset kernels' sweep loops re-test whether every active lane of the wave
+// has the settle structure (the lanes without it usually converge first)
+#ifndef CP_C44_CHECK
+#define CP_C44_CHECK 8
+#endif
 CP_DEV void sweeps_c44_slow(Ctx& c, real* pool, real tol, int it0, int it1, Stamps& ST);
 template <bool C44 = false, bool PM = false>
 CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0, bool second, int it0, int it1,
@@ -1050,7 +1055,7 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0,
     for (int it = it0; it < it1; ++it) {
         if (__ballot(c.active) == 0ull) break;
         if constexpr (C44 && !PM) {  // every still-active lane in the settle structure (the reset kernels)
-            if ((it - it0) % 8 == 0 && __ballot(c.active && !c44_ok(c)) == 0ull) {
+            if ((it - it0) % CP_C44_CHECK == 0 && __ballot(c.active && !c44_ok(c)) == 0ull) {
                 sweeps_c44_slow(c, pool, tol, it, it1, ST);
                 return;
             }
@@ -1279,6 +1284,9 @@ CP_DEV void sweeps_c44(Ctx& c, FastIsl& F, real tol, int it0, int it1, Stamps& S
 #ifdef CP_STAMPS
         ST.sweeps += 1;
 #endif
+#ifdef CP_STAMP_C44  // diagnostic: settle-loop sweeps in the integration slot
+        ST.integ += 1;
+#endif
         bool bad = false;
         if (c.active) {
 #pragma unroll
@@ -1349,7 +1357,7 @@ CP_DEV void sweeps_fast(Ctx& c, FastIsl& F, Sim& S, const cp_physics& P, real* p
         // (the reset kernel's option: there every settle substep is in it; in the step kernel
         // the periodic test cost more than it saved, 0.450 -> 0.480 ms at B = 4,096)
         if constexpr (C44) {
-            if ((it - it0) % 8 == 0 && __ballot(c.active && !c44_ok(c)) == 0ull) {
+            if ((it - it0) % CP_C44_CHECK == 0 && __ballot(c.active && !c44_ok(c)) == 0ull) {
                 CP_STAMP(q0);
                 sweeps_c44(c, F, tol, it, it1, ST);
 #ifdef CP_STAMP_C44  // diagnostic: the settle loop's own cycles in the row-setup slot
@@ -1973,7 +1981,9 @@ CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx
         S.b[d].q[3] = rw * inv;
     }
     CP_STAMP(t4);
+#ifndef CP_STAMP_C44
     CP_ACC(integ, t3, t4);
+#endif
 #ifdef CP_STAMPS
     ST.substeps += 1;
 #endif
