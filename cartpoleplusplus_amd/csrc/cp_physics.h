@@ -1301,6 +1301,39 @@ CP_DEV void sweeps_c44(Ctx& c, FastIsl& F, real tol, int it0, int it1, Stamps& S
     }
 }
 
+// The bump phase's structures: the cart on the ground (4 rows of local pair 0, normal exactly +z) and
+// 0-4 rows of its pole on the cart (a tilting or bouncing pole), no pole-ground rows, no cross contact.
+// ~94 % of the island-substeps of a reset's 30 bump substeps that are not the settle structure
+// (oracle ORC_STATS run of 256 resets).
+CP_DEV bool c4k_ok(const Ctx& c) {
+    return pk_cnt(c.T.pk[0]) == 4 && pk_cnt(c.T.pk[1]) == 0 && !c.merged && is_plus_z(c.T.n[0]);
+}
+
+// sweeps_c44 with the cart-pole rows guarded by the lane's own count (the same rows in the same order
+// as sweeps_fast runs them for this structure, without its other pairs' guards and checks)
+CP_DEV void sweeps_c4k(Ctx& c, FastIsl& F, real tol, int it0, int it1, Stamps& ST) {
+    const V3 n2 = c.T.n[2];
+    const int cnt2 = pk_cnt(c.T.pk[2]);
+    for (int it = it0; it < it1; ++it) {
+        if (__ballot(c.active) == 0ull) break;
+#ifdef CP_STAMPS
+        ST.sweeps += 1;
+#endif
+        bool bad = false;
+        if (c.active) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                bad |= fast_grow_ez<0, false>(c.I.d1, c.I.im1, F.g0[k].rbt, F.g0[k].ib, F.g0[k].ie, F.g0[k].tg,
+                                              F.g0[k].lam, real(0.0), tol);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < cnt2) bad |= fast_crow(c.I, n2, F.c2[k], F.c2[k].lam, tol);
+        }
+        const uint32_t pbad = partner_u(bad ? 1u : 0u);  // every lane that entered the loop is here
+        if (c.active && !bad && pbad == 0u) c.active = false;
+    }
+}
+
 // sweeps() when every active lane of the wave has the settle structure, rows from the LDS
 // pool: then the ground-cart rows are pool slots 0-3 and the cart-pole rows slots 4-7 on every
 // lane (the pool fills in pair order), so the loop is straight-line with compile-time slots.
@@ -1366,6 +1399,12 @@ CP_DEV void sweeps_fast(Ctx& c, FastIsl& F, Sim& S, const cp_physics& P, real* p
 #endif
                 return;
             }
+#ifndef CP_NO_C4K
+            if (it == it0 && __ballot(c.active && !c4k_ok(c)) == 0ull) {  // the bump phase's structures
+                sweeps_c4k(c, F, tol, it, it1, ST);
+                return;
+            }
+#endif
         }
 #endif
 #ifdef CP_STAMPS
