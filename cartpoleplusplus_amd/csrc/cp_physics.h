@@ -1030,7 +1030,9 @@ CP_DEV bool c44_ok(const Ctx& c);
 #ifndef CP_C44_CHECK
 #define CP_C44_CHECK 8
 #endif
+CP_DEV bool c4k_ok(const Ctx& c);
 CP_DEV void sweeps_c44_slow(Ctx& c, real* pool, real tol, int it0, int it1, Stamps& ST);
+CP_DEV void sweeps_c4k_slow(Ctx& c, real* pool, real tol, int it0, int it1, Stamps& ST);
 template <bool C44 = false, bool PM = false>
 CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0, bool second, int it0, int it1,
                    Stamps& ST) {
@@ -1059,6 +1061,12 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0,
                 sweeps_c44_slow(c, pool, tol, it, it1, ST);
                 return;
             }
+#ifndef CP_NO_C4K
+            if (it == it0 && __ballot(c.active && !c4k_ok(c)) == 0ull) {  // the bump phase's structures
+                sweeps_c4k_slow(c, pool, tol, it, it1, ST);
+                return;
+            }
+#endif
         }
 #ifdef CP_STAMPS
         ST.sweeps += 1;
@@ -1270,8 +1278,10 @@ CP_DEV bool fast_crow(Isl& I, V3 t, const CRow& R, real& lam, real tol) {
 // cross contact.  Every island of a reset's 100 settle substeps, and ~85 % of the islands
 // that run to the sweep cap in the step.
 CP_DEV bool c44_ok(const Ctx& c) {
+    // no friction rows on pairs 0 and 2: the reference scene's cart has mu = 0 (cart.urdf), so its pairs have
+    // none, but a configured cart friction gives them some, and the settle loops do not run them
     return pk_cnt(c.T.pk[0]) == 4 && pk_cnt(c.T.pk[2]) == 4 && pk_cnt(c.T.pk[1]) == 0 && !c.merged &&
-           is_plus_z(c.T.n[0]);
+           is_plus_z(c.T.n[0]) && pk_fcnt(c.T.pk[0]) == 0 && pk_fcnt(c.T.pk[2]) == 0;
 }
 
 // sweeps_fast when every active lane of the wave has the settle structure: the same rows in
@@ -1306,7 +1316,8 @@ CP_DEV void sweeps_c44(Ctx& c, FastIsl& F, real tol, int it0, int it1, Stamps& S
 // ~94 % of the island-substeps of a reset's 30 bump substeps that are not the settle structure
 // (oracle ORC_STATS run of 256 resets).
 CP_DEV bool c4k_ok(const Ctx& c) {
-    return pk_cnt(c.T.pk[0]) == 4 && pk_cnt(c.T.pk[1]) == 0 && !c.merged && is_plus_z(c.T.n[0]);
+    return pk_cnt(c.T.pk[0]) == 4 && pk_cnt(c.T.pk[1]) == 0 && !c.merged && is_plus_z(c.T.n[0]) &&
+           pk_fcnt(c.T.pk[0]) == 0 && pk_fcnt(c.T.pk[2]) == 0;
 }
 
 // sweeps_c44 with the cart-pole rows guarded by the lane's own count (the same rows in the same order
@@ -1361,6 +1372,43 @@ CP_DEV void sweeps_c44_slow(Ctx& c, real* pool, real tol, int it0, int it1, Stam
                 bad |= isl_row<1, 2, false>(c.I, rb, n2, pool_n(pool, F_IE, s), pool_n(pool, F_TG, s), lam, real(0.0),
                                             tol);
                 pool_n(pool, F_LAM, s) = lam;
+            }
+        }
+        const uint32_t pbad = partner_u(bad ? 1u : 0u);  // every lane that entered the loop is here
+        if (c.active && !bad && pbad == 0u) c.active = false;
+    }
+}
+
+// sweeps_c44_slow for the bump phase's structures (c4k_ok): the cart-pole rows are pool slots 4 .. 4 +
+// the lane's count - 1 (local pair 1 has no rows), guarded by that count
+CP_DEV void sweeps_c4k_slow(Ctx& c, real* pool, real tol, int it0, int it1, Stamps& ST) {
+    const V3 n2 = c.T.n[2];
+    const int cnt2 = pk_cnt(c.T.pk[2]);
+    for (int it = it0; it < it1; ++it) {
+        if (__ballot(c.active) == 0ull) break;
+#ifdef CP_STAMPS
+        ST.sweeps += 1;
+#endif
+        bool bad = false;
+        if (c.active) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
+                real lam = pool_n(pool, F_LAM, s);
+                bad |= isl_row_ez<1, 0, false>(c.I, rb, pool_n(pool, F_IE, s), pool_n(pool, F_TG, s), lam, real(0.0),
+                                               tol);
+                pool_n(pool, F_LAM, s) = lam;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (k < cnt2) {
+                    const int s = 4 + k;
+                    const V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
+                    real lam = pool_n(pool, F_LAM, s);
+                    bad |= isl_row<1, 2, false>(c.I, rb, n2, pool_n(pool, F_IE, s), pool_n(pool, F_TG, s), lam,
+                                                real(0.0), tol);
+                    pool_n(pool, F_LAM, s) = lam;
+                }
             }
         }
         const uint32_t pbad = partner_u(bad ? 1u : 0u);  // every lane that entered the loop is here

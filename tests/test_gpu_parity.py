@@ -403,3 +403,28 @@ def test_batched_rejects_wrong_buffers_before_the_abi():
         env.set_state(torch.zeros((abi.CP_STATE_FIELDS, 15), device="cuda"))
     o, r, d = env.step(torch.zeros((16, 2), dtype=torch.int8, device="cuda"))
     assert torch.isfinite(o).all() and (r == 1).all()
+
+
+@shapes
+def test_cart_friction_config(oracle_mod, shape):
+    """A non-default scene: the carts get friction (the reference's cart.urdf has mu = 0), so the
+    ground-cart and cart-pole pairs carry friction rows, which the reset kernels' settle and bump-phase
+    loops do not run (c44_ok / c4k_ok must route such islands to the general loop)."""
+    B = 96
+    cfg = native.default_config(num_envs=B, action_repeats=2, initial_force=55.0, seed=17, autoreset=1,
+                                done_on_bounds=1, max_episode_len=30)
+    cfg.phys.friction[abi.CP_BODY_CART] = 0.3
+    cfg.phys.friction[abi.CP_BODY_CART2] = 0.3
+    gpu = BatchedCartpole(B, 0, config=abi.cp_config.from_buffer_copy(cfg))
+    gpu.set_kernel_shape(*shape)
+    orc = oracle_mod.Envs(abi.cp_config.from_buffer_copy(cfg))
+    _assert_same(_np(gpu.reset()), orc.reset(), "reset")
+    _compare_state(gpu, orc, "reset")
+    rng = np.random.default_rng(2)
+    for t in range(70):
+        a = rng.integers(0, 5, (B, 2)).astype(np.int8)
+        go, gr, gd = gpu.step(torch.from_numpy(a).cuda())
+        oo, orw, od = orc.step(a)
+        _assert_same(_np(go), oo, f"obs step {t}")
+        _assert_same(_np(gd), od, f"done step {t}")
+    _compare_state(gpu, orc, "after 70 steps")
