@@ -1033,6 +1033,13 @@ CP_DEV bool c44_ok(const Ctx& c);
 CP_DEV bool c4k_ok(const Ctx& c);
 CP_DEV void sweeps_c44_slow(Ctx& c, real* pool, real tol, int it0, int it1, Stamps& ST);
 CP_DEV void sweeps_c4k_slow(Ctx& c, real* pool, real tol, int it0, int it1, Stamps& ST);
+CP_DEV bool p1_ok(const Ctx& c);
+CP_DEV void sweeps_p1_slow(Ctx& c, real* pool, real tol, int it0, int it1, Stamps& ST);
+// how often (in sweeps) the step kernels' sweep loops test whether every active lane of the wave is a
+// pole standing on the ground (p1_ok)
+#ifndef CP_P1_CHECK
+#define CP_P1_CHECK 8
+#endif
 template <bool C44 = false, bool PM = false>
 CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0, bool second, int it0, int it1,
                    Stamps& ST) {
@@ -1068,6 +1075,14 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0,
             }
 #endif
         }
+#ifdef CP_P1  // opt-in: measured slower in the step kernels
+        if constexpr (!C44 && !PM) {  // the step kernels: every still-active lane a pole standing on the ground
+            if ((it - it0) % CP_P1_CHECK == 0 && __ballot(c.active && !p1_ok(c)) == 0ull) {
+                sweeps_p1_slow(c, pool, tol, it, it1, ST);
+                return;
+            }
+        }
+#endif
 #ifdef CP_STAMPS
         ST.sweeps += 1;
 #endif
@@ -1345,6 +1360,40 @@ CP_DEV void sweeps_c4k(Ctx& c, FastIsl& F, real tol, int it0, int it1, Stamps& S
     }
 }
 
+// sweeps_p1_slow with the rows in fast form (the latency-shaped step kernel)
+CP_DEV void sweeps_p1_fast(Ctx& c, FastIsl& F, real tol, int it0, int it1, Stamps& ST) {
+    const bool cart = pk_cnt(c.T.pk[0]) != 0;
+    for (int it = it0; it < it1; ++it) {
+        if (__ballot(c.active) == 0ull) break;
+#ifdef CP_STAMPS
+        ST.sweeps += 1;
+#endif
+        bool bad = false;
+        if (c.active) {
+            if (cart) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    bad |= fast_grow_ez<0, false>(c.I.d1, c.I.im1, F.g0[k].rbt, F.g0[k].ib, F.g0[k].ie, F.g0[k].tg,
+                                                  F.g0[k].lam, real(0.0), tol);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                bad |= fast_grow_ez<0, false>(c.I.d2, c.I.im2, F.g1[k].rbt, F.g1[k].ib, F.g1[k].ie, F.g1[k].tg,
+                                              F.g1[k].lam, real(0.0), tol);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const real bound = c.mu1 * F.g1[k].lam;
+                bad |= fast_grow_ez<1, true>(c.I.d2, c.I.im2, F.f1[k].rbt1, F.f1[k].ib1, F.f1[k].ie1, real(0.0),
+                                             F.f1[k].l1, bound, tol);
+                bad |= fast_grow_ez<2, true>(c.I.d2, c.I.im2, F.f1[k].rbt2, F.f1[k].ib2, F.f1[k].ie2, real(0.0),
+                                             F.f1[k].l2, bound, tol);
+            }
+        }
+        const uint32_t pbad = partner_u(bad ? 1u : 0u);  // every lane that entered the loop is here
+        if (c.active && !bad && pbad == 0u) c.active = false;
+    }
+}
+
 // sweeps() when every active lane of the wave has the settle structure, rows from the LDS
 // pool: then the ground-cart rows are pool slots 0-3 and the cart-pole rows slots 4-7 on every
 // lane (the pool fills in pair order), so the loop is straight-line with compile-time slots.
@@ -1416,6 +1465,67 @@ CP_DEV void sweeps_c4k_slow(Ctx& c, real* pool, real tol, int it0, int it1, Stam
     }
 }
 
+// The step kernels' dominant island (tools/row_classes.py: 94 % of the C3 steady state's island
+// solves, and nearly all of the sweep-cap stragglers): the pole standing on the ground on its 1 cm
+// base (local pair 1: 4 normal rows and 4 friction points, normal exactly +z), its cart either off
+// the ground or standing on it (local pair 0: 0 or 4 rows, +z), nothing on the cart-pole pair, no
+// friction rows on pairs 0 / 2, no cross contact.
+CP_DEV bool p1_ok(const Ctx& c) {
+    const int c0 = pk_cnt(c.T.pk[0]);
+    return pk_cnt(c.T.pk[1]) == 4 && pk_fcnt(c.T.pk[1]) == 4 && is_plus_z(c.T.n[1]) && pk_cnt(c.T.pk[2]) == 0 &&
+           pk_fcnt(c.T.pk[0]) == 0 && pk_fcnt(c.T.pk[2]) == 0 && !c.merged &&
+           (c0 == 0 || (c0 == 4 && is_plus_z(c.T.n[0])));
+}
+
+// sweeps() for islands with p1_ok, rows from the LDS pool: the same rows in the same order (pair 0's
+// normal rows, pair 1's normal rows, pair 1's friction points; +z forms), the pole's rows without
+// per-row guards, the cart's behind one guard
+CP_DEV void sweeps_p1_slow(Ctx& c, real* pool, real tol, int it0, int it1, Stamps& ST) {
+    const bool cart = pk_cnt(c.T.pk[0]) != 0;
+    const int b1 = pk_base(c.T.pk[1]), f1 = pk_fbase(c.T.pk[1]);
+    for (int it = it0; it < it1; ++it) {
+        if (__ballot(c.active) == 0ull) break;
+#ifdef CP_STAMPS
+        ST.sweeps += 1;
+#endif
+        bool bad = false;
+        if (c.active) {
+            if (cart) {
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
+                    real lam = pool_n(pool, F_LAM, s);
+                    bad |= isl_row_ez<1, 0, false>(c.I, rb, pool_n(pool, F_IE, s), pool_n(pool, F_TG, s), lam,
+                                                   real(0.0), tol);
+                    pool_n(pool, F_LAM, s) = lam;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int s = b1 + k;
+                const V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
+                real lam = pool_n(pool, F_LAM, s);
+                bad |= isl_row_ez<2, 0, false>(c.I, rb, pool_n(pool, F_IE, s), pool_n(pool, F_TG, s), lam, real(0.0),
+                                               tol);
+                pool_n(pool, F_LAM, s) = lam;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int s = b1 + k, fs = f1 + k;
+                const V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
+                const real bound = c.mu1 * pool_n(pool, F_LAM, s);
+                real l1 = pool_f(pool, FF_L1, fs), l2 = pool_f(pool, FF_L2, fs);
+                bad |= isl_row_ez<2, 1, true>(c.I, rb, pool_f(pool, FF_IE1, fs), real(0.0), l1, bound, tol);
+                bad |= isl_row_ez<2, 2, true>(c.I, rb, pool_f(pool, FF_IE2, fs), real(0.0), l2, bound, tol);
+                pool_f(pool, FF_L1, fs) = l1;
+                pool_f(pool, FF_L2, fs) = l2;
+            }
+        }
+        const uint32_t pbad = partner_u(bad ? 1u : 0u);  // every lane that entered the loop is here
+        if (c.active && !bad && pbad == 0u) c.active = false;
+    }
+}
+
 // sweeps() with the island rows in fast form (same row order, same stopping rule)
 template <bool C44>
 CP_DEV void sweeps_fast(Ctx& c, FastIsl& F, Sim& S, const cp_physics& P, real* pool, real* pool0, bool second,
@@ -1453,6 +1563,14 @@ CP_DEV void sweeps_fast(Ctx& c, FastIsl& F, Sim& S, const cp_physics& P, real* p
                 return;
             }
 #endif
+        }
+#endif
+#ifdef CP_P1  // opt-in: measured slower in the step kernels
+        if constexpr (!C44) {  // the step kernels: every still-active lane a pole standing on the ground
+            if ((it - it0) % CP_P1_CHECK == 0 && __ballot(c.active && !p1_ok(c)) == 0ull) {
+                sweeps_p1_fast(c, F, tol, it, it1, ST);
+                return;
+            }
         }
 #endif
 #ifdef CP_STAMPS
