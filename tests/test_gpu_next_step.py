@@ -115,3 +115,43 @@ def test_next_step_refusals():
         env.enable_raster()
     env.step(torch.zeros((64, 2), dtype=torch.int8))
     env.close()   # a reset may be in flight: cp_destroy waits for it
+
+
+@pytest.mark.parametrize("shape", [("throughput", "throughput"), ("latency", "latency")], ids=["tp-tp", "lat-lat"])
+def test_next_step_lqr_done_thresholds(oracle_mod, shape):
+    """The in-kernel LQR policy with the agent's done thresholds (per-env gains) under NEXT_STEP: the
+    8-states of the reset-only calls are left as they were, on both sides."""
+    from cartpoleplusplus_amd.lqr import exact_gains
+    B = 128
+    gpu, orc = _pair(oracle_mod, shape, num_envs=B, action_repeats=3, initial_force=55.0, seed=21)
+    rng = np.random.default_rng(5)
+    K = (exact_gains()[None] * rng.uniform(0.0, 1.5, (B, 1, 1, 8))).astype(np.float32)
+    gpu.enable_lqr(torch.from_numpy(K), per_env=True, done_pos=0.02, done_angle=0.02)
+    orc.set_lqr(K, per_env=True, state8=True, done_pos=0.02, done_angle=0.02)
+    _assert_same(_np(gpu.reset()), orc.reset(), "reset")
+    pend = 0
+    for t in range(100):
+        a = rng.uniform(-0.3, 0.3, (B, 2, 2)).astype(np.float32)
+        pend += int(_pending(orc).sum())
+        go, gr, gd = gpu.step(torch.from_numpy(a).cuda())
+        oo, orw, od = orc.step(a, obs=_np(go).copy())
+        _assert_same(_np(go), oo, f"obs call {t}")
+        _assert_same(_np(gr), orw, f"reward call {t}")
+        _assert_same(_np(gd), od, f"done call {t}")
+        _assert_same(_np(gpu.state8), orc.state8, f"state8 call {t}")
+    _state(gpu, orc, "final")
+    assert pend > 0
+
+
+def test_next_step_persistent_manifold(oracle_mod):
+    """NEXT_STEP with the persistent-manifold contact model (latency-shaped kernels): the in-flight
+    reset clears the env's manifolds while the next step kernel runs the other envs."""
+    B = 64
+    cfg = native.default_config(autoreset=abi.CP_AUTORESET_NEXT_STEP, num_envs=B, action_repeats=2,
+                                initial_force=55.0, seed=7, done_on_bounds=1, max_episode_len=20)
+    cfg.phys.model_flags = abi.CP_MODEL_PERSISTENT
+    gpu = BatchedCartpole(B, 0, config=abi.cp_config.from_buffer_copy(cfg))
+    orc = oracle_mod.Envs(abi.cp_config.from_buffer_copy(cfg))
+    _assert_same(_np(gpu.reset()), orc.reset(), "reset")
+    rng = np.random.default_rng(3)
+    assert _drive(gpu, orc, B, 50, rng, abi.CP_ACTION_DISCRETE, "pm", check_state_every=10) > 0
