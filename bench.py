@@ -33,6 +33,9 @@ the kernel's results) on bounded samples: C3 on every CPU of the process's affin
 parity (rank 0, N = 1): SURVEY.md §8d's matrix, GPU vs the oracle's fp32 build (bit-exact
 bar) and fp64 build (drift), with and without the PGS early exit; every GPU handle of the
 parity leg runs the kernel shapes the timed region ran (cp_set_kernel_shape).
+secondary (rank 0, N = 1, the default C3 run only): the other configurations DESIGN.md §5
+reports (cp_rollout K = 200, bounds termination in both autoreset modes, fp64, C2), each on a
+fresh handle and timed the same way, so the driver's own run observes them.
 """
 import argparse
 import json
@@ -600,6 +603,51 @@ def parity_check(device, R, shape, B=128, steps=WINDOW):
                     "algorithm in double precision, state kept in double (DESIGN.md §7)"}
 
 
+# ------------------------------------------------------------ secondary lines
+# Configurations other than the headline, measured inside the default run (rank 0, N = 1) so the
+# driver's own run observes them: each on a fresh handle, reset + W untimed steps, then K steps
+# timed like the headline (synchronize on both sides).  (name, envs, steps, kwargs, continuous,
+# rollout K): the BASELINE.json configs and the modes DESIGN.md §5 reports.
+SECONDARY = (
+    ("C3_rollout_k200", 65536, 200, {}, False, 200),
+    ("C3_bounds_next_step", 65536, 200, {"done_on_bounds": True, "autoreset": "next_step"}, False, 0),
+    ("C3_bounds_same_step", 65536, 50, {"done_on_bounds": True}, False, 0),
+    ("C3_f64", 65536, 200, {"precision": "f64"}, False, 0),
+    ("C2_continuous_4096", 4096, 200, {}, True, 0),
+)
+
+
+def secondary_lines(dev, R, W=20):
+    """Each SECONDARY config: {value env-steps/s, ms_per_step, steps, warmup, resets}.  Bounds
+    termination needs its episodes desynchronised before the window: W + 40 untimed steps."""
+    out = {}
+    for name, B, K, kw, continuous, rollout in SECONDARY:
+        kw = dict(kw)
+        autoreset = kw.pop("autoreset", "same_step")
+        next_step = autoreset == "next_step"
+        w = W + (40 if kw.get("done_on_bounds") else 0)
+        env = BatchedCartpole(B, dev.index, action_repeats=R, steps_per_repeat=1, max_episode_len=WINDOW,
+                              initial_force=55.0, autoreset=autoreset, seed=SEED, **kw)
+        actions = make_actions(continuous, B, 0, w + K, SEED, dev)
+        env.reset()
+        for t in range(w):
+            env.step(actions[t])
+        torch.cuda.synchronize()
+        ep0 = episodes(env)
+        p0 = pending(env) if next_step else 0
+        el, _, _ = timed(env, actions, w, K, 1, dev, gather_at_end=False, rollout=rollout)
+        sim, ran = simulated_steps(env, B, K, ep0, p0, next_step)
+        out[name] = {"value": round(sim / el, 1), "unit": "env-steps/s", "ms_per_step": round(el / K * 1e3, 4),
+                     "envs": B, "steps": K, "warmup": w, "resets_in_window": ran,
+                     "kernel_shape": dict(zip(("step", "reset"), env.kernel_shape())),
+                     **({"rollout_k": rollout} if rollout else {}), **kw,
+                     **({"autoreset": autoreset} if next_step else {})}
+        env.close()
+        del actions
+        torch.cuda.synchronize()
+    return out
+
+
 # ----------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
@@ -612,9 +660,11 @@ def main():
     ap.add_argument("--dtype", choices=("f32", "f64"), default="f32",
                     help="f64: the fp64 kernel variant (cp_config.precision; the parity mode, DESIGN.md §7)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the cpu_baseline and parity legs")
+    ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the cpu_baseline, parity and secondary legs (profiling runs: only the headline's kernels)")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-steady-state", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the secondary configurations (rollout, bounds, fp64, C2) measured after the headline")
     ap.add_argument("--raster", action="store_true",
                     help="BASELINE.json configs[4] (C5): + in-kernel 50x50x3 fp16 raster obs per repeat")
     ap.add_argument("--cameras", type=int, default=1)
@@ -776,6 +826,12 @@ def main():
     }
     env.close()
     del actions
+    headline = not (args.rollout or args.continuous or args.dtype != "f32" or args.done_on_bounds or args.persistent
+                    or args.streams > 1 or args.raster or next_step or args.shape != "auto"
+                    or args.solver_iterations is not None or args.batch != 65536 or args.repeats != 3)
+    if rank == 0 and world == 1 and headline and not (args.no_secondary or args.no_cpu_baseline):
+        log("secondary configurations ...")
+        out["secondary"] = secondary_lines(dev, R)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
         out["cpu_baseline"] = cpu_baseline(R, args.cpu_seconds)

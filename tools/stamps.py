@@ -18,18 +18,19 @@ from cartpoleplusplus_amd.batched import BatchedCartpole  # noqa: E402
 
 B = int(os.environ.get("B", "65536"))
 steps = int(os.environ.get("STEPS", "150"))
+warm = int(os.environ.get("WARM", "20"))
 bounds = os.environ.get("BOUNDS", "0") == "1"
 env = BatchedCartpole(B, 0, action_repeats=3, initial_force=55.0, autoreset=True, seed=1234, done_on_bounds=bounds)
 gen = torch.Generator(device="cuda").manual_seed(1234)
-acts = torch.randint(0, 5, (steps + 20, B, 2), dtype=torch.int8, device="cuda", generator=gen)
+acts = torch.randint(0, 5, (steps + warm, B, 2), dtype=torch.int8, device="cuda", generator=gen)
 env.reset()
-for t in range(20):
+for t in range(warm):
     env.step(acts[t])
 out = (C.c_uint64 * 64)()
 rc = env.lib.cp_debug_stamps(env.h, out, 1)
 assert rc == 1, "not a stamp build (set CP_LIB_PATH to libcartpole_hip_stamps.so)"
 for t in range(steps):
-    env.step(acts[20 + t])
+    env.step(acts[warm + t])
 env.lib.cp_debug_stamps(env.h, out, 0)
 res = {"B": B, "steps": steps, "done_on_bounds": bounds}
 for name, base in (("step_kernel", 0), ("reset_kernel", 16)):

@@ -50,11 +50,12 @@ def main():
         env.step(rng.integers(0, 5, (B, 2)).astype(np.int8))
     lib.orc_stats_open(None)
     rows = np.loadtxt(path, dtype=np.int64)
-    # two lines per solve (island 0, island 1; same sweep count); env-major, then substep
+    # two lines per solve (island 0, island 1; same sweep count); one block per step call,
+    # env-major inside it, then substep: (steps, B, R)
     its = rows[0::2, 11]
     cap = cfg.phys.solver_iterations
-    per_env = its.reshape(B, -1)                    # (B, steps * R) solves
-    waves = per_env.reshape(B // 32, 32, -1).max(1)  # what each 64-lane wave pays
+    per_step = its.reshape(args.steps, B, R)
+    waves = per_step.reshape(args.steps, B // 32, 32, R).max(2)  # what each 64-lane wave pays
     out = {"envs": B, "warmup_steps": args.warmup, "recorded_steps": args.steps,
            "residual_threshold": cfg.phys.residual_threshold, "sweep_cap": cap,
            "solves": int(its.size), "mean_sweeps": float(its.mean()), "median_sweeps": float(np.median(its)),
