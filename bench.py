@@ -300,6 +300,9 @@ def simulated_steps(env, B, K, ep0, p0, next_step):
     return B * K - (ran + p0 - pending(env)), ran
 
 
+LAST_ENQUEUE_S = 0.0
+
+
 def timed(env, actions, t0, K, world, dev, gather_at_end, rollout=0):
     """K steps between barrier + synchronize; -> (max-over-ranks seconds, histogram, gathers).
     rollout > 0: the steps run as cp_rollout launches of up to `rollout` steps, split at the
@@ -326,6 +329,8 @@ def timed(env, actions, t0, K, world, dev, gather_at_end, rollout=0):
         r, _ = env.episode_returns()
         hist = return_histogram(gather_returns(r), WINDOW)
         gathers += 1
+    global LAST_ENQUEUE_S
+    LAST_ENQUEUE_S = time.perf_counter() - start   # host time to enqueue the K steps (diagnostic)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -732,6 +737,7 @@ def main():
     env.timing_begin(K)
     env.timing_stride(1 if args.rollout else STEP_EVENT_STRIDE, 1)
     elapsed, hist, gathers = timed(env, actions, W, K, world, dev, gather_at_end=world > 1, rollout=args.rollout)
+    enqueue_ms = LAST_ENQUEUE_S / K * 1e3
     tm = env.timing_end()
     simulated, resets = simulated_steps(env, B, K, ep0, p0, next_step)
 
@@ -746,6 +752,7 @@ def main():
         if world > 1:
             dist.all_reduce(r2)
         steady = {"steps": ss_steps, "ms_per_step": round(el2 / ss_steps * 1e3, 4),
+                  "host_enqueue_ms_per_step": round(LAST_ENQUEUE_S / ss_steps * 1e3, 4),
                   "value": round(int(r2[1].item()) / el2, 1), "resets": int(r2[0].item()), "collectives": g2,
                   "note": "one full 200-step episode cycle (its autoreset burst included) right after the timed "
                           "window, timed the same way"}
@@ -791,6 +798,7 @@ def main():
         "steps": K,
         "warmup": W,
         "ms_per_step": round(elapsed / K * 1e3, 4),
+        "host_enqueue_ms_per_step": round(enqueue_ms, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

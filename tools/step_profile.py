@@ -39,6 +39,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--phases", type=int, default=3)
+    ap.add_argument("--full", action="store_true", help="also print every step's time")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     B, R = a.batch, 3
@@ -46,11 +48,14 @@ def main():
                           initial_force=55.0, autoreset="same_step", seed=bench.SEED)
     actions = bench.make_actions(False, B, 0, a.steps, bench.SEED, dev)
     out = {"batch": B, "steps": a.steps}
-    for phase in ("cold", "second", "third"):
+    for phase in ("cold", "second", "third")[:a.phases]:
         ms = run(env, actions, a.steps)
         rng = {f"{lo}-{hi}": round(sum(ms[lo - 1:hi]) / (hi - lo + 1), 4)
-               for lo, hi in ((1, 5), (6, 25), (26, 100), (101, 199), (200, 200), (201, a.steps)) if hi <= a.steps}
+               for lo, hi in ((1, 5), (6, 25), (26, 100), (101, 199), (200, 200), (201, min(a.steps, 399)), (26, 225), (206, 405))
+               if hi <= a.steps}
         out[phase] = {"mean_ms_by_steps": rng, "first40": [round(x, 4) for x in ms[:40]]}
+        if a.full:
+            out[phase]["all"] = [round(x, 4) for x in ms]
     env.close()
     print(json.dumps(out))
 
