@@ -729,6 +729,12 @@ def main():
     env.reset()
     for t in range(W):
         env.step(actions[t])
+    # warm the return-gather path too (cp_episode_returns, the RCCL all-gather, torch's bincount):
+    # their first call in a process loads code objects and sets up buffers, ~17 ms once, which would
+    # otherwise land in whichever timed window holds the first 200-step boundary
+    r_, _ = env.episode_returns()
+    return_histogram(gather_returns(r_), WINDOW)
+    del r_
     torch.cuda.synchronize()
     log(f"rank {rank}: B={B} R={R} warmup {W} done; timing {K} steps")
 
