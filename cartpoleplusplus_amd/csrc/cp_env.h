@@ -32,6 +32,13 @@ constexpr bool kF64 = sizeof(real) == 8;
 #define CP_ALLIN_STEP 1
 #endif
 constexpr bool kAllinStep = CP_ALLIN_STEP != 0;  // the all-inside face-contact exit in the step kernel (C3 kernel -0.6 %, C2 -2 %)
+// the reset kernels' guard-free settle / bump-structure sweep loops (sweeps_c44_slow, sweeps_c4k_slow) in
+// the throughput-shaped step kernel too: the first ~10 steps of an episode are poles standing on their
+// carts, every wave at the 50-sweep cap (tools/episode_phase.py)
+#ifndef CP_STEP_C44
+#define CP_STEP_C44 0
+#endif
+constexpr bool kC44Step = CP_STEP_C44 != 0;
 
 using Bufs = cpc::Bufs;
 using Lqr = cpc::Lqr;
@@ -410,7 +417,8 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
             }
             for (int r = 0; r < R; ++r) {
                 for (int s = 0; s < SR; ++s) {
-                    substep<LAT && !kF64, false, kAllinStep, PM>(S, cfg.phys, L, pool, pool0, ov, G, ST);
+                    substep<LAT && !kF64, kC44Step && !LAT && !kF64 && !PM, kAllinStep, PM>(S, cfg.phys, L, pool, pool0,
+                                                                                              ov, G, ST);
                     if constexpr (LQR) {  // disturbance + control (:897-901), control from the pre-step state
                         apply_force_link<0>(S, f00 + u[0][0], f01 + u[0][1]);
                         apply_force_link<1>(S, f10 + u[1][0], f11 + u[1][1]);

@@ -749,15 +749,35 @@ struct Hdr {
     V3 n;
     uint32_t pk;
 };
+// Opaque register copies for the cross-row code of merged envs (CP_CROSS_OPAQUE).  Its inputs that
+// stay fixed during a solve (both islands' positions, inverse inertias and manifold headers, read
+// from the partner lane by DPP) are loop-invariant in the sweep loop; hoisted out of it, the partner
+// copies and selects stay live across every sweep of every wave, merged env or not, and push the
+// island rows' values into scratch.  The empty asm makes them fresh values inside each cross block.
+#ifndef CP_CROSS_OPAQUE
+#define CP_CROSS_OPAQUE 0
+#endif
+CP_DEV void opq(real& x) {
+    if constexpr (CP_CROSS_OPAQUE != 0) asm volatile("" : "+v"(x));
+}
+CP_DEV void opq(uint32_t& x) {
+    if constexpr (CP_CROSS_OPAQUE != 0) asm volatile("" : "+v"(x));
+}
+CP_DEV V3 opq3(V3 v) { opq(v.x); opq(v.y); opq(v.z); return v; }
+CP_DEV Sym opqs(Sym m) { opq(m.m0); opq(m.m1); opq(m.m2); opq(m.m3); opq(m.m4); opq(m.m5); return m; }
+
 template <int PAIR>
 CP_DEV Hdr pair_hdr(const Step& T, bool second) {
     constexpr int j = local_of(PAIR);
     const bool mine = (island_of(PAIR) != 0) == second;
-    const V3 on = partner(T.n[j]);
-    const uint32_t opk = partner_u(T.pk[j]);
+    const V3 tn = opq3(T.n[j]);
+    uint32_t tpk = T.pk[j];
+    opq(tpk);
+    const V3 on = partner(tn);
+    const uint32_t opk = partner_u(tpk);
     Hdr h;
-    h.n = selv(mine, T.n[j], on);
-    h.pk = mine ? T.pk[j] : opk;
+    h.n = selv(mine, tn, on);
+    h.pk = mine ? tpk : opk;
     return h;
 }
 
@@ -983,12 +1003,14 @@ CP_DEV Sym sel_sym(bool t, const Sym& a, const Sym& b) {
 }
 CP_DEV void cross_view(Sim& S, Step& T, const Isl& I, bool second) {
     const V3 v1 = partner(I.d1.v), w1 = partner(I.d1.w), v2 = partner(I.d2.v), w2 = partner(I.d2.w);
-    const V3 x1 = partner(I.d1.x), x2 = partner(I.d2.x);
-    const Sym M1 = partner_sym(I.d1.M), M2 = partner_sym(I.d2.M);
-    S.b[0].x = selv(second, x1, I.d1.x);
-    S.b[1].x = selv(second, x2, I.d2.x);
-    S.b[2].x = selv(second, I.d1.x, x1);
-    S.b[3].x = selv(second, I.d2.x, x2);
+    const V3 ox1 = opq3(I.d1.x), ox2 = opq3(I.d2.x);           // fixed during the solve: see opq
+    const Sym oM1 = opqs(I.d1.M), oM2 = opqs(I.d2.M);
+    const V3 x1 = partner(ox1), x2 = partner(ox2);
+    const Sym M1 = partner_sym(oM1), M2 = partner_sym(oM2);
+    S.b[0].x = selv(second, x1, ox1);
+    S.b[1].x = selv(second, x2, ox2);
+    S.b[2].x = selv(second, ox1, x1);
+    S.b[3].x = selv(second, ox2, x2);
     S.b[0].v = selv(second, v1, I.d1.v);
     S.b[0].w = selv(second, w1, I.d1.w);
     S.b[1].v = selv(second, v2, I.d2.v);
@@ -997,10 +1019,10 @@ CP_DEV void cross_view(Sim& S, Step& T, const Isl& I, bool second) {
     S.b[2].w = selv(second, I.d1.w, w1);
     S.b[3].v = selv(second, I.d2.v, v2);
     S.b[3].w = selv(second, I.d2.w, w2);
-    T.M[0] = sel_sym(second, M1, I.d1.M);
-    T.M[1] = sel_sym(second, M2, I.d2.M);
-    T.M[2] = sel_sym(second, I.d1.M, M1);
-    T.M[3] = sel_sym(second, I.d2.M, M2);
+    T.M[0] = sel_sym(second, M1, oM1);
+    T.M[1] = sel_sym(second, M2, oM2);
+    T.M[2] = sel_sym(second, oM1, M1);
+    T.M[3] = sel_sym(second, oM2, M2);
 }
 CP_DEV void cross_back(Isl& I, const Sim& S, bool second) {
     I.d1.v = selv(second, S.b[2].v, S.b[0].v);
@@ -1017,6 +1039,8 @@ struct Ctx {
     real mu0, mu1, mu2;
     int used, tot;   // rows of the own island, of the env
     bool merged, active;
+    bool xfric;      // merged, and a cross pair of the env has friction rows (only pole-pole contacts do:
+                     // the carts' friction is 0); else the friction half of the cross block is a no-op
 };
 
 // One PGS sweep range [it0, it1) over the lane's island (+ the cross rows of a merged
@@ -1111,7 +1135,10 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0,
             else isl_friction_rows<1, true>(c.I, c.T, c.mu1, pool, tol, bad, h1, h2);
             isl_friction_rows<2, false, PM>(c.I, c.T, c.mu2, pool, tol, bad);
         }
-        if (__ballot(cross) != 0ull && cross) {
+        // the friction half only where a cross pair has friction rows: cross_view + cross_back alone
+        // change no value (the whole-env view and back), and a wave with a merged env pays them per sweep
+        const bool crossf = cross && c.xfric;
+        if (__ballot(crossf) != 0ull && crossf) {
             cross_view(S, c.T, c.I, second);
             pair_friction_rows<5, PM>(S, c.T, second, P, pool0, tol, badc);
             pair_friction_rows<6, PM>(S, c.T, second, P, pool0, tol, badc);
@@ -1638,7 +1665,8 @@ CP_DEV void sweeps_fast(Ctx& c, FastIsl& F, Sim& S, const cp_physics& P, real* p
                 }
             }
         }
-        if (__ballot(cross) != 0ull && cross) {
+        const bool crossf = cross && c.xfric;  // see sweeps()
+        if (__ballot(crossf) != 0ull && crossf) {
             cross_view(S, c.T, c.I, second);
             pair_friction_rows<5>(S, c.T, second, P, pool0, tol, badc);
             pair_friction_rows<6>(S, c.T, second, P, pool0, tol, badc);
@@ -2085,6 +2113,12 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
     const uint32_t own_cross = (pk_cnt(T.pk[3]) + pk_cnt(T.pk[4])) > 0 ? 1u : 0u;
     const uint32_t any_cross = own_cross | partner_u(own_cross);
     c.merged = any_cross != 0u;
+    const uint32_t own_xf = (pk_fcnt(T.pk[3]) + pk_fcnt(T.pk[4])) > 0 ? 1u : 0u;
+    const uint32_t any_xf = own_xf | partner_u(own_xf);  // unconditionally, like any_cross
+    c.xfric = (any_cross & any_xf) != 0u;
+#ifdef CP_DIAG_NO_CROSS  // diagnostic only (wrong physics for merged envs): what the cross-row code costs
+    c.merged = false;
+#endif
 #ifdef CP_STAMPS
     ST.flags |= __ballot(c.merged) != 0ull ? 1u : 0u;
 #endif
