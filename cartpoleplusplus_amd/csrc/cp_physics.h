@@ -1003,14 +1003,11 @@ CP_DEV Sym sel_sym(bool t, const Sym& a, const Sym& b) {
 }
 CP_DEV void cross_view(Sim& S, Step& T, const Isl& I, bool second) {
     const V3 v1 = partner(I.d1.v), w1 = partner(I.d1.w), v2 = partner(I.d2.v), w2 = partner(I.d2.w);
-    const V3 ox1 = opq3(I.d1.x), ox2 = opq3(I.d2.x);           // fixed during the solve: see opq
-    const Sym oM1 = opqs(I.d1.M), oM2 = opqs(I.d2.M);
-    const V3 x1 = partner(ox1), x2 = partner(ox2);
+    const Sym oM1 = opqs(I.d1.M), oM2 = opqs(I.d2.M);           // fixed during the solve: see opq
     const Sym M1 = partner_sym(oM1), M2 = partner_sym(oM2);
-    S.b[0].x = selv(second, x1, ox1);
-    S.b[1].x = selv(second, x2, ox2);
-    S.b[2].x = selv(second, ox1, x1);
-    S.b[3].x = selv(second, ox2, x2);
+    // positions: S.b[*].x already holds them.  Both lanes of an env load and integrate the whole env
+    // identically, and island_view copies the lane's island out of S, so the partner's island
+    // positions equal this lane's S.b[*].x bit for bit (no DPP copies or selects per sweep)
     S.b[0].v = selv(second, v1, I.d1.v);
     S.b[0].w = selv(second, w1, I.d1.w);
     S.b[1].v = selv(second, v2, I.d2.v);
