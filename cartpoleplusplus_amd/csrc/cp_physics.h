@@ -1061,6 +1061,9 @@ CP_DEV void sweeps_p1_slow(Ctx& c, real* pool, real tol, int it0, int it1, Stamp
 #ifndef CP_P1_CHECK
 #define CP_P1_CHECK 8
 #endif
+#ifndef CP_PRIO_AFTER
+#define CP_PRIO_AFTER 16  // sweeps into a solve after which the step kernels' wave raises its priority (0: off)
+#endif
 template <bool C44 = false, bool PM = false>
 CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0, bool second, int it0, int it1,
                    Stamps& ST) {
@@ -1084,6 +1087,12 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0,
 #endif
     for (int it = it0; it < it1; ++it) {
         if (__ballot(c.active) == 0ull) break;
+#if CP_PRIO_AFTER > 0
+        // a wave deep into a long solve (a capped env: the launch's tail) takes its SIMD's issue
+        // priority from its co-resident partner: C3 +1.2 % (threshold 8, 16 or 30 alike)
+        if constexpr (!C44)
+            if (it == it0 + CP_PRIO_AFTER) __builtin_amdgcn_s_setprio(1);
+#endif
         if constexpr (C44 && !PM) {  // every still-active lane in the settle structure (the reset kernels)
             if ((it - it0) % CP_C44_CHECK == 0 && __ballot(c.active && !c44_ok(c)) == 0ull) {
                 sweeps_c44_slow(c, pool, tol, it, it1, ST);
@@ -1147,6 +1156,9 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0,
         const uint32_t pbad = partner_u(bad ? 1u : 0u);
         if (c.active && !bad && !badc && pbad == 0u) c.active = false;
     }
+#if CP_PRIO_AFTER > 0
+    if constexpr (!C44) __builtin_amdgcn_s_setprio(0);
+#endif
 }
 
 // ---- fast-form island rows.  Bullet's sequential-impulse solver
