@@ -45,6 +45,20 @@ CP_DEV double partner(double x) {
     const uint64_t lo = partner_u((uint32_t)u), hi = partner_u((uint32_t)(u >> 32));
     return __longlong_as_double((long long)(lo | (hi << 32)));
 }
+// Island ISL's lane of the pair, read by both lanes (DPP quad_perm [0,0,2,2] / [1,1,3,3]): one move where
+// "own value on one lane, the partner's on the other" took a partner read and a select.  Same rule.
+template <int ISL>
+CP_DEV uint32_t lane_of_u(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, ISL ? 0xF5 : 0xA0, 0xF, 0xF, false);
+}
+template <int ISL>
+CP_DEV float lane_of(float x) { return __uint_as_float(lane_of_u<ISL>(__float_as_uint(x))); }
+template <int ISL>
+CP_DEV double lane_of(double x) {
+    const uint64_t u = (uint64_t)__double_as_longlong(x);
+    const uint64_t lo = lane_of_u<ISL>((uint32_t)u), hi = lane_of_u<ISL>((uint32_t)(u >> 32));
+    return __longlong_as_double((long long)(lo | (hi << 32)));
+}
 
 // Integer fields (steps, episode, done, warm-start ids, packed headers) kept in a
 // real-typed array: the int32 bits in the first 4 bytes; an fp64 field's high word is 0

@@ -22,6 +22,8 @@ using cpc::clamp_sym;
 using cpc::fma_;
 using cpc::partner;
 using cpc::partner_u;
+using cpc::lane_of;
+using cpc::lane_of_u;
 using cpc::sqrt_;
 using cpc::to_bits;
 using real = CP_REAL;

@@ -475,6 +475,8 @@ CP_DEV void plane_space(V3 n, V3& t1, V3& t2) {
 // cross pairs 5 6; island 1 = ground, cart2, pole2 (pairs 2 3 9) plus 7 8.  Both
 // lanes keep the whole env state; they exchange results through DPP swaps.
 CP_DEV V3 partner(V3 v) { return mk(partner(v.x), partner(v.y), partner(v.z)); }
+template <int ISL>
+CP_DEV V3 lane_of3(V3 v) { return mk(lane_of<ISL>(v.x), lane_of<ISL>(v.y), lane_of<ISL>(v.z)); }
 
 // global pair of island `isl`'s local pair j (oracle: ISLAND_PAIR)
 CP_DEV int island_pair(int isl, int j) { return (int)(((isl ? 0x87932u : 0x65410u) >> (4 * j)) & 15u); }
@@ -768,16 +770,14 @@ CP_DEV Sym opqs(Sym m) { opq(m.m0); opq(m.m1); opq(m.m2); opq(m.m3); opq(m.m4); 
 
 template <int PAIR>
 CP_DEV Hdr pair_hdr(const Step& T, bool second) {
-    constexpr int j = local_of(PAIR);
-    const bool mine = (island_of(PAIR) != 0) == second;
+    (void)second;
+    constexpr int j = local_of(PAIR), isl = island_of(PAIR) != 0 ? 1 : 0;
     const V3 tn = opq3(T.n[j]);
     uint32_t tpk = T.pk[j];
     opq(tpk);
-    const V3 on = partner(tn);
-    const uint32_t opk = partner_u(tpk);
-    Hdr h;
-    h.n = selv(mine, tn, on);
-    h.pk = mine ? tpk : opk;
+    Hdr h;  // the owning island's lane's header, on both lanes
+    h.n = lane_of3<isl>(tn);
+    h.pk = lane_of_u<isl>(tpk);
     return h;
 }
 
@@ -1001,25 +1001,32 @@ CP_DEV Sym sel_sym(bool t, const Sym& a, const Sym& b) {
     r.m3 = t ? a.m3 : b.m3; r.m4 = t ? a.m4 : b.m4; r.m5 = t ? a.m5 : b.m5;
     return r;
 }
+template <int ISL>
+CP_DEV Sym lane_of_sym(const Sym& m) {
+    Sym r;
+    r.m0 = lane_of<ISL>(m.m0); r.m1 = lane_of<ISL>(m.m1); r.m2 = lane_of<ISL>(m.m2);
+    r.m3 = lane_of<ISL>(m.m3); r.m4 = lane_of<ISL>(m.m4); r.m5 = lane_of<ISL>(m.m5);
+    return r;
+}
 CP_DEV void cross_view(Sim& S, Step& T, const Isl& I, bool second) {
-    const V3 v1 = partner(I.d1.v), w1 = partner(I.d1.w), v2 = partner(I.d2.v), w2 = partner(I.d2.w);
+    (void)second;
+    // island 0's bodies (cart, pole) from the pair's even lane, island 1's (cart2, pole2) from the odd
+    // lane, one DPP move per value on both lanes.  Positions: S.b[*].x already holds them.  Both lanes
+    // of an env load and integrate the whole env identically, and island_view copies the lane's island
+    // out of S, so the partner's island positions equal this lane's S.b[*].x bit for bit.
+    S.b[0].v = lane_of3<0>(I.d1.v);
+    S.b[0].w = lane_of3<0>(I.d1.w);
+    S.b[1].v = lane_of3<0>(I.d2.v);
+    S.b[1].w = lane_of3<0>(I.d2.w);
+    S.b[2].v = lane_of3<1>(I.d1.v);
+    S.b[2].w = lane_of3<1>(I.d1.w);
+    S.b[3].v = lane_of3<1>(I.d2.v);
+    S.b[3].w = lane_of3<1>(I.d2.w);
     const Sym oM1 = opqs(I.d1.M), oM2 = opqs(I.d2.M);           // fixed during the solve: see opq
-    const Sym M1 = partner_sym(oM1), M2 = partner_sym(oM2);
-    // positions: S.b[*].x already holds them.  Both lanes of an env load and integrate the whole env
-    // identically, and island_view copies the lane's island out of S, so the partner's island
-    // positions equal this lane's S.b[*].x bit for bit (no DPP copies or selects per sweep)
-    S.b[0].v = selv(second, v1, I.d1.v);
-    S.b[0].w = selv(second, w1, I.d1.w);
-    S.b[1].v = selv(second, v2, I.d2.v);
-    S.b[1].w = selv(second, w2, I.d2.w);
-    S.b[2].v = selv(second, I.d1.v, v1);
-    S.b[2].w = selv(second, I.d1.w, w1);
-    S.b[3].v = selv(second, I.d2.v, v2);
-    S.b[3].w = selv(second, I.d2.w, w2);
-    T.M[0] = sel_sym(second, M1, oM1);
-    T.M[1] = sel_sym(second, M2, oM2);
-    T.M[2] = sel_sym(second, oM1, M1);
-    T.M[3] = sel_sym(second, oM2, M2);
+    T.M[0] = lane_of_sym<0>(oM1);
+    T.M[1] = lane_of_sym<0>(oM2);
+    T.M[2] = lane_of_sym<1>(oM1);
+    T.M[3] = lane_of_sym<1>(oM2);
 }
 CP_DEV void cross_back(Isl& I, const Sim& S, bool second) {
     I.d1.v = selv(second, S.b[2].v, S.b[0].v);
@@ -1064,6 +1071,9 @@ CP_DEV void sweeps_p1_slow(Ctx& c, real* pool, real tol, int it0, int it1, Stamp
 #ifndef CP_PRIO_AFTER
 #define CP_PRIO_AFTER 16  // sweeps into a solve after which the step kernels' wave raises its priority (0: off)
 #endif
+#ifndef CP_PRIO_MODE
+#define CP_PRIO_MODE 0    // 0: for the rest of that solve; 1, 2: diagnostics (sticky, accumulated)
+#endif
 template <bool C44 = false, bool PM = false>
 CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0, bool second, int it0, int it1,
                    Stamps& ST) {
@@ -1090,8 +1100,18 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0,
 #if CP_PRIO_AFTER > 0
         // a wave deep into a long solve (a capped env: the launch's tail) takes its SIMD's issue
         // priority from its co-resident partner: C3 +1.2 % (threshold 8, 16 or 30 alike)
-        if constexpr (!C44)
-            if (it == it0 + CP_PRIO_AFTER) __builtin_amdgcn_s_setprio(1);
+        if constexpr (!C44) {
+            if (it == it0 + CP_PRIO_AFTER) {
+#if CP_PRIO_MODE == 2  // diagnostic: +1 per long solve of the step (the wave's level, up to 3)
+                const uint32_t lvl = __builtin_amdgcn_s_getreg((1 << 11) | (0 << 6) | 2) & 3u;  // STATUS.PRIORITY
+                if (lvl == 0u) __builtin_amdgcn_s_setprio(1);
+                else if (lvl == 1u) __builtin_amdgcn_s_setprio(2);
+                else __builtin_amdgcn_s_setprio(3);
+#else
+                __builtin_amdgcn_s_setprio(1);
+#endif
+            }
+        }
 #endif
         if constexpr (C44 && !PM) {  // every still-active lane in the settle structure (the reset kernels)
             if ((it - it0) % CP_C44_CHECK == 0 && __ballot(c.active && !c44_ok(c)) == 0ull) {
@@ -1156,7 +1176,7 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0,
         const uint32_t pbad = partner_u(bad ? 1u : 0u);
         if (c.active && !bad && !badc && pbad == 0u) c.active = false;
     }
-#if CP_PRIO_AFTER > 0
+#if CP_PRIO_AFTER > 0 && CP_PRIO_MODE == 0  // modes 1 (sticky) and 2 (accumulated): kept to the wave's end
     if constexpr (!C44) __builtin_amdgcn_s_setprio(0);
 #endif
 }
@@ -2165,16 +2185,15 @@ CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx
     const bool second = L.isl != 0;
     CP_STAMP(t3);
     {
-        const Isl& I = c.I;
-        const V3 v1 = partner(I.d1.v), w1 = partner(I.d1.w), v2 = partner(I.d2.v), w2 = partner(I.d2.w);
-        S.b[0].v = selv(second, v1, I.d1.v);
-        S.b[0].w = selv(second, w1, I.d1.w);
-        S.b[1].v = selv(second, v2, I.d2.v);
-        S.b[1].w = selv(second, w2, I.d2.w);
-        S.b[2].v = selv(second, I.d1.v, v1);
-        S.b[2].w = selv(second, I.d1.w, w1);
-        S.b[3].v = selv(second, I.d2.v, v2);
-        S.b[3].w = selv(second, I.d2.w, w2);
+        const Isl& I = c.I;  // whole-env velocities: island 0's from the even lane, island 1's from the odd
+        S.b[0].v = lane_of3<0>(I.d1.v);
+        S.b[0].w = lane_of3<0>(I.d1.w);
+        S.b[1].v = lane_of3<0>(I.d2.v);
+        S.b[1].w = lane_of3<0>(I.d2.w);
+        S.b[2].v = lane_of3<1>(I.d1.v);
+        S.b[2].w = lane_of3<1>(I.d1.w);
+        S.b[3].v = lane_of3<1>(I.d2.v);
+        S.b[3].w = lane_of3<1>(I.d2.w);
     }
     // refresh the warm-start cache of the lane's island.  A pair with no point before or after
     // the substep holds 0 impulses and keeps them: it is not rewritten (the id word is a 0xFF-padded prefix,
