@@ -661,11 +661,17 @@ CP_DEV void isl_warmstart(Isl& I, const Step& T, real* pool) {
     }
 }
 
+// CP_UNROLL_ROWS (diagnostic): the generic row loops unrolled to the 4-point bound like the +z ones
+#if defined(CP_UNROLL_ROWS) && CP_UNROLL_ROWS
+#define CP_ROW_LOOP(k, n) _Pragma("unroll") for (int k = 0; k < 4; ++k) if (k < (n))
+#else
+#define CP_ROW_LOOP(k, n) for (int k = 0; k < (n); ++k)
+#endif
 template <int J, bool PM = false>
 CP_DEV void isl_normal_rows(Isl& I, const Step& T, real* pool, real tol, bool& bad) {
     const uint32_t pk = T.pk[J];
     const int cnt = pk_cnt(pk), base = pk_base(pk);
-    for (int k = 0; k < cnt; ++k) {
+    CP_ROW_LOOP(k, cnt) {
         const int s = base + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
         real lam = pool_n(pool, F_LAM, s);
@@ -692,7 +698,7 @@ CP_DEV void isl_friction_rows(Isl& I, const Step& T, real mu, real* pool, real t
         asm volatile("" : "+v"(n.x), "+v"(n.y), "+v"(n.z));
         plane_space(n, t1, t2);
     }
-    for (int k = 0; k < fcnt; ++k) {
+    CP_ROW_LOOP(k, fcnt) {
         const int s = base + k, fs = fbase + k;
         if constexpr (PM) plane_space(pool_normal(pool, s), t1, t2);  // the point's own normal
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
