@@ -1107,6 +1107,9 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0,
         // a wave deep into a long solve (a capped env: the launch's tail) takes its SIMD's issue
         // priority from its co-resident partner: C3 +1.2 % (threshold 8, 16 or 30 alike)
         if constexpr (!C44) {
+#ifdef CP_PRIO_MERGED  // diagnostic: a wave holding a merged env (the launch's tail) raises its priority at once
+            if (it == it0 && __ballot(c.merged) != 0ull) __builtin_amdgcn_s_setprio(1);
+#endif
             if (it == it0 + CP_PRIO_AFTER) {
 #if CP_PRIO_MODE == 2  // diagnostic: +1 per long solve of the step (the wave's level, up to 3)
                 const uint32_t lvl = __builtin_amdgcn_s_getreg((1 << 11) | (0 << 6) | 2) & 3u;  // STATUS.PRIORITY
