@@ -30,7 +30,7 @@ FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=off", "-f
          "-Wno-unused-result",
          # LLVM's iterative ILP scheduler for gfx9: step kernel 0.634 -> 0.624 ms (r11);
          # scheduling never reorders a rounding, so the results stay bit-identical
-         "-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
+         "-mllvm", "-amdgpu-sched-strategy=" + os.environ.get("CP_SCHED_STRATEGY", "iterative-ilp")]
 
 
 def up_to_date(lib=LIB):
