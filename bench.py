@@ -4,8 +4,16 @@
     python bench.py [--gpus N --steps K --warmup W]                       # C3 (default)
     python bench.py --continuous --batch 4096                             # C2
     python bench.py --raster                                              # C5
+    python bench.py --gpus N                                              # C4: launches N ranks itself
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
-        --master-port P bench.py --gpus N --steps K --warmup W            # C4 at N = 8
+        --master-port P bench.py --gpus N --steps K --warmup W            # C4, externally launched
+
+Multi-GPU launch: with --gpus N > 1 and no WORLD_SIZE in the environment, this process counts the
+visible devices (torch.cuda.device_count(), which does not initialise the GPU), refuses with a
+clear error when fewer than N are visible, and otherwise starts torch.distributed.run with N
+ranks on 127.0.0.1 as a CHILD process (no exec, no GPU call in this parent) and exits with its
+code; the ranks run this same file.  Under an external launcher WORLD_SIZE must equal --gpus.
+Every rank checks the process group's size (rccl_world_size in the line) against --gpus.
 
 Workloads (the line's config.workload is derived from the arguments):
   C2  4,096 envs, continuous (B,2,2) U[-1,1] actions, R = 3
@@ -23,6 +31,9 @@ N*B*K / max-over-ranks wall.  A K-step window need not contain an autoreset burs
 episode is 200 steps) or, at N > 1, a return gather; so the line also reports
 resets_in_window, collectives_in_window, and a steady_state sub-object: one more full
 200-step cycle (its reset burst and one gather included) timed the same way.
+SURVEY.md §8d's "median of 5 runs": `median5` holds the headline window and 4 more K-step
+windows right after it (same definition as value, each its own barrier + synchronize), and
+steady_state.median5 five consecutive 200-step cycles; value itself stays the first window.
 
 roofline: the step kernel's algorithmic HBM bytes per launch over its
 average duration from HIP events recorded on its launch stream in the timed region
@@ -466,20 +477,26 @@ def gym_mirror_rate(steps=400):
     opts = p.parse_args(["--initial-force", "55"])
     env = bullet_cartpole.BulletCartpole(opts, discrete_actions=True)
     rng = np.random.default_rng(0)
+    np_state = np.random.get_state()   # the mirror draws its bumps from np.random, as the reference does
     np.random.seed(0)
-    t0 = time.perf_counter()
-    env.reset()
-    t_reset = time.perf_counter() - t0
-    n, resets, t0 = 0, 0, time.perf_counter()
-    while n < steps:
-        _, _, done, _ = env.step(rng.integers(0, 5, 2))
-        n += 1
-        if done:
-            env.reset()
-            resets += 1
-    dt = time.perf_counter() - t0
+    try:
+        t0 = time.perf_counter()
+        env.reset()
+        t_reset = time.perf_counter() - t0
+        n, resets, t0 = 0, 0, time.perf_counter()
+        while n < steps:
+            _, _, done, _ = env.step(rng.integers(0, 5, 2))
+            n += 1
+            if done:
+                env.reset()
+                resets += 1
+        dt = time.perf_counter() - t0
+        use_graph = env.use_graph
+    finally:
+        env.close()
+        np.random.set_state(np_state)
     return {"value": round(n / dt, 1), "unit": "env-steps/s", "ms_per_step": round(dt / n * 1e3, 4),
-            "reset_ms": round(t_reset * 1e3, 2), "step_as_hipgraph": env.use_graph,
+            "reset_ms": round(t_reset * 1e3, 2), "step_as_hipgraph": use_graph,
             "sample": f"C1 config on the GPU: B=1, R=2, F_init 55, discrete random actions, {n} steps incl. "
                       f"{resets} resets ({dt:.2f} s)"}
 
@@ -653,6 +670,60 @@ def secondary_lines(dev, R, W=20):
     return out
 
 
+# ----------------------------------------------------------------------- launch
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n, argv, dry_run=False):
+    """`--gpus N` without an external launcher: run this file as N ranks under
+    torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) in a CHILD process and
+    return its exit code.  Nothing here touches the GPU: torch.cuda.device_count() counts the
+    devices without initialising them, so the ranks own the GPUs from the start (and no
+    process that initialised the GPU ever execs).  Fewer visible devices than N is an error."""
+    import subprocess
+    if not dry_run:
+        visible = torch.cuda.device_count()
+        if visible < n:
+            log(f"bench.py: --gpus {n} needs {n} visible GPUs, {visible} visible "
+                f"(HIP_VISIBLE_DEVICES={os.environ.get('HIP_VISIBLE_DEVICES')!r}); not launching")
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only on this pool (RCCL)
+    log("bench.py: launching " + " ".join(cmd))
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run_rank(args, world, rank):
+    """`--cpu-dry-run` (tests/test_bench_launch.py): the launch and collective path of a rank with no
+    GPU work: the gloo process group, the shard rule and the return gather + histogram of bench's
+    C4 window on synthetic returns (each env's return = its global id mod 201)."""
+    dist.init_process_group("gloo")
+    try:
+        got = dist.get_world_size()
+        if got != args.gpus:
+            raise SystemExit(f"bench.py: process group has {got} ranks, --gpus {args.gpus}")
+        B = args.batch or 65536
+        spec = shard_spec(B, rank, world, seed=SEED)
+        ids = torch.arange(spec["env_id_offset"], spec["env_id_offset"] + B, dtype=torch.int64)
+        allret = gather_returns((ids % (WINDOW + 1)).to(torch.float32))
+        hist = return_histogram(allret, WINDOW)
+        expect = return_histogram((torch.arange(world * B) % (WINDOW + 1)).to(torch.float32), WINDOW)
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "rccl_world_size": got, "backend": "gloo",
+                              "global_batch": spec["global_batch"], "gathered": int(allret.numel()),
+                              "hist_equal_unsharded": bool(torch.equal(hist, expect))}), flush=True)
+    finally:
+        dist.destroy_process_group()
+
+
 # ----------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
@@ -692,23 +763,41 @@ def main():
                          "handed out by the next step (gymnasium >= 1.0 / envpool), overlapped with the steps")
     ap.add_argument("--solver-iterations", type=int, default=None,
                     help="override the PGS sweep cap (default: the model's 50; non-default runs are diagnostics)")
+    ap.add_argument("--no-median", action="store_true",
+                    help="skip the 4 extra K-step windows and 4 extra cycles of the median-of-5 (median5)")
+    ap.add_argument("--cpu-dry-run", action="store_true",
+                    help="launch / collective path only, on CPU with gloo (no GPU work; tests the --gpus N launcher)")
     args = ap.parse_args()
     if args.batch is None:
         args.batch = 4096 if args.continuous else 65536
     next_step = args.autoreset == "next_step"
     if next_step and (args.rollout or args.raster or args.streams > 1):
         ap.error("--autoreset next_step steps through cp_step only (no --rollout / --raster / --streams)")
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], dry_run=args.cpu_dry_run))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+        ap.error(f"--gpus {args.gpus} but the launcher's WORLD_SIZE is {world}: they must agree")
+    if args.cpu_dry_run:
+        if world == 1:
+            ap.error("--cpu-dry-run is for --gpus N > 1 (the launch path)")
+        dry_run_rank(args, world, rank)
+        return
+    ndev = torch.cuda.device_count()
+    if local >= ndev:
+        raise SystemExit(f"bench.py: rank {rank} has LOCAL_RANK {local} but {ndev} GPU(s) are visible")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     rccl_world = dist.get_world_size() if world > 1 else 1
+    if rccl_world != args.gpus:
+        raise SystemExit(f"bench.py: process group has {rccl_world} ranks, --gpus {args.gpus}")
 
     B, R, K, W = args.batch, args.repeats, args.steps, args.warmup
     spec = shard_spec(B, rank, world, seed=SEED)
@@ -725,7 +814,8 @@ def main():
     if args.raster:
         env.enable_raster(True, num_cameras=args.cameras)
     ss_steps = 0 if args.no_steady_state else WINDOW
-    actions = make_actions(args.continuous, B, spec["env_id_offset"], W + K + ss_steps, SEED, dev)
+    n_med = 1 if args.no_median else 5
+    actions = make_actions(args.continuous, B, spec["env_id_offset"], W + n_med * (K + ss_steps), SEED, dev)
     env.reset()
     for t in range(W):
         env.step(actions[t])
@@ -747,27 +837,48 @@ def main():
     tm = env.timing_end()
     simulated, resets = simulated_steps(env, B, K, ep0, p0, next_step)
 
-    steady = None
-    if ss_steps:
-        ep1 = episodes(env)
-        p1 = pending(env) if next_step else 0
-        el2, hist2, g2 = timed(env, actions, W + K, ss_steps, world, dev, gather_at_end=world > 1,
-                               rollout=args.rollout)
-        sim2, ran2 = simulated_steps(env, B, ss_steps, ep1, p1, next_step)
-        r2 = torch.tensor([ran2, sim2], device=dev, dtype=torch.int64)
+    def window(t0, n):
+        """One more n-step window from step t0, timed like the headline: (value over ranks, seconds,
+        resets, gathers, histogram, host enqueue s)."""
+        epj = episodes(env)
+        pj = pending(env) if next_step else 0
+        el_, hist_, g_ = timed(env, actions, t0, n, world, dev, gather_at_end=world > 1, rollout=args.rollout)
+        enq_ = LAST_ENQUEUE_S
+        sim_, ran_ = simulated_steps(env, B, n, epj, pj, next_step)
+        r_ = torch.tensor([ran_, sim_], device=dev, dtype=torch.int64)
         if world > 1:
-            dist.all_reduce(r2)
-        steady = {"steps": ss_steps, "ms_per_step": round(el2 / ss_steps * 1e3, 4),
-                  "host_enqueue_ms_per_step": round(LAST_ENQUEUE_S / ss_steps * 1e3, 4),
-                  "value": round(int(r2[1].item()) / el2, 1), "resets": int(r2[0].item()), "collectives": g2,
-                  "note": "one full 200-step episode cycle (its autoreset burst included) right after the timed "
-                          "window, timed the same way"}
-        hist = hist2 if hist2 is not None else hist
+            dist.all_reduce(r_)
+        return int(r_[1].item()) / el_, el_, int(r_[0].item()), g_, hist_, enq_
+
+    def med5(vals):
+        s = sorted(vals)
+        return {"median": round(s[len(s) // 2], 1), "min": round(s[0], 1), "max": round(s[-1], 1),
+                "spread": round((s[-1] - s[0]) / s[len(s) // 2], 4), "values": [round(v, 1) for v in vals]}
 
     rt = torch.tensor([resets, simulated], device=dev, dtype=torch.int64)
     if world > 1:
         dist.all_reduce(rt)
     value = int(rt[1].item()) / elapsed   # = world * B * K / elapsed except for NEXT_STEP's reset-only calls
+    win_values = [value]
+    for j in range(1, n_med):
+        win_values.append(window(W + j * K, K)[0])
+    median5 = None if n_med == 1 else {
+        **med5(win_values), "windows": n_med, "steps_per_window": K,
+        "note": "SURVEY.md §8d median of 5: the headline window (values[0] = value) and 4 more K-step windows "
+                "right after it, each between barrier + synchronize"}
+
+    steady = None
+    if ss_steps:
+        t_ss = W + n_med * K
+        cyc = [window(t_ss + j * ss_steps, ss_steps) for j in range(n_med)]
+        v2, el2, ran2, g2, hist2, enq2 = cyc[0]
+        steady = {"steps": ss_steps, "ms_per_step": round(el2 / ss_steps * 1e3, 4),
+                  "host_enqueue_ms_per_step": round(enq2 / ss_steps * 1e3, 4),
+                  "value": round(v2, 1), "resets": ran2, "collectives": g2,
+                  **({"median5": med5([c[0] for c in cyc])} if n_med > 1 else {}),
+                  "note": "one full 200-step episode cycle (its autoreset burst included) after the timed "
+                          "windows, timed the same way; median5 over 5 consecutive cycles (value = the first)"}
+        hist = cyc[-1][4] if cyc[-1][4] is not None else hist
     kind = "continuous" if args.continuous else "discrete"
     per_launch_s = tm["step_ms"] / max(1, tm["step_launches"]) / 1e3
     bytes_launch = B * step_kernel_bytes(R, 16 if args.continuous else 2, 8 if args.dtype == "f64" else 4)
@@ -805,6 +916,7 @@ def main():
         "warmup": W,
         "ms_per_step": round(elapsed / K * 1e3, 4),
         "host_enqueue_ms_per_step": round(enqueue_ms, 4),
+        "median5": median5,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -849,7 +961,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
         out["cpu_baseline"] = cpu_baseline(R, args.cpu_seconds)
-        out["cpu_baseline"]["gym_mirror_b1_gpu"] = gym_mirror_rate()
+        out["gym_mirror_b1_gpu"] = gym_mirror_rate()   # a GPU B = 1 measurement, beside (not in) cpu_baseline
         if not args.no_parity:
             log("parity vs oracle ...")
             out["parity"] = parity_check(dev, R, shape)

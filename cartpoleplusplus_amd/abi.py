@@ -5,7 +5,7 @@ library's entry points with these types.
 """
 import ctypes as C
 
-CP_ABI_VERSION = 4
+CP_ABI_VERSION = 5
 
 CP_BODY_GROUND, CP_BODY_CART, CP_BODY_POLE, CP_BODY_CART2, CP_BODY_POLE2 = range(5)
 CP_NUM_BODIES = 5
@@ -118,7 +118,11 @@ class cp_config(C.Structure):
         ("env_id_offset", C.c_int64),
         ("phys", cp_physics),
         ("precision", C.c_int32),
+        ("reset_flags", C.c_int32),
     ]
+
+
+CP_RESET_CLEAR_NONFINITE_FORCE = 0x1
 
 
 CP_PRECISION_F32 = 0

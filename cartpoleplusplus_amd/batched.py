@@ -151,8 +151,9 @@ class BatchedCartpole:
         """K env-steps in one kernel launch (cp_rollout): actions (K,B,2,2) float32 or (K,B,2)
         int8 -> (obs (K,B,R,2,7), reward (K,B), done (K,B)); bit for bit K step() calls.
         With autoreset, self.rollout_terminal_obs (K,B,R,2,7) holds the finishing obs of the
-        episodes that ended (terminal=False skips it).  The output tensors are reused by the
-        next rollout of the same K (clone them to keep them)."""
+        episodes that ended (terminal=False skips it).  Afterwards self.obs / reward / done (and
+        terminal_obs when collected) hold step K-1's values, as after K step() calls.  The returned
+        tensors are reused (overwritten) by the next rollout of the same K: clone them to keep them."""
         if not isinstance(actions, torch.Tensor):
             actions = torch.as_tensor(actions)
         if actions.dim() < 3:
@@ -177,7 +178,17 @@ class BatchedCartpole:
         obs, rew, done, self.rollout_terminal_obs = self._roll_bufs
         native.check(self.h, self.lib.cp_rollout(self.h, K, _ptr(actions), kind, _ptr(obs), _ptr(rew), _ptr(done),
                                                  _ptr(self.rollout_terminal_obs), self._stream()), "cp_rollout")
+        # the handle is K steps on: the step()-level attributes follow it (the last step's values)
         self.obs.copy_(obs[-1])
+        self.reward.copy_(rew[-1])
+        self.done.copy_(done[-1])
+        if self.terminal_obs is not None and self.rollout_terminal_obs is not None:
+            # step() writes an env's terminal obs when it finishes: keep each env's last one
+            d = done.bool()
+            fin = d.any(0)
+            k_last = (K - 1) - d.flip(0).to(torch.int32).argmax(0)
+            last = self.rollout_terminal_obs[k_last.long(), torch.arange(self.B, device=self.device)]
+            self.terminal_obs[fin] = last[fin]
         return obs, rew, done
 
     def set_kernel_shape(self, step="auto", reset="auto"):
@@ -287,4 +298,10 @@ class BatchedCartpole:
     def overflow_counts(self):
         o = torch.empty(self.B, device=self.device, dtype=torch.int32)
         native.check(self.h, self.lib.cp_overflow_counts(self.h, _ptr(o), self._stream()), "cp_overflow_counts")
+        return o
+
+    def nonfinite_counts(self):
+        """(B,) int32: env-steps and resets per env that ended with a non-finite body state."""
+        o = torch.empty(self.B, device=self.device, dtype=torch.int32)
+        native.check(self.h, self.lib.cp_nonfinite_counts(self.h, _ptr(o), self._stream()), "cp_nonfinite_counts")
         return o

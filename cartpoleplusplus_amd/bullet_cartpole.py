@@ -137,6 +137,12 @@ class BulletCartpole(Env):
     def render(self, mode, close):
         pass
 
+    def close(self):
+        """gym.Env.close (the reference relies on p.disconnect at exit): drop the captured step
+        graph, then the library handle and its device buffers."""
+        self._graph = None
+        self._env.close()
+
     def _step_eager(self, a):
         self._act.copy_(torch.from_numpy(a).view(1, 2, 2))
         obs, _, _ = self._env.step(self._act)

@@ -21,6 +21,15 @@
 #define CP_PM_PAIR_FIELDS 45
 #define CP_PM_FIELDS (CP_ISLAND_PAIRS * CP_PM_PAIR_FIELDS)
 
+// Scratch SoA (Bufs::scratch), one column per lane: rows [0, CP_SCR_HDR_FIELDS) hold the manifold
+// headers of CP_HDR_SCRATCH builds (4 per pair, written and read inside one substep); rows
+// [CP_SCR_RC_BASE, CP_SCR_FIELDS) hold cp_rollout's per-lane state machine (RC_* in cp_env.h), kept
+// across substeps -- disjoint, so a header write never lands on the rollout's state.
+#define CP_SCR_HDR_FIELDS (4 * CP_ISLAND_PAIRS)
+#define CP_SCR_RC_BASE CP_SCR_HDR_FIELDS
+#define CP_SCR_RC_FIELDS 10
+#define CP_SCR_FIELDS (CP_SCR_RC_BASE + CP_SCR_RC_FIELDS)
+
 namespace cpc {
 
 CP_DEV float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
@@ -129,10 +138,11 @@ struct Bufs {
     float* last_ret;   // [B]
     int32_t* last_len; // [B]
     int32_t* overflow; // [B]
+    int32_t* nonfinite;  // [B] steps / resets that ended with a non-finite body state
     int32_t* list;     // [B] reset list
     int32_t* count;    // reset list length (one of the handle's two counters, by step parity)
     int32_t* count_next;  // the other counter: zeroed by the reset kernel for the next call
-    void* scratch;     // [4*CP_ISLAND_PAIRS][2B] real: manifold headers (CP_HDR_SCRATCH builds)
+    void* scratch;     // [CP_SCR_FIELDS][2B] real: manifold headers (CP_HDR_SCRATCH builds), cp_rollout state
     uint64_t* stamps;  // [waves][8] diagnostic phase cycles (CP_STAMPS builds only)
     float* rposes;     // [B][R][4][7] repeat-end poses for the raster obs (NULL: raster off)
     float4* rtable;    // [C][H*W] (d, t_ground) then [C][H*W] uint8 ground class (cp_raster_table_kernel)

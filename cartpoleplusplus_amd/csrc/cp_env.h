@@ -145,6 +145,29 @@ CP_DEV void store_sim(const Sim& S, const Soa& st, uint32_t o) {
 CP_DEV int32_t ldi(const Soa& st, int f, uint32_t o) { return (int32_t)to_bits(st.ld(f, o)); }
 CP_DEV void sti(const Soa& st, int f, uint32_t o, int32_t v) { st.st(f, o, bits_to<real>((uint32_t)v)); }
 
+// true if every body value (pos, quat, v, w of the 4 bodies) is finite: x * 0 is +-0 for a finite
+// x and NaN for an inf or NaN, so the fma chain stays a zero exactly when all 52 values are finite
+CP_DEV bool sim_finite(const Sim& S) {
+    real acc = real(0.0);
+#pragma unroll
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        const Body& y = S.b[d];
+        acc = fma_(y.x.x, real(0.0), acc); acc = fma_(y.x.y, real(0.0), acc); acc = fma_(y.x.z, real(0.0), acc);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc = fma_(y.q[k], real(0.0), acc);
+        acc = fma_(y.v.x, real(0.0), acc); acc = fma_(y.v.y, real(0.0), acc); acc = fma_(y.v.z, real(0.0), acc);
+        acc = fma_(y.w.x, real(0.0), acc); acc = fma_(y.w.y, real(0.0), acc); acc = fma_(y.w.z, real(0.0), acc);
+    }
+    return acc == real(0.0);
+}
+
+// CP_RESET_CLEAR_NONFINITE_FORCE: a reset zeroes a cart's pending force with a non-finite component
+CP_DEV V3 reset_force(const cp_config& cfg, V3 f) {
+    if (!(cfg.reset_flags & CP_RESET_CLEAR_NONFINITE_FORCE)) return f;
+    const real z = fma_(f.x, real(0.0), fma_(f.y, real(0.0), f.z * real(0.0)));
+    return z == real(0.0) ? f : mk(real(0.0), real(0.0), real(0.0));
+}
+
 CP_DEV void write_obs_row(const Sim& S, float* dst) {
     dst[0] = (float)S.b[0].x.x; dst[1] = (float)S.b[0].x.y; dst[2] = (float)S.b[0].x.z;
     dst[3] = (float)S.b[0].q[0]; dst[4] = (float)S.b[0].q[1]; dst[5] = (float)S.b[0].q[2]; dst[6] = (float)S.b[0].q[3];
@@ -270,6 +293,7 @@ __global__ void __launch_bounds__(256) cp_init_kernel(cp_config cfg, Bufs b) {
     b.last_ret[i] = 0.0f;
     b.last_len[i] = 0;
     b.overflow[i] = 0;
+    b.nonfinite[i] = 0;
 }
 
 // LAT = false: the throughput shape of the step kernel (2 waves per SIMD), for reset bursts
@@ -298,6 +322,8 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     CP_RT(r0);
     Sim S;
     load_sim(S, G.st, G.off);  // pending forces survive the reset (pybullet keeps them)
+    S.f0 = reset_force(cfg, S.f0);
+    S.f2 = reset_force(cfg, S.f2);
     if constexpr (PM)  // resetBasePositionAndOrientation: no cached contact survives the teleport
         for (int j = 0; j < CP_ISLAND_PAIRS; ++j) G.sp(pmf(j, 0), bits_to<real>(0u));
     const int episode = ldi(G.st, CP_SF_EPISODE, G.off);
@@ -336,6 +362,7 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     if (!lead) return;
     store_sim(S, G.st, G.off);
     b.overflow[i] += ov;
+    if (!sim_finite(S)) b.nonfinite[i] += 1;
     float row[14];
     write_obs_row(S, row);
     const int R = cfg.action_repeats;
@@ -452,6 +479,7 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
             if (LQR && lqr_done) done = true;
             if (lead) {
                 store_sim(S, G.st, G.off);
+                if (!sim_finite(S)) b.nonfinite[i] += 1;
                 sti(G.st, CP_SF_STEPS, G.off, steps);
                 put_out(&reward_out[i], 1.0f);  // bullet_cartpole.py:260
                 put_out(&done_out[i], (uint8_t)(done ? 1 : 0));
@@ -534,9 +562,10 @@ CP_DEV void action_forces(const void* actions, size_t row, real F, real f[4]) {
 // L2-resident, each lane reads only its own writes) rather than in registers across the
 // substep, whose peak register pressure they would add to; the action forces are re-read
 // from the action array after each substep.
-enum : int { RC_K = 0, RC_SUB, RC_STEPS, RC_EPISODE, RC_FLAGS, RC_RET, RC_U0, RC_U1, RC_U2, RC_U3, RC_FIELDS };
+enum : int { RC_K = CP_SCR_RC_BASE, RC_SUB, RC_STEPS, RC_EPISODE, RC_FLAGS, RC_RET, RC_U0, RC_U1, RC_U2, RC_U3, RC_END };
 enum : uint32_t { RF_DONE = 1u, RF_RESETTING = 2u, RF_LAST_SIM = 4u, RF_LQR_DONE = 8u };
-static_assert(RC_FIELDS <= 4 * CP_ISLAND_PAIRS, "rollout state must fit the scratch SoA's per-lane fields");
+static_assert(RC_END - RC_K == CP_SCR_RC_FIELDS, "rollout state rows of the scratch SoA (cp_common.h)");
+static_assert(RC_K >= CP_SCR_HDR_FIELDS, "rollout state must not overlap the CP_HDR_SCRATCH manifold headers");
 
 template <int KIND, bool LQR, bool LAT, bool PM = false>
 __global__ void __launch_bounds__(WAVE)
@@ -638,6 +667,7 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
             if (LQR && (flags & RF_LQR_DONE)) done = true;
             const float ret = __uint_as_float(to_bits(G.lx(RC_RET))) + 1.0f;
             if (lead) {
+                if (!sim_finite(S)) b.nonfinite[e] += 1;
                 put_out(&reward_out[(size_t)k * B + e], 1.0f);
                 put_out(&done_out[(size_t)k * B + e], (uint8_t)(done ? 1 : 0));
             }
@@ -651,6 +681,8 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
                 }
                 flags |= RF_DONE;
                 if (cfg.autoreset) {  // the reset kernel's prologue: pending forces survive
+                    S.f0 = reset_force(cfg, S.f0);
+                    S.f2 = reset_force(cfg, S.f2);
 #pragma unroll
                     for (int d = 0; d < CP_NUM_DYN; ++d) {
                         S.b[d].x = mk(cfg.phys.spawn_pos[d + 1][0], cfg.phys.spawn_pos[d + 1][1],
@@ -692,6 +724,7 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
             }
             // reset end (the reset kernel's epilogue): every repeat slot shows the new pose
             if (lead) {
+                if (!sim_finite(S)) b.nonfinite[env()] += 1;
                 float row[14];
                 write_obs_row(S, row);
                 float* o = obs_out + (size_t)k * obs_step + env() * R * 14;

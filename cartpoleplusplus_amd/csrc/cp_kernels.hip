@@ -304,6 +304,8 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
         return fail(nullptr, "cp_create: autoreset must be CP_AUTORESET_OFF, _SAME_STEP or _NEXT_STEP");
     if (cfg->precision != CP_PRECISION_F32 && cfg->precision != CP_PRECISION_F64)
         return fail(nullptr, "cp_create: precision must be CP_PRECISION_F32 or CP_PRECISION_F64");
+    if (cfg->reset_flags & ~CP_RESET_CLEAR_NONFINITE_FORCE)
+        return fail(nullptr, "cp_create: reset_flags holds an unknown CP_RESET_* bit");
     if ((unsigned long long)cfg->num_envs * CP_STATE_FIELDS * (cfg->precision == CP_PRECISION_F64 ? 8ull : 4ull) >= (1ull << 32) ||
         (unsigned long long)cfg->num_envs * cfg->action_repeats * 14ull * 4ull >= (1ull << 32))
         return fail(nullptr, "cp_create: num_envs too large for one handle (SoA arrays must stay below 4 GiB)");
@@ -342,9 +344,10 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     CP_ALLOC(h->b.last_ret, B * sizeof(float));
     CP_ALLOC(h->b.last_len, B * sizeof(int32_t));
     CP_ALLOC(h->b.overflow, B * sizeof(int32_t));
+    CP_ALLOC(h->b.nonfinite, B * sizeof(int32_t));
     CP_ALLOC(h->b.list, B * sizeof(int32_t));
     CP_ALLOC(h->count2, 3 * sizeof(int32_t));
-    CP_ALLOC(h->b.scratch, (size_t)4 * CP_ISLAND_PAIRS * 2 * B * rb);
+    CP_ALLOC(h->b.scratch, (size_t)CP_SCR_FIELDS * 2 * B * rb);
     CP_ALLOC(h->b.stamps, CP_STAMP_SLOTS * sizeof(uint64_t));
     CP_ALLOC(h->b.stepped, B * sizeof(uint8_t));
     if (cfg->phys.model_flags & CP_MODEL_PERSISTENT) {  // the persistent manifolds, empty
@@ -411,6 +414,7 @@ void cp_destroy(cp_handle* h) {
     (void)hipFree(h->b.last_ret);
     (void)hipFree(h->b.last_len);
     (void)hipFree(h->b.overflow);
+    (void)hipFree(h->b.nonfinite);
     (void)hipFree(h->b.list);
     (void)hipFree(h->count2);
     (void)hipFree(h->b.scratch);
@@ -693,6 +697,11 @@ int cp_set_state(cp_handle* h, const void* state_in, void* stream) {
     size_t n = (size_t)CP_STATE_FIELDS * h->cfg.num_envs;
     CP_TRY(h, hipMemcpyAsync(h->b.state, state_in, n * (h->f64 ? sizeof(double) : sizeof(float)), hipMemcpyDeviceToDevice,
                              (hipStream_t)stream));
+    // the persistent manifolds are not part of the state SoA: no cached contact survives a teleport
+    // (as in the reset kernel), so the next step rebuilds them from the new poses
+    if (h->b.pman)
+        CP_TRY(h, hipMemsetAsync(h->b.pman, 0, (size_t)CP_PM_FIELDS * 2 * h->cfg.num_envs *
+                                                   (h->f64 ? sizeof(double) : sizeof(float)), (hipStream_t)stream));
     return 0;
 }
 
@@ -705,6 +714,15 @@ int cp_episode_returns(cp_handle* h, float* returns_out, int32_t* lengths_out, v
     if (returns_out) CP_TRY(h, hipMemcpyAsync(returns_out, h->b.last_ret, B * sizeof(float), hipMemcpyDeviceToDevice, st));
     if (lengths_out)
         CP_TRY(h, hipMemcpyAsync(lengths_out, h->b.last_len, B * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    return 0;
+}
+
+int cp_nonfinite_counts(cp_handle* h, int32_t* out, void* stream) {
+    if (!h || !out) return fail(h, "cp_nonfinite_counts: null argument");
+    CP_TRY(h, hipSetDevice(h->device));
+    if (join_next_step(h, (hipStream_t)stream)) return -1;
+    CP_TRY(h, hipMemcpyAsync(out, h->b.nonfinite, (size_t)h->cfg.num_envs * sizeof(int32_t), hipMemcpyDeviceToDevice,
+                             (hipStream_t)stream));
     return 0;
 }
 

@@ -79,7 +79,7 @@ struct Sim {
 using Soa = SoaT<real>;
 struct Mem {
     Soa st;           // state SoA [CP_STATE_FIELDS][B]
-    Soa scr;          // scratch SoA [4*CP_ISLAND_PAIRS][2B], one column per lane
+    Soa scr;          // scratch SoA [CP_SCR_FIELDS][2B], one column per lane (cp_common.h)
     Soa pm;           // CP_MODEL_PERSISTENT: the island's persistent manifolds [PM_FIELDS][2B], one column per lane
     uint32_t off;     // env index * sizeof(real)
     uint32_t woff;    // off + island * CP_ISLAND_PAIRS fields  (warm-start ids of the lane's island)
@@ -88,7 +88,7 @@ struct Mem {
     CP_DEV static Mem make(void* state, void* scratch, int B, int env, int isl, void* pman = nullptr) {
         Mem m;
         m.st = Soa::make(state, B, CP_STATE_FIELDS);
-        m.scr = Soa::make(scratch, 2 * B, 4 * CP_ISLAND_PAIRS);
+        m.scr = Soa::make(scratch, 2 * B, CP_SCR_FIELDS);
         m.pm = Soa::make(pman, pman ? 2 * B : 0, CP_PM_FIELDS);  // null: an empty resource (no PM kernel reads it)
         m.off = Soa::eoff(env);
         m.woff = m.off + (uint32_t)(isl * CP_ISLAND_PAIRS) * m.st.fstride;

@@ -22,6 +22,7 @@ EXPORTS = (
     "cp_event_record_bytes", "cp_encode_events", "cp_eventlog_open", "cp_eventlog_write", "cp_eventlog_close",
     "cp_set_lqr", "cp_get_stepped", "cp_replay_init", "cp_replay_add", "cp_replay_sample",
     "cp_state_bytes", "cp_set_kernel_shape", "cp_get_kernel_shape", "cp_rollout",
+    "cp_nonfinite_counts",
 )
 
 _lib = None
@@ -57,6 +58,7 @@ def load():
         "cp_set_state": (I, [VP, VP, VP]),
         "cp_episode_returns": (I, [VP, VP, VP, VP]),
         "cp_overflow_counts": (I, [VP, VP, VP]),
+        "cp_nonfinite_counts": (I, [VP, VP, VP]),
         "cp_timing_begin": (I, [VP, I]),
         "cp_timing_stride": (I, [VP, I, I]),
         "cp_debug_stamps": (I, [VP, P(C.c_uint64), I]),

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CP_ABI_VERSION 4
+#define CP_ABI_VERSION 5
 
 /* Bodies, in the reference's loadURDF order (bullet_cartpole.py:154-160). */
 #define CP_BODY_GROUND 0
@@ -142,7 +142,16 @@ typedef struct cp_config {
     int64_t env_id_offset;       /* global id of env 0 (rank * B when sharded) */
     cp_physics phys;
     int32_t precision;           /* CP_PRECISION_F32 (the product path) or _F64  */
+    int32_t reset_flags;         /* CP_RESET_* (0: the reference's behaviour)   */
 } cp_config;
+
+/* cp_config.reset_flags.  CLEAR_NONFINITE_FORCE: a reset (cp_reset, autoreset, cp_rollout's
+ * inline reset) zeroes a cart's pending external force if any component of it is not finite.
+ * Off by default: pybullet keeps pending forces across resetBasePositionAndOrientation
+ * (bullet_cartpole.py:313-323), so an env whose state went NaN (the explicit
+ * gyroscopic term of a spinning loose pole) carries its NaN force into every later episode;
+ * with the flag the next reset brings it back.  cp_nonfinite_counts shows such envs either way. */
+#define CP_RESET_CLEAR_NONFINITE_FORCE 0x1
 
 /* Arithmetic type of a handle (cp_config.precision).  F32: the fp32 kernels, state float32.
  * F64: the same algorithm in double precision (the parity variant: bit-exact against the
@@ -251,7 +260,10 @@ int cp_set_lqr(cp_handle* h, const float* gains, int per_env, float* state8_out,
                float done_angle);
 
 /* Full env state, SoA [CP_STATE_FIELDS][B] of the handle's real type (float32, or float64
- * for CP_PRECISION_F64 handles), device pointers of cp_state_bytes(h) bytes. */
+ * for CP_PRECISION_F64 handles), device pointers of cp_state_bytes(h) bytes.
+ * CP_MODEL_PERSISTENT handles: the persistent contact manifolds are not part of this state;
+ * cp_set_state clears them (a teleport, as resetBasePositionAndOrientation in cp_reset), so a
+ * get_state -> set_state round trip mid-episode rebuilds the contacts from the poses. */
 int cp_get_state(cp_handle* h, void* state_out, void* stream);
 int cp_set_state(cp_handle* h, const void* state_in, void* stream);
 int64_t cp_state_bytes(const cp_handle* h);   /* CP_STATE_FIELDS * B * sizeof(real); <0: error */
@@ -275,6 +287,13 @@ int cp_episode_returns(cp_handle* h, float* returns_out, int32_t* lengths_out, v
 /* Diagnostics: per-env count of contact rows dropped by the CP_ISLAND_* caps since
  * creation (int32 [B], device).  0 everywhere in normal operation. */
 int cp_overflow_counts(cp_handle* h, int32_t* out, void* stream);
+
+/* Diagnostics: per-env count (int32 [B], device) of env-steps and resets since creation that
+ * ended with a non-finite body state (a NaN or inf in any position, quaternion, linear or
+ * angular velocity of cart, pole, cart2, pole2).  0 everywhere in normal operation; an env
+ * that went NaN keeps counting up (one per step) until a reset brings it back (see
+ * CP_RESET_CLEAR_NONFINITE_FORCE).  The oracle counts the same (oracle/cp_oracle.c). */
+int cp_nonfinite_counts(cp_handle* h, int32_t* out, void* stream);
 
 /* Kernel timing with HIP events recorded on the launch stream around every
  * step-kernel and reset-kernel launch of the next `max_launches` cp_step /

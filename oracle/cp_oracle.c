@@ -1327,6 +1327,7 @@ int orc_envs_create(const cp_config* cfg, orc_envs** out) {
     e->last_ret = (float*)calloc(B, sizeof(float));
     e->last_len = (int32_t*)calloc(B, sizeof(int32_t));
     e->overflow = (int32_t*)calloc(B, sizeof(int32_t));
+    e->nonfinite = (int32_t*)calloc(B, sizeof(int32_t));
     e->sweeps = (int32_t*)calloc((size_t)B * 2, sizeof(int32_t));
     e->merged = (int32_t*)calloc(B, sizeof(int32_t));
     e->pman = calloc(B * CP_NUM_PAIRS, sizeof(pman_t));
@@ -1348,7 +1349,7 @@ int orc_envs_create(const cp_config* cfg, orc_envs** out) {
 void orc_envs_destroy(orc_envs* e) {
     if (!e) return;
     free(e->state); free(e->term_obs); free(e->bump_forces); free(e->ret_acc);
-    free(e->last_ret); free(e->last_len); free(e->overflow); free(e->sweeps); free(e->merged); free(e->pman);
+    free(e->last_ret); free(e->last_len); free(e->overflow); free(e->nonfinite); free(e->sweeps); free(e->merged); free(e->pman);
     free(e->held_obs);
     free(e);
 }
@@ -1360,6 +1361,8 @@ void orc_envs_get_state(const orc_envs* e, void* out) {
 }
 void orc_envs_set_state(orc_envs* e, const void* in) {
     memcpy(e->state, in, (size_t)CP_STATE_FIELDS * e->B * sizeof(real));
+    /* cp_set_state: the persistent manifolds (outside the state SoA) are cleared */
+    memset(e->pman, 0, (size_t)e->B * CP_NUM_PAIRS * sizeof(pman_t));
 }
 
 /* bump force k (0..initial_force_steps-1) on cart c (0: cart, 1: cart2), LINK frame */
@@ -1386,10 +1389,25 @@ static void bump_force(const orc_envs* e, int i, int episode, int k, int c, real
     *fy = F * s;
 }
 
+/* 1 if every body value (pos, quat, v, w of the 4 dynamic bodies) is finite (cp_nonfinite_counts) */
+static int sim_finite(const sim_t* S) {
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        const real v[13] = {S->x[d].x, S->x[d].y, S->x[d].z, S->q[d][0], S->q[d][1], S->q[d][2], S->q[d][3],
+                            S->v[d].x, S->v[d].y, S->v[d].z, S->w[d].x, S->w[d].y, S->w[d].z};
+        for (int k = 0; k < 13; ++k)
+            if (!isfinite(v[k])) return 0;
+    }
+    return 1;
+}
+
 static void reset_one(orc_envs* e, int i, float* obs_row /* R*14 */) {
     const cp_config* cfg = &e->cfg;
     sim_t S;
     env_load(e, i, &S);   /* keeps the pending forces (pybullet does not clear them) */
+    if (cfg->reset_flags & CP_RESET_CLEAR_NONFINITE_FORCE)   /* opt-in: a NaN force does not outlive the reset */
+        for (int c = 0; c < 2; ++c)
+            if (!isfinite(S.f[2 * c].x) || !isfinite(S.f[2 * c].y) || !isfinite(S.f[2 * c].z))
+                S.f[2 * c] = mk(RC(0), RC(0), RC(0));
     int episode = get_i(e, CP_SF_EPISODE, i);
     for (int d = 0; d < CP_NUM_DYN; ++d) {
         S.x[d] = mk((real)cfg->phys.spawn_pos[d + 1][0], (real)cfg->phys.spawn_pos[d + 1][1],
@@ -1415,6 +1433,7 @@ static void reset_one(orc_envs* e, int i, float* obs_row /* R*14 */) {
         }
     }
     e->overflow[i] += ov;
+    if (!sim_finite(&S)) e->nonfinite[i] += 1;
     env_store(e, i, &S);
     float row[14];
     write_obs_row(&S, row);
@@ -1572,6 +1591,7 @@ static void step_one(orc_envs* e, int i, const void* actions, int kind, float* o
     int done = steps >= cfg->max_episode_len;
     if (cfg->done_on_bounds && bounds_exceeded(e, &S)) done = 1;
     if (lqr_done) done = 1;
+    if (!sim_finite(&S)) e->nonfinite[i] += 1;
     env_store(e, i, &S);
     set_i(e, CP_SF_STEPS, i, steps);
     reward_out[i] = 1.0f;            /* bullet_cartpole.py:260 */
@@ -1631,6 +1651,7 @@ int orc_envs_step_omp(orc_envs* e, const void* actions, int kind, float* obs_out
     return used;
 }
 void orc_envs_sweeps(const orc_envs* e, int32_t* out) { memcpy(out, e->sweeps, (size_t)e->B * 2 * sizeof(int32_t)); }
+void orc_envs_nonfinite(const orc_envs* e, int32_t* out) { memcpy(out, e->nonfinite, (size_t)e->B * sizeof(int32_t)); }
 void orc_envs_merged(const orc_envs* e, int32_t* out) { memcpy(out, e->merged, (size_t)e->B * sizeof(int32_t)); }
 void orc_envs_episode_returns(const orc_envs* e, float* ret, int32_t* len) {
     if (ret) memcpy(ret, e->last_ret, (size_t)e->B * sizeof(float));

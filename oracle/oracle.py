@@ -88,6 +88,7 @@ def load(precision="f32"):
         "orc_envs_episode_returns": (None, [VP, VP, VP]),
         "orc_envs_sweeps": (None, [VP, VP]),
         "orc_envs_merged": (None, [VP, VP]),
+        "orc_envs_nonfinite": (None, [VP, VP]),
         "orc_render_frame": (None, [VP, VP, VP, C.c_int, VP]),
         "orc_philox4x32_10": (None, [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]),
         "orc_sincos_turns": (None, [C.c_float, P(C.c_float), P(C.c_float)]),
@@ -274,6 +275,12 @@ class Envs:
         contact: pairs 5-8, solved in the order 0 2 1 3 4 9 5 6 7 8)."""
         out = np.zeros(self.B, np.int32)
         self.lib.orc_envs_merged(self.h, _ptr(out))
+        return out
+
+    def nonfinite(self):
+        """(B,) steps / resets that ended with a non-finite body state (cp_nonfinite_counts)."""
+        out = np.zeros(self.B, np.int32)
+        self.lib.orc_envs_nonfinite(self.h, _ptr(out))
         return out
 
     def sweeps(self):

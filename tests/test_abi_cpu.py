@@ -156,8 +156,13 @@ def test_cp_create_rejects_inconsistent_derived_fields():
     assert b"model_flags" in lib.cp_last_error(None)
     # a threshold near pi/2, built by default_config: accepted (relative tolerance on tan;
     # without a GPU cp_create then fails later, for another reason)
+    cfg = native.default_config(num_envs=4)
+    cfg.reset_flags = 0x80                        # an unknown CP_RESET_* bit
+    assert lib.cp_create(C.byref(cfg), 0, C.byref(h)) != 0
+    assert b"reset_flags" in lib.cp_last_error(None)
     cfg = native.default_config(num_envs=4, angle_threshold=1.45)
-    lib.cp_create(C.byref(cfg), 0, C.byref(h))
+    if lib.cp_create(C.byref(cfg), 0, C.byref(h)) == 0:   # a GPU host: do not leak the handle
+        lib.cp_destroy(h)
     assert b"angle_threshold" not in lib.cp_last_error(None)
 
 

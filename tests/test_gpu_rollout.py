@@ -47,6 +47,12 @@ def _compare(roll, step_env, actions, what):
         for k in range(actions.shape[0]):
             _assert_same(_np(roll.rollout_terminal_obs[k])[d[k]], _np(st[k])[d[k]], f"{what} terminal obs step {k}")
     _assert_same(_np(roll.get_state()), _np(step_env.get_state()), what + " state")
+    # the step()-level attributes follow the handle after a rollout
+    _assert_same(_np(roll.obs), _np(step_env.obs), what + " .obs")
+    _assert_same(_np(roll.reward), _np(step_env.reward), what + " .reward")
+    _assert_same(_np(roll.done), _np(step_env.done), what + " .done")
+    if roll.terminal_obs is not None:
+        _assert_same(_np(roll.terminal_obs), _np(step_env.terminal_obs), what + " .terminal_obs")
     _assert_same(_np(roll.episode_returns()[0]), _np(step_env.episode_returns()[0]), what + " returns")
     _assert_same(_np(roll.episode_returns()[1]), _np(step_env.episode_returns()[1]), what + " lengths")
     return _np(rd)
@@ -116,3 +122,73 @@ def test_rollout_rejects_side_outputs():
     o, r, d = env.rollout(torch.zeros((3, 16, 2), dtype=torch.int8, device="cuda"))
     assert o.shape == (3, 16, 2, 2, 7) and torch.isfinite(o).all()
     assert env.lib.cp_rollout(env.h, 0, o.data_ptr(), 1, o.data_ptr(), r.data_ptr(), d.data_ptr(), None, None) != 0
+
+
+@shapes
+def test_rollout_discrete_bounds_desynchronised_vs_oracle(oracle_mod, shape):
+    """The discrete, bounds-termination, desynchronised-reset rollout straight against the oracle
+    (not only against cp_step): every step's obs, reward, done and terminal obs, then the state."""
+    B, K = 128, 80
+    cfg, (roll, _) = _handles(shape, num_envs=B, action_repeats=3, initial_force=55.0, seed=77, autoreset=1,
+                              done_on_bounds=1, max_episode_len=30)
+    orc = oracle_mod.Envs(abi.cp_config.from_buffer_copy(cfg))
+    _assert_same(_np(roll.reset()), orc.reset(), "reset")
+    st = _np(roll.get_state())
+    st.view(np.int32)[abi.CP_SF_STEPS] = np.random.default_rng(21).integers(0, 30, B)
+    roll.set_state(torch.from_numpy(st).cuda())
+    orc.set_state(np.ascontiguousarray(st))
+    a = np.random.default_rng(22).integers(0, 5, (K, B, 2)).astype(np.int8)
+    go, gr, gd = roll.rollout(torch.from_numpy(a).cuda())
+    go, gr, gd, gt = _np(go), _np(gr), _np(gd), _np(roll.rollout_terminal_obs)
+    ks = set()
+    for k in range(K):
+        oo, orw, od, ot = orc.step(np.ascontiguousarray(a[k]), terminal=True)
+        _assert_same(go[k], oo, f"obs step {k}")
+        _assert_same(gr[k], orw, f"reward step {k}")
+        _assert_same(gd[k], od, f"done step {k}")
+        dk = od.astype(bool)
+        _assert_same(gt[k][dk], ot[dk], f"terminal obs step {k}")
+        ks |= {k} if dk.any() else set()
+    assert gd.sum() > B and len(ks) > 20          # resets on many different steps
+    _assert_same(_np(roll.get_state()), orc.get_state(), "final state")
+    _assert_same(_np(roll.episode_returns()[0]), orc.episode_returns()[0], "returns")
+
+
+@pytest.mark.parametrize("shape", [("throughput", "throughput"), ("latency", "latency")], ids=["tp", "lat"])
+def test_rollout_full_size_c3_k200_across_the_burst(oracle_mod, shape):
+    """cp_rollout at the size bench.py times it (C3_rollout_k200): 65,536 envs, bench's hashed
+    discrete actions, K = 200 in one launch; every step counter starts at 190, so the 65,536-env
+    autoreset burst happens at k = 9 inside the launch.  All envs: finite obs, unit quaternions,
+    done exactly at k = 9.  Four 128-env blocks (incl. the last) re-simulated on the oracle from the
+    same state: every step's obs, done and terminal obs bit for bit, then the block's final state."""
+    import bench
+    B, K = 65536, 200
+    cfg, (roll, _) = _handles(shape, num_envs=B, action_repeats=3, initial_force=55.0, seed=bench.SEED,
+                              autoreset=1, max_episode_len=200)
+    roll.reset()
+    st = _np(roll.get_state())
+    st.view(np.int32)[abi.CP_SF_STEPS] = 190
+    roll.set_state(torch.from_numpy(st).cuda())
+    acts = bench.make_actions(False, B, 0, K, bench.SEED, roll.device)
+    go, gr, gd = roll.rollout(acts)
+    assert bool(torch.isfinite(go).all())
+    q = go[..., 3:7].double()
+    assert bool(torch.allclose(q.norm(dim=-1), torch.ones_like(q[..., 0]), atol=1e-5))
+    dsum = gd.sum(1).cpu().numpy()
+    assert dsum[9] == B and dsum[:9].sum() == 0 and dsum[10:].sum() == 0
+    a_np = acts.cpu().numpy()
+    gst = _np(roll.get_state())
+    for lo in (0, 17000, 40960, B - 128):
+        sub = abi.cp_config.from_buffer_copy(cfg)
+        sub.num_envs, sub.env_id_offset = 128, lo
+        orc = oracle_mod.Envs(sub)
+        orc.set_state(np.ascontiguousarray(st[:, lo:lo + 128]))
+        bo, bd, bt = _np(go[:, lo:lo + 128]), _np(gd[:, lo:lo + 128]), _np(roll.rollout_terminal_obs[:, lo:lo + 128])
+        for k in range(K):
+            oo, orw, od, ot = orc.step(np.ascontiguousarray(a_np[k, lo:lo + 128]), terminal=True)
+            _assert_same(bo[k], oo, f"block {lo} obs step {k}")
+            _assert_same(bd[k], od, f"block {lo} done step {k}")
+            if od.any():
+                _assert_same(bt[k][od.astype(bool)], ot[od.astype(bool)], f"block {lo} terminal obs step {k}")
+        _assert_same(gst[:, lo:lo + 128], orc.get_state(), f"block {lo} final state")
+    roll.close()
