@@ -716,11 +716,34 @@ CP_DEV void isl_friction_rows(Isl& I, const Step& T, real mu, real* pool, real t
 #define CP_EZ_LOOP(k, n) _Pragma("unroll") for (int k = 0; k < 4; ++k) if (k < (n))
 // The rows of ground pair J (0 or 1) when every lane of the wave with rows on it has a +z
 // normal (wave-uniform choice in sweeps()): the same sweep with isl_row_ez.
+// CP_EZ_PREFETCH: software-pipelined LDS reads.  Each row's operands are read from the pool one row
+// ahead (inside the next row's own guard, so no lane reads a slot it does not own), so the ds_read
+// latency of row k + 1 overlaps row k's dependent VALU chain instead of stalling at its s_waitcnt.
+// No row writes a slot another row of the same loop reads (row k writes only its own lambda), so the
+// values -- and every result -- are those of the plain loop.
+#ifndef CP_EZ_PREFETCH
+#define CP_EZ_PREFETCH 0
+#endif
 template <int J>
 CP_DEV void isl_normal_rows_ez(Isl& I, const Step& T, real* pool, real tol, bool& bad) {
     static_assert(loc_a<J>() == 0, "ground pairs only");
     const uint32_t pk = T.pk[J];
     const int cnt = pk_cnt(pk), base = pk_base(pk);
+#if CP_EZ_PREFETCH
+    struct Op { real rx, ry, ie, tg, lam; };
+    auto ld = [&](int s) { return Op{pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_IE, s),
+                                     pool_n(pool, F_TG, s), pool_n(pool, F_LAM, s)}; };
+    Op cur{};
+    if (cnt > 0) cur = ld(base);
+    CP_EZ_LOOP(k, cnt) {
+        Op nxt = cur;
+        if (k + 1 < 4 && k + 1 < cnt) nxt = ld(base + k + 1);
+        real lam = cur.lam;
+        bad |= isl_row_ez<loc_b<J>(), 0, false>(I, mk(cur.rx, cur.ry, real(0.0)), cur.ie, cur.tg, lam, real(0.0), tol);
+        pool_n(pool, F_LAM, base + k) = lam;
+        cur = nxt;
+    }
+#else
     CP_EZ_LOOP(k, cnt) {
         const int s = base + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
@@ -728,6 +751,7 @@ CP_DEV void isl_normal_rows_ez(Isl& I, const Step& T, real* pool, real tol, bool
         bad |= isl_row_ez<loc_b<J>(), 0, false>(I, rb, pool_n(pool, F_IE, s), pool_n(pool, F_TG, s), lam, real(0.0), tol);
         pool_n(pool, F_LAM, s) = lam;
     }
+#endif
 }
 template <int J>
 CP_DEV void isl_friction_rows_ez(Isl& I, const Step& T, real mu, real* pool, real tol, bool& bad) {
@@ -736,6 +760,26 @@ CP_DEV void isl_friction_rows_ez(Isl& I, const Step& T, real mu, real* pool, rea
     const int fcnt = pk_fcnt(pk);
     if (fcnt == 0) return;
     const int base = pk_base(pk), fbase = pk_fbase(pk);
+#if CP_EZ_PREFETCH
+    struct Op { real rx, ry, rz, ln, ie1, ie2, l1, l2; };
+    auto ld = [&](int s, int fs) {
+        return Op{pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s), pool_n(pool, F_LAM, s),
+                  pool_f(pool, FF_IE1, fs), pool_f(pool, FF_IE2, fs), pool_f(pool, FF_L1, fs), pool_f(pool, FF_L2, fs)};
+    };
+    Op cur = ld(base, fbase);
+    CP_EZ_LOOP(k, fcnt) {
+        Op nxt = cur;
+        if (k + 1 < 4 && k + 1 < fcnt) nxt = ld(base + k + 1, fbase + k + 1);
+        const V3 rb = mk(cur.rx, cur.ry, cur.rz);
+        const real bound = mu * cur.ln;
+        real l1 = cur.l1, l2 = cur.l2;
+        bad |= isl_row_ez<loc_b<J>(), 1, true>(I, rb, cur.ie1, real(0.0), l1, bound, tol);
+        bad |= isl_row_ez<loc_b<J>(), 2, true>(I, rb, cur.ie2, real(0.0), l2, bound, tol);
+        pool_f(pool, FF_L1, fbase + k) = l1;
+        pool_f(pool, FF_L2, fbase + k) = l2;
+        cur = nxt;
+    }
+#else
     CP_EZ_LOOP(k, fcnt) {
         const int s = base + k, fs = fbase + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
@@ -746,6 +790,7 @@ CP_DEV void isl_friction_rows_ez(Isl& I, const Step& T, real mu, real* pool, rea
         pool_f(pool, FF_L1, fs) = l1;
         pool_f(pool, FF_L2, fs) = l2;
     }
+#endif
 }
 
 // ---- merged solve (an env with a cross-island contact): both lanes run the
