@@ -733,11 +733,18 @@ CP_DEV void isl_normal_rows_ez(Isl& I, const Step& T, real* pool, real tol, bool
     struct Op { real rx, ry, ie, tg, lam; };
     auto ld = [&](int s) { return Op{pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_IE, s),
                                      pool_n(pool, F_TG, s), pool_n(pool, F_LAM, s)}; };
+#if CP_EZ_PREFETCH == 2  // unguarded: the next slot clamped into the pool, no per-row branch or copies
+    Op cur = ld(base < MAXP - 1 ? base : MAXP - 1);
+    CP_EZ_LOOP(k, cnt) {
+        const int sn = base + k + 1;
+        Op nxt = ld(sn < MAXP - 1 ? sn : MAXP - 1);
+#else
     Op cur{};
     if (cnt > 0) cur = ld(base);
     CP_EZ_LOOP(k, cnt) {
         Op nxt = cur;
         if (k + 1 < 4 && k + 1 < cnt) nxt = ld(base + k + 1);
+#endif
         real lam = cur.lam;
         bad |= isl_row_ez<loc_b<J>(), 0, false>(I, mk(cur.rx, cur.ry, real(0.0)), cur.ie, cur.tg, lam, real(0.0), tol);
         pool_n(pool, F_LAM, base + k) = lam;
@@ -768,8 +775,13 @@ CP_DEV void isl_friction_rows_ez(Isl& I, const Step& T, real mu, real* pool, rea
     };
     Op cur = ld(base, fbase);
     CP_EZ_LOOP(k, fcnt) {
+#if CP_EZ_PREFETCH == 2
+        const int sn = base + k + 1, fsn = fbase + k + 1;
+        Op nxt = ld(sn < MAXP - 1 ? sn : MAXP - 1, fsn < MAXF - 1 ? fsn : MAXF - 1);
+#else
         Op nxt = cur;
         if (k + 1 < 4 && k + 1 < fcnt) nxt = ld(base + k + 1, fbase + k + 1);
+#endif
         const V3 rb = mk(cur.rx, cur.ry, cur.rz);
         const real bound = mu * cur.ln;
         real l1 = cur.l1, l2 = cur.l2;
