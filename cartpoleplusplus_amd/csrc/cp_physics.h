@@ -667,10 +667,33 @@ CP_DEV void isl_warmstart(Isl& I, const Step& T, real* pool) {
 #else
 #define CP_ROW_LOOP(k, n) for (int k = 0; k < (n); ++k)
 #endif
+#ifndef CP_EZ_PREFETCH
+#define CP_EZ_PREFETCH 0
+#endif
 template <int J, bool PM = false>
 CP_DEV void isl_normal_rows(Isl& I, const Step& T, real* pool, real tol, bool& bad) {
     const uint32_t pk = T.pk[J];
     const int cnt = pk_cnt(pk), base = pk_base(pk);
+#if CP_EZ_PREFETCH >= 4
+    if constexpr (!PM) {  // the counted loop software-pipelined: row k + 1's operands in flight during row k
+        struct Op { real rx, ry, rz, ie, tg, lam; };
+        auto ld = [&](int s) {
+            s = s < MAXP - 1 ? s : MAXP - 1;
+            return Op{pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s), pool_n(pool, F_IE, s),
+                      pool_n(pool, F_TG, s), pool_n(pool, F_LAM, s)};
+        };
+        Op cur = ld(base);
+        for (int k = 0; k < cnt; ++k) {
+            const Op nxt = ld(base + k + 1);
+            real lam = cur.lam;
+            bad |= isl_row<loc_a<J>(), loc_b<J>(), false>(I, mk(cur.rx, cur.ry, cur.rz), T.n[J], cur.ie, cur.tg, lam,
+                                                          real(0.0), tol);
+            pool_n(pool, F_LAM, base + k) = lam;
+            cur = nxt;
+        }
+        return;
+    }
+#endif
     CP_ROW_LOOP(k, cnt) {
         const int s = base + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
@@ -698,6 +721,30 @@ CP_DEV void isl_friction_rows(Isl& I, const Step& T, real mu, real* pool, real t
         asm volatile("" : "+v"(n.x), "+v"(n.y), "+v"(n.z));
         plane_space(n, t1, t2);
     }
+#if CP_EZ_PREFETCH >= 4
+    if constexpr (!PM) {  // software-pipelined like isl_normal_rows (the normal rows of this sweep are done)
+        struct Op { real rx, ry, rz, ln, ie1, ie2, l1, l2; };
+        auto ld = [&](int s, int fs) {
+            s = s < MAXP - 1 ? s : MAXP - 1;
+            fs = fs < MAXF - 1 ? fs : MAXF - 1;
+            return Op{pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s), pool_n(pool, F_LAM, s),
+                      pool_f(pool, FF_IE1, fs), pool_f(pool, FF_IE2, fs), pool_f(pool, FF_L1, fs), pool_f(pool, FF_L2, fs)};
+        };
+        Op cur = ld(base, fbase);
+        for (int k = 0; k < fcnt; ++k) {
+            const Op nxt = ld(base + k + 1, fbase + k + 1);
+            const V3 rb = mk(cur.rx, cur.ry, cur.rz);
+            const real bound = mu * cur.ln;
+            real l1 = cur.l1, l2 = cur.l2;
+            bad |= isl_row<loc_a<J>(), loc_b<J>(), true>(I, rb, t1, cur.ie1, real(0.0), l1, bound, tol);
+            bad |= isl_row<loc_a<J>(), loc_b<J>(), true>(I, rb, t2, cur.ie2, real(0.0), l2, bound, tol);
+            pool_f(pool, FF_L1, fbase + k) = l1;
+            pool_f(pool, FF_L2, fbase + k) = l2;
+            cur = nxt;
+        }
+        return;
+    }
+#endif
     CP_ROW_LOOP(k, fcnt) {
         const int s = base + k, fs = fbase + k;
         if constexpr (PM) plane_space(pool_normal(pool, s), t1, t2);  // the point's own normal
@@ -955,6 +1002,25 @@ CP_DEV void pair_normal_rows(Sim& S, const Step& T, bool second, const cp_physic
     const Hdr H = pair_hdr<PAIR>(T, second);
     const uint32_t pk = H.pk;
     const int cnt = pk_cnt(pk), base = pk_base(pk);
+#if CP_EZ_PREFETCH >= 4
+    if constexpr (!PM) {  // software-pipelined (isl_normal_rows): each row writes only its own lambda
+        struct Op { real rx, ry, rz, ie, tg, lam; };
+        auto ld = [&](int s) {
+            s = s < MAXP - 1 ? s : MAXP - 1;
+            return Op{pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s), pool_n(pool, F_IE, s),
+                      pool_n(pool, F_TG, s), pool_n(pool, F_LAM, s)};
+        };
+        Op cur = ld(base);
+        for (int k = 0; k < cnt; ++k) {
+            const Op nxt = ld(base + k + 1);
+            real lam = cur.lam;
+            bad |= solve_row<A, B, false>(S, T, P, mk(cur.rx, cur.ry, cur.rz), H.n, cur.ie, cur.tg, lam, real(0.0), tol);
+            pool_n(pool, F_LAM, base + k) = lam;
+            cur = nxt;
+        }
+        return;
+    }
+#endif
     for (int k = 0; k < cnt; ++k) {
         const int s = base + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
@@ -1188,6 +1254,13 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0,
     // has its own normal, the generic rows)
 #ifdef CP_NO_EZ
     const bool ez0 = false, ez1 = false;
+#elif defined(CP_EZ_DYNAMIC)
+    // diagnostic: re-decided every sweep over the lanes still solving (once the tilted-cart lanes have
+    // converged, the capped lanes left run the +z rows)
+    const bool nz0 = pk_cnt(c.T.pk[0]) > 0 && !is_plus_z(c.T.n[0]);
+    const bool nz1 = pk_cnt(c.T.pk[1]) > 0 && !is_plus_z(c.T.n[1]);
+    bool ez0 = !PM && __ballot(nz0) == 0ull;
+    bool ez1 = !PM && __ballot(nz1) == 0ull;
 #else
     const bool ez0 = !PM && __ballot(pk_cnt(c.T.pk[0]) > 0 && !is_plus_z(c.T.n[0])) == 0ull;
     const bool ez1 = !PM && __ballot(pk_cnt(c.T.pk[1]) > 0 && !is_plus_z(c.T.n[1])) == 0ull;
@@ -1238,6 +1311,12 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0,
 #endif
 #ifdef CP_STAMPS
         ST.sweeps += 1;
+#endif
+#if defined(CP_EZ_DYNAMIC) && !defined(CP_NO_EZ)
+        if (it > it0) {
+            ez0 = !PM && __ballot(c.active && nz0) == 0ull;
+            ez1 = !PM && __ballot(c.active && nz1) == 0ull;
+        }
 #endif
         bool bad = false, badc = false;
 #if CP_EZ_PREFETCH >= 3
