@@ -877,11 +877,9 @@ def main():
         return {"median": round(s[len(s) // 2], 1), "min": round(s[0], 1), "max": round(s[-1], 1),
                 "spread": round((s[-1] - s[0]) / s[len(s) // 2], 4), "values": [round(v, 1) for v in vals]}
 
-    nf = torch.tensor([int((env.nonfinite_counts() > 0).sum().item())], device=dev, dtype=torch.int64)
     rt = torch.tensor([resets, simulated], device=dev, dtype=torch.int64)
     if world > 1:
         dist.all_reduce(rt)
-        dist.all_reduce(nf)
     value = int(rt[1].item()) / elapsed   # = world * B * K / elapsed except for NEXT_STEP's reset-only calls
     win_values = [value]
     for j in range(1, n_med):
@@ -903,6 +901,11 @@ def main():
                   "note": "one full 200-step episode cycle (its autoreset burst included) after the timed "
                           "windows, timed the same way; median5 over 5 consecutive cycles (value = the first)"}
         hist = cyc[-1][4] if cyc[-1][4] is not None else hist
+
+    # envs whose state went non-finite at any point of the run (every window above included)
+    nf = torch.tensor([int((env.nonfinite_counts() > 0).sum().item())], device=dev, dtype=torch.int64)
+    if world > 1:
+        dist.all_reduce(nf)
     kind = "continuous" if args.continuous else "discrete"
     per_launch_s = tm["step_ms"] / max(1, tm["step_launches"]) / 1e3
     bytes_launch = B * step_kernel_bytes(R, 16 if args.continuous else 2, 8 if args.dtype == "f64" else 4)

@@ -171,8 +171,13 @@ def test_rollout_full_size_c3_k200_across_the_burst(oracle_mod, shape):
     roll.set_state(torch.from_numpy(st).cuda())
     acts = bench.make_actions(False, B, 0, K, bench.SEED, roll.device)
     go, gr, gd = roll.rollout(acts)
-    assert bool(torch.isfinite(go).all())
-    q = go[..., 3:7].double()
+    # finite obs and unit quaternions on every env but the model's rare NaN envs (the loose-pole yaw-spin
+    # divergence, DESIGN.md §3: a few per 65,536 envs and 200 steps), which cp_nonfinite_counts shows
+    fin = torch.isfinite(go).flatten(2).all(2).all(0)
+    bad = set(torch.nonzero(~fin).flatten().tolist())
+    counted = set(torch.nonzero(roll.nonfinite_counts()).flatten().tolist())
+    assert len(bad) <= 16 and bad <= counted and len(counted) <= 16, (sorted(bad), sorted(counted))
+    q = go[:, fin][..., 3:7].double()
     assert bool(torch.allclose(q.norm(dim=-1), torch.ones_like(q[..., 0]), atol=1e-5))
     dsum = gd.sum(1).cpu().numpy()
     assert dsum[9] == B and dsum[:9].sum() == 0 and dsum[10:].sum() == 0
