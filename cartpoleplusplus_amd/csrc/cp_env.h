@@ -148,6 +148,10 @@ CP_DEV void sti(const Soa& st, int f, uint32_t o, int32_t v) { st.st(f, o, bits_
 // true if every body value (pos, quat, v, w of the 4 bodies) is finite: x * 0 is +-0 for a finite
 // x and NaN for an inf or NaN, so the fma chain stays a zero exactly when all 52 values are finite
 CP_DEV bool sim_finite(const Sim& S) {
+#ifdef CP_NO_NONFINITE  // diagnostic A/B build: the counter's cost (never counts)
+    (void)S;
+    return true;
+#endif
     real acc = real(0.0);
 #pragma unroll
     for (int d = 0; d < CP_NUM_DYN; ++d) {

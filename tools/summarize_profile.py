@@ -5,8 +5,10 @@ Per kernel: launches, average duration (kernel-trace), SQ counters per launch, a
 HBM traffic per launch from FETCH_SIZE / WRITE_SIZE (KiB units).  gfx950 correction
 (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts 64 B per 128-B request, i.e. half the
 bytes of wide coalesced reads, so read bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE is
-exact for 16-B streaming stores.  Our kernels use 4-B per-lane buffer loads/stores,
-which the guide lists as uncalibrated: the JSON carries the raw counters too.
+exact for 16-B streaming stores.  Round 4 calibrated both on the step kernel's own access shape
+(4-B per-lane buffer loads / stores over the state SoA, two lanes per env; tools/micro/soa_traffic.hip,
+profiles/rd4a_pmc_micro.json): FETCH_SIZE = 0.50 x the bytes read, WRITE_SIZE = 1.00 x the bytes
+written, so the same correction holds.  The JSON carries the raw counters too.
 """
 import csv
 import json
