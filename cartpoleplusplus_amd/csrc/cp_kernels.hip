@@ -16,6 +16,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/cartpole_amd.h"
@@ -150,6 +151,7 @@ struct cp_handle {
     cp_timing timing;
     cp_raster_config raster;
     uint16_t* pixels;  // raster obs output (NULL: raster off)
+    bool render_v1;    // CP_RENDER_V1=1 at cp_create: the round-3 small-frame render kernel (A/B diagnostic)
     int32_t* count2;   // [3] reset-list counters: [0] [1] alternating by call (SAME_STEP: each reset launch
                        // zeroes the other one; NEXT_STEP: one per reset list), [2] NEXT_STEP's cp_reset list
     int par;           // counter the next call appends to
@@ -318,6 +320,10 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     h->lqr = cpc::Lqr{nullptr, 0, nullptr, 0.0f, 0.0f};
     h->f64 = cfg->precision == CP_PRECISION_F64;
     h->pixels = nullptr;
+    {
+        const char* v1 = std::getenv("CP_RENDER_V1");
+        h->render_v1 = v1 && v1[0] == '1';
+    }
     h->npar = 0;
     h->ninflight = -1;
     h->reset_req = h->step_req = CP_SHAPE_AUTO;
@@ -435,7 +441,23 @@ static int launch_render(cp_handle* h, const int32_t* list, const int32_t* count
     const int C = h->raster.num_cameras, R = h->cfg.action_repeats, npx = h->raster.width * h->raster.height;
     const uint8_t* cls = reinterpret_cast<const uint8_t*>(h->b.rtable + (size_t)C * npx);
     const size_t small = (size_t)cp::render_small_lds(C, R, npx).total;
-    if (small <= (size_t)cp::SMALL_LDS_MAX) {  // one block per env, dense ray tests
+    const int F = C * R;
+    // v2 of the small-frame kernel for the common frame counts (compile-time C * R)
+    auto small2 = [&](auto nf) -> bool {
+        constexpr int NF = decltype(nf)::value;
+        if (F != NF || h->render_v1) return false;
+        const size_t lds = (size_t)cp::render_small2_lds<NF>(C, R, npx).total;
+        if (lds > (size_t)cp::SMALL_LDS_MAX) return false;
+        hipLaunchKernelGGL(cp::cp_render_small2_kernel<NF>, dim3((unsigned)h->cfg.num_envs),
+                           dim3(cp::RENDER_WAVES * cp::WAVE_R), lds, st, h->raster, h->cfg.phys, R, list, count,
+                           h->b.rposes, h->b.rtable, cls, h->pixels);
+        return true;
+    };
+    if (small2(std::integral_constant<int, 3>{}) || small2(std::integral_constant<int, 2>{}) ||
+        small2(std::integral_constant<int, 1>{}) || small2(std::integral_constant<int, 4>{}) ||
+        small2(std::integral_constant<int, 6>{})) {
+        // launched
+    } else if (small <= (size_t)cp::SMALL_LDS_MAX) {  // one block per env, dense ray tests
         hipLaunchKernelGGL(cp::cp_render_small_kernel, dim3((unsigned)h->cfg.num_envs),
                            dim3(cp::RENDER_WAVES * cp::WAVE_R), small, st, h->raster, h->cfg.phys, R, list, count,
                            h->b.rposes, h->b.rtable, cls, h->pixels);

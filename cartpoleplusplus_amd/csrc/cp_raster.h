@@ -53,7 +53,11 @@ CP_DEV int to_u8(float x) {
     return (int)(x * 255.0f + 0.5f);
 }
 
-// conservative pixel rectangle of box (centre cc, axes A, half h) seen by camera k
+// conservative pixel rectangle of box (centre cc, axes A, half h) seen by camera k.  FAST: the
+// perspective divisions by the hardware reciprocal (v_rcp_f32, <= 1 ulp) instead of IEEE division:
+// the rectangle only decides which ray tests run (every pixel value comes from ray_box_o's exact
+// arithmetic, as the oracle's), and its +-1 pixel margin covers the ~1e-5 px an edge can move
+template <bool FAST = false>
 CP_DEV void box_rect(const Cam& k, V3 cc, const Axes& A, V3 h, float sxk, float syk, int W, int H, int16_t* out) {
     float x0 = 1e30f, x1 = -1e30f, y0 = 1e30f, y1 = -1e30f;
     bool behind = false, all_behind = true;
@@ -67,7 +71,14 @@ CP_DEV void box_rect(const Cam& k, V3 cc, const Axes& A, V3 h, float sxk, float 
         const float z = dot(v, k.f);
         behind = behind || z < 1e-3f;
         all_behind = all_behind && z < -1e-3f;
-        const float xs = dot(v, k.r) / (z * sxk), ys = dot(v, k.u) / (z * syk);
+        float xs, ys;
+        if constexpr (FAST) {
+            xs = dot(v, k.r) * __builtin_amdgcn_rcpf(z * sxk);
+            ys = dot(v, k.u) * __builtin_amdgcn_rcpf(z * syk);
+        } else {
+            xs = dot(v, k.r) / (z * sxk);
+            ys = dot(v, k.u) / (z * syk);
+        }
         const float px = (xs + 1.0f) * 0.5f * (float)W - 0.5f, py = (1.0f - ys) * 0.5f * (float)H - 0.5f;
         x0 = fminf(x0, px); x1 = fmaxf(x1, px); y0 = fminf(y0, py); y1 = fmaxf(y1, py);
     }
@@ -554,6 +565,229 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small_kernel(
             }
         }
 #endif
+        wave_sync();
+    }
+}
+
+// ---- small frames, v2 (round 4): the same images as cp_render_small_kernel, fewer instructions.
+// For NF = C * R frames known at compile time: the code buffer is pixel-major, [npx][CS] bytes
+// (CS = NF rounded up to 4), so the colour pass reads a pixel's codes with CS / 4 dword loads
+// instead of NF byte loads and the initialisation writes dwords; the pixel's 3 * NF float16 values
+// are assembled in registers and staged with dword writes (one 16-bit write at an odd start) instead
+// of 3 * NF 16-bit writes; the box rectangles use the hardware reciprocal (box_rect<true>).  The dense
+// ray tests, the colour LUT and the strip stores are cp_render_small_kernel's.
+struct Small2Lds {
+    int lut, best, code, stage, total;
+    RenderLds w;
+};
+// per wave: the strip's 512 values between two 24-value margins (a pixel's 3 * NF <= 24 values overhang a
+// strip edge by less than that; 16-byte multiples)
+template <int NF>
+__host__ __device__ constexpr int small2_stage_halves() { return 24 + WAVE_R * 8 + 24; }
+template <int NF>
+__host__ __device__ inline Small2Lds render_small2_lds(int C, int R, int npx) {
+    constexpr int CS = (NF + 3) & ~3;
+    Small2Lds s;
+    s.w = render_lds(C, R);
+    int o = s.w.face;
+    s.lut = o;   o = (o + R * 32 * 8 + 15) & ~15;
+    s.best = o;  o = (o + npx * 4 + 15) & ~15;
+    s.code = o;  o = (o + npx * CS + 15) & ~15;
+    s.stage = o; o = (o + RENDER_WAVES * small2_stage_halves<NF>() * 2 + 15) & ~15;
+    s.total = o;
+    return s;
+}
+
+template <int NF>
+__global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel(
+    cp_raster_config rc, cp_physics P, int R, const int32_t* list, const int32_t* count, const float* poses,
+    const float4* tabd, const uint8_t* cls, uint16_t* pixels) {
+    constexpr int CS = (NF + 3) & ~3, PP = 3 * NF, NT = RENDER_WAVES * WAVE_R;
+    extern __shared__ __align__(16) unsigned char render_lds_raw[];
+    if ((int)blockIdx.x >= *count) return;  // block-uniform
+    const int env = list[blockIdx.x];
+    const int tid = threadIdx.x, wave = tid / WAVE_R, lane = tid % WAVE_R;
+    const int W = rc.width, H = rc.height, C = rc.num_cameras, npx = W * H;
+    const Small2Lds L = render_small2_lds<NF>(C, R, npx);
+    unsigned char* base = render_lds_raw;
+    float* sax = reinterpret_cast<float*>(base + L.w.ax);
+    float* sc = reinterpret_cast<float*>(base + L.w.c);
+    float* soloc = reinterpret_cast<float*>(base + L.w.oloc);
+    int16_t* srect = reinterpret_cast<int16_t*>(base + L.w.rect);
+    uint2* slut = reinterpret_cast<uint2*>(base + L.lut);
+    float* sbest = reinterpret_cast<float*>(base + L.best);
+    uint8_t* scode = reinterpret_cast<uint8_t*>(base + L.code);
+    uint16_t* stage = reinterpret_cast<uint16_t*>(base + L.stage) + wave * small2_stage_halves<NF>();
+
+    const float* pe = poses + (size_t)env * R * CP_NUM_DYN * 7;
+    if (tid < R * CP_NUM_DYN) {
+        const float* q = pe + tid * 7;
+        const Axes A = quat_axes(q[3], q[4], q[5], q[6]);
+        float* a9 = sax + tid * 9;
+        a9[0] = A.a0.x; a9[1] = A.a0.y; a9[2] = A.a0.z;
+        a9[3] = A.a1.x; a9[4] = A.a1.y; a9[5] = A.a1.z;
+        a9[6] = A.a2.x; a9[7] = A.a2.y; a9[8] = A.a2.z;
+        sc[tid * 3 + 0] = q[0]; sc[tid * 3 + 1] = q[1]; sc[tid * 3 + 2] = q[2];
+    }
+    // every frame starts as the static ground / background: pixel p's byte f = (cam of f)'s class
+    for (int p = tid; p < npx; p += NT) {
+        uint32_t w[CS / 4];
+#pragma unroll
+        for (int q = 0; q < CS / 4; ++q) w[q] = 0u;
+        int cl = 0;
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+            if (f == 0 || f % R == 0) {  // a new camera (frames are (cam, r), r fastest)
+                cl = cls[(size_t)(f / R) * npx + p];
+                cl = cl < 6 ? cl : CODE_BG;
+            }
+            w[f / 4] |= (uint32_t)cl << (8 * (f % 4));
+        }
+#pragma unroll
+        for (int q = 0; q < CS / 4; ++q) reinterpret_cast<uint32_t*>(scode + (size_t)p * CS)[q] = w[q];
+    }
+    __syncthreads();
+    const float syk = rc.tan_half_fov;
+    const float sxk = rc.tan_half_fov * ((float)W / (float)H);
+    if (tid < NF * CP_NUM_DYN) {
+        const int cam = tid / (R * CP_NUM_DYN), rb = tid % (R * CP_NUM_DYN), b = rb % CP_NUM_DYN;
+        const Cam k = make_cam(rc, cam);
+        const float* a9 = sax + rb * 9;
+        Axes A;
+        A.a0 = mk(a9[0], a9[1], a9[2]); A.a1 = mk(a9[3], a9[4], a9[5]); A.a2 = mk(a9[6], a9[7], a9[8]);
+        const V3 c = mk(sc[rb * 3 + 0], sc[rb * 3 + 1], sc[rb * 3 + 2]);
+        const V3 oc = sub(k.eye, c);
+        soloc[tid * 3 + 0] = dot(oc, A.a0);
+        soloc[tid * 3 + 1] = dot(oc, A.a1);
+        soloc[tid * 3 + 2] = dot(oc, A.a2);
+        int16_t q[4];
+        box_rect<true>(k, c, A, mk(P.half_extents[b + 1][0], P.half_extents[b + 1][1], P.half_extents[b + 1][2]),
+                       sxk, syk, W, H, q);
+        srect[tid * 4 + 0] = q[0] < 0 ? 0 : q[0];
+        srect[tid * 4 + 1] = q[1] > W - 1 ? (int16_t)(W - 1) : q[1];
+        srect[tid * 4 + 2] = q[2] < 0 ? 0 : q[2];
+        srect[tid * 4 + 3] = q[3] > H - 1 ? (int16_t)(H - 1) : q[3];
+    }
+    const V3 light = mk(rc.light[0], rc.light[1], rc.light[2]);
+    for (int it = tid; it < R * 32; it += NT) {  // colour LUT [r][code] (cp_render_small_kernel's)
+        const int r = it / 32, code = it % 32;
+        uint16_t h[3];
+        if (code < CP_NUM_BODIES * 6) {
+            const int b = code / 6, fc = code % 6, ax = fc >> 1;
+            const float sg = (fc & 1) ? 1.0f : -1.0f;
+            V3 an;
+            if (b == 0) {
+                an = ax == 0 ? mk(1.0f, 0.0f, 0.0f) : (ax == 1 ? mk(0.0f, 1.0f, 0.0f) : mk(0.0f, 0.0f, 1.0f));
+            } else {
+                const float* a9 = sax + (r * CP_NUM_DYN + b - 1) * 9 + 3 * ax;
+                an = mk(a9[0], a9[1], a9[2]);
+            }
+            const float ndl = dot(scl(an, sg), light);
+            const float sh = fmaf_(rc.diffuse, ndl > 0.0f ? ndl : 0.0f, rc.ambient);
+            for (int ch = 0; ch < 3; ++ch) h[ch] = u8_to_half(to_u8(rc.color[b][ch] * sh));
+        } else {
+            for (int ch = 0; ch < 3; ++ch) h[ch] = u8_to_half(to_u8(rc.background[ch]));
+        }
+        slut[it] = make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2]);
+    }
+    __syncthreads();
+
+    // dense ray tests: frame by frame, body by body (cp_render_small_kernel's, pixel-major codes)
+#pragma unroll 1
+    for (int f = 0; f < NF; ++f) {
+        const int cam = f / R, r = f % R;
+        uint8_t* cf = scode + f;
+        for (int b = 1; b < CP_NUM_BODIES; ++b) {
+            const int item = f * CP_NUM_DYN + b - 1;
+            const int x0 = srect[item * 4 + 0], x1 = srect[item * 4 + 1];
+            const int y0 = srect[item * 4 + 2], y1 = srect[item * 4 + 3];
+            if (x0 > x1 || y0 > y1) continue;  // block-uniform
+            const int rw = x1 - x0 + 1, area = rw * (y1 - y0 + 1);
+            const float inv_rw = 1.0f / (float)rw;
+            const float* a9 = sax + (r * CP_NUM_DYN + b - 1) * 9;
+            Axes A;
+            A.a0 = mk(a9[0], a9[1], a9[2]); A.a1 = mk(a9[3], a9[4], a9[5]); A.a2 = mk(a9[6], a9[7], a9[8]);
+            const V3 h = mk(P.half_extents[b][0], P.half_extents[b][1], P.half_extents[b][2]);
+            const float* ol = soloc + item * 3;
+            for (int k = tid; k < area; k += NT) {
+                int yy = (int)((float)k * inv_rw), xx = k - yy * rw;  // k / rw, corrected
+                if (xx < 0) { --yy; xx += rw; }
+                if (xx >= rw) { ++yy; xx -= rw; }
+                const int p = (y0 + yy) * W + x0 + xx;
+                const float4 t0 = tabd[(size_t)cam * npx + p];
+                float t, sg;
+                int ax;
+                if (ray_box_o(mk(t0.x, t0.y, t0.z), ol, A, h, t, ax, sg)) {
+                    const int cur = cf[(size_t)p * CS];
+                    const float best = (cur < 6 || cur == CODE_BG) ? t0.w : sbest[p];
+                    if (t < best) {
+                        sbest[p] = t;
+                        cf[(size_t)p * CS] = (uint8_t)(b * 6 + ax * 2 + (sg > 0.0f ? 1 : 0));
+                    }
+                }
+            }
+            __syncthreads();  // the next body compares against this one's hits
+        }
+    }
+
+    // colours, in strips of 64 output chunks: chunk q is the 16 bytes at out + 16 q - (out mod 16), so
+    // every strip is 16-byte aligned and each lane stores one whole chunk; the pixels overlapping the
+    // strip's 512 values (<= 59) are computed one per lane (a pixel cut by a strip edge is computed by
+    // both strips), their 3 * NF values assembled in registers and staged with dword writes at their
+    // position relative to the strip; only the env's first and last chunks are written by halves
+    uint16_t* out = pixels + (size_t)env * npx * PP;
+    const int N = npx * PP;                                             // the env's values
+    const int sh = (int)((reinterpret_cast<uintptr_t>(out) & 15) >> 1);  // values before out in its chunk
+    const int Q = (N + sh + 7) >> 3;                                     // chunks touched
+    constexpr int M = 24;                                                // stage margin (>= PP, 16-byte multiple)
+    static_assert(PP <= M, "small2_stage_halves: the margins must hold a pixel's values");
+    uint4* d4 = reinterpret_cast<uint4*>(out - sh);
+    for (int s0 = wave * WAVE_R; s0 < Q; s0 += RENDER_WAVES * WAVE_R) {
+        const int g0 = s0 * 8 - sh;                                     // the strip's first value (env-relative)
+        const int glo = g0 > 0 ? g0 : 0;
+        const int ghi = (g0 + WAVE_R * 8 < N ? g0 + WAVE_R * 8 : N) - 1;
+        const int plo = glo / PP, np = ghi / PP - plo + 1;              // pixels overlapping the strip
+        for (int i = lane; i < np; i += WAVE_R) {                       // one pass for 3 * NF >= 9
+            const int p = plo + i;
+            uint32_t cw[CS / 4];
+#pragma unroll
+            for (int q = 0; q < CS / 4; ++q) cw[q] = reinterpret_cast<const uint32_t*>(scode + (size_t)p * CS)[q];
+            uint16_t hv[PP];
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const int code = (int)((cw[f / 4] >> (8 * (f % 4))) & 0xFFu);
+                const uint2 c = slut[(f % R) * 32 + code];
+                hv[f] = (uint16_t)c.x;
+                hv[NF + f] = (uint16_t)(c.x >> 16);
+                hv[2 * NF + f] = (uint16_t)c.y;
+            }
+            const int o = M + p * PP - g0;                              // in (M - PP, M + 512)
+            if (o & 1) {  // a leading half, then dword pairs (the stage is 16-byte aligned)
+                stage[o] = hv[0];
+                uint32_t* s32 = reinterpret_cast<uint32_t*>(stage + o + 1);
+#pragma unroll
+                for (int j = 0; j < (PP - 1) / 2; ++j)
+                    s32[j] = (uint32_t)hv[1 + 2 * j] | ((uint32_t)hv[2 + 2 * j] << 16);
+                if ((PP - 1) & 1) stage[o + PP - 1] = hv[PP - 1];
+            } else {
+                uint32_t* s32 = reinterpret_cast<uint32_t*>(stage + o);
+#pragma unroll
+                for (int j = 0; j < PP / 2; ++j) s32[j] = (uint32_t)hv[2 * j] | ((uint32_t)hv[2 * j + 1] << 16);
+                if (PP & 1) stage[o + PP - 1] = hv[PP - 1];
+            }
+        }
+        wave_sync();
+        const int q = s0 + lane;
+        const int e0 = q * 8 - sh;                                      // the chunk's first value
+        if (q < Q) {
+            const uint16_t* src = stage + M + lane * 8;
+            if (e0 >= 0 && e0 + 8 <= N) {
+                store_stream(&d4[q], *reinterpret_cast<const uint4*>(src));
+            } else {  // the env's first / last chunk: its values only (the neighbour env owns the rest)
+                for (int e = 0; e < 8; ++e)
+                    if (e0 + e >= 0 && e0 + e < N) out[e0 + e] = src[e];
+            }
+        }
         wave_sync();
     }
 }

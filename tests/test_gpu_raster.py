@@ -148,3 +148,25 @@ def test_full_size_c5_properties_and_subset(oracle_mod):
     st = env.get_state().cpu().numpy()[:, idx]
     for k in range(len(idx)):
         _check_env(oracle_mod, env, pix, st, k, 2)
+
+
+@pytest.mark.parametrize("R,C,W,H", [(3, 1, 50, 50), (2, 1, 50, 50), (1, 1, 37, 23), (2, 2, 50, 50), (3, 2, 37, 23)])
+def test_render_v2_equals_v1_every_pixel(monkeypatch, R, C, W, H):
+    """cp_render_small2_kernel<C*R> (round 4: pixel-major codes, packed stage writes, reciprocal
+    rectangles) against the round-3 small-frame kernel (CP_RENDER_V1=1 at cp_create): every pixel of
+    every env, frame and step equal, bit for bit (both are held to the oracle by the tests above)."""
+    B, T = 64, 12
+    out = []
+    for v1 in ("1", "0"):
+        monkeypatch.setenv("CP_RENDER_V1", v1)
+        env = BatchedCartpole(B, 0, action_repeats=R, initial_force=55.0, seed=21)
+        env.enable_raster(True, num_cameras=C, width=W, height=H)
+        env.reset()
+        frames = [env.pixels.clone()]
+        g = torch.Generator(device="cuda").manual_seed(4)
+        for _ in range(T):
+            env.step(torch.rand((B, 2, 2), device="cuda", generator=g) * 2 - 1)
+            frames.append(env.pixels.clone())
+        out.append(torch.stack(frames).view(torch.int16))
+        env.close()
+    assert torch.equal(out[0], out[1])
