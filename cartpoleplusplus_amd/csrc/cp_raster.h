@@ -379,6 +379,7 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_kernel(
 // pass maps codes to colours through a per-repeat LUT and streams strips of 64
 // pixels out as cp_render_kernel does.
 constexpr int CODE_BG = 30;  // background; codes 0..29 = body * 6 + face (body 0 = ground)
+constexpr int CODE_NONE = 0xFF;  // cp_render_small2_kernel: no dynamic body seen yet (ground / background)
 struct SmallLds {
     int lut, best, code, stage, total;
     RenderLds w;  // the scene part (its own face / stage fields unused)
@@ -591,9 +592,12 @@ __host__ __device__ inline Small2Lds render_small2_lds(int C, int R, int npx) {
     s.w = render_lds(C, R);
     int o = s.w.face;
     s.lut = o;   o = (o + R * 32 * 8 + 15) & ~15;
-    s.best = o;  o = (o + npx * 4 + 15) & ~15;
+    // the dense pass's depth buffer and, after it, the colour pass's stages (two strips per wave) share
+    // one region: they are never live together
+    const int stage_bytes = RENDER_WAVES * 2 * small2_stage_halves<NF>() * 2;
+    s.best = o;
+    s.stage = o; o = (o + (npx * 4 > stage_bytes ? npx * 4 : stage_bytes) + 15) & ~15;
     s.code = o;  o = (o + npx * CS + 15) & ~15;
-    s.stage = o; o = (o + RENDER_WAVES * small2_stage_halves<NF>() * 2 + 15) & ~15;
     s.total = o;
     return s;
 }
@@ -606,6 +610,9 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
     extern __shared__ __align__(16) unsigned char render_lds_raw[];
     if ((int)blockIdx.x >= *count) return;  // block-uniform
     const int env = list[blockIdx.x];
+#if defined(CP_RV_STOP) && CP_RV_STOP == 0  // diagnostic: the launch alone
+    if (env >= 0) return;
+#endif
     const int tid = threadIdx.x, wave = tid / WAVE_R, lane = tid % WAVE_R;
     const int W = rc.width, H = rc.height, C = rc.num_cameras, npx = W * H;
     const Small2Lds L = render_small2_lds<NF>(C, R, npx);
@@ -617,7 +624,7 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
     uint2* slut = reinterpret_cast<uint2*>(base + L.lut);
     float* sbest = reinterpret_cast<float*>(base + L.best);
     uint8_t* scode = reinterpret_cast<uint8_t*>(base + L.code);
-    uint16_t* stage = reinterpret_cast<uint16_t*>(base + L.stage) + wave * small2_stage_halves<NF>();
+    uint16_t* stage = reinterpret_cast<uint16_t*>(base + L.stage) + wave * 2 * small2_stage_halves<NF>();
 
     const float* pe = poses + (size_t)env * R * CP_NUM_DYN * 7;
     if (tid < R * CP_NUM_DYN) {
@@ -629,22 +636,13 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
         a9[6] = A.a2.x; a9[7] = A.a2.y; a9[8] = A.a2.z;
         sc[tid * 3 + 0] = q[0]; sc[tid * 3 + 1] = q[1]; sc[tid * 3 + 2] = q[2];
     }
-    // every frame starts as the static ground / background: pixel p's byte f = (cam of f)'s class
-    for (int p = tid; p < npx; p += NT) {
-        uint32_t w[CS / 4];
-#pragma unroll
-        for (int q = 0; q < CS / 4; ++q) w[q] = 0u;
-        int cl = 0;
-#pragma unroll
-        for (int f = 0; f < NF; ++f) {
-            if (f == 0 || f % R == 0) {  // a new camera (frames are (cam, r), r fastest)
-                cl = cls[(size_t)(f / R) * npx + p];
-                cl = cl < 6 ? cl : CODE_BG;
-            }
-            w[f / 4] |= (uint32_t)cl << (8 * (f % 4));
-        }
-#pragma unroll
-        for (int q = 0; q < CS / 4; ++q) reinterpret_cast<uint32_t*>(scode + (size_t)p * CS)[q] = w[q];
+    // every frame starts as "no body hit" (CODE_NONE): the dense pass compares such a pixel against the
+    // ground's t from the table and the colour pass shows its static class (cls, L1-resident): a memset
+    // instead of copying the class table into every block
+    {
+        uint4* c16 = reinterpret_cast<uint4*>(scode);
+        const int n16 = (npx * CS + 15) >> 4;
+        for (int k = tid; k < n16; k += NT) c16[k] = make_uint4(~0u, ~0u, ~0u, ~0u);
     }
     __syncthreads();
     const float syk = rc.tan_half_fov;
@@ -691,8 +689,12 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
         slut[it] = make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2]);
     }
     __syncthreads();
+#if defined(CP_RV_STOP) && CP_RV_STOP == 1  // diagnostic: the launch + the scene setup
+    if (env >= 0) return;
+#endif
 
     // dense ray tests: frame by frame, body by body (cp_render_small_kernel's, pixel-major codes)
+#ifndef CP_RV_NO_DENSE
 #pragma unroll 1
     for (int f = 0; f < NF; ++f) {
         const int cam = f / R, r = f % R;
@@ -719,7 +721,7 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
                 int ax;
                 if (ray_box_o(mk(t0.x, t0.y, t0.z), ol, A, h, t, ax, sg)) {
                     const int cur = cf[(size_t)p * CS];
-                    const float best = (cur < 6 || cur == CODE_BG) ? t0.w : sbest[p];
+                    const float best = cur == CODE_NONE ? t0.w : sbest[p];
                     if (t < best) {
                         sbest[p] = t;
                         cf[(size_t)p * CS] = (uint8_t)(b * 6 + ax * 2 + (sg > 0.0f ? 1 : 0));
@@ -729,6 +731,7 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
             __syncthreads();  // the next body compares against this one's hits
         }
     }
+#endif
 
     // colours, in strips of 64 output chunks: chunk q is the 16 bytes at out + 16 q - (out mod 16), so
     // every strip is 16-byte aligned and each lane stores one whole chunk; the pixels overlapping the
@@ -742,50 +745,74 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
     constexpr int M = 24;                                                // stage margin (>= PP, 16-byte multiple)
     static_assert(PP <= M, "small2_stage_halves: the margins must hold a pixel's values");
     uint4* d4 = reinterpret_cast<uint4*>(out - sh);
-    for (int s0 = wave * WAVE_R; s0 < Q; s0 += RENDER_WAVES * WAVE_R) {
-        const int g0 = s0 * 8 - sh;                                     // the strip's first value (env-relative)
-        const int glo = g0 > 0 ? g0 : 0;
-        const int ghi = (g0 + WAVE_R * 8 < N ? g0 + WAVE_R * 8 : N) - 1;
-        const int plo = glo / PP, np = ghi / PP - plo + 1;              // pixels overlapping the strip
-        for (int i = lane; i < np; i += WAVE_R) {                       // one pass for 3 * NF >= 9
-            const int p = plo + i;
-            uint32_t cw[CS / 4];
+#ifdef CP_RV_NO_OUTPUT
+    if (Q > 0) return;
+#endif
+    constexpr int SH = small2_stage_halves<NF>();
+    // two strips per trip (stage u = 0, 1): two independent load / LUT / stage chains between syncs;
+    // wave w takes strips w, w + 4, w + 8, ... (in units of 64 chunks)
+    for (int s0 = wave * WAVE_R; s0 < Q; s0 += 2 * RENDER_WAVES * WAVE_R) {
 #pragma unroll
-            for (int q = 0; q < CS / 4; ++q) cw[q] = reinterpret_cast<const uint32_t*>(scode + (size_t)p * CS)[q];
-            uint16_t hv[PP];
+        for (int u = 0; u < 2; ++u) {
+            const int sa = s0 + u * RENDER_WAVES * WAVE_R;
+            if (sa >= Q) break;  // wave-uniform
+            uint16_t* st = stage + u * SH;
+            const int g0 = sa * 8 - sh;                                 // the strip's first value (env-relative)
+            const int glo = g0 > 0 ? g0 : 0;
+            const int ghi = (g0 + WAVE_R * 8 < N ? g0 + WAVE_R * 8 : N) - 1;
+            const int plo = glo / PP, np = ghi / PP - plo + 1;          // pixels overlapping the strip
+            for (int i = lane; i < np; i += WAVE_R) {                   // one pass for 3 * NF >= 9
+                const int p = plo + i;
+                uint32_t cw[CS / 4];
 #pragma unroll
-            for (int f = 0; f < NF; ++f) {
-                const int code = (int)((cw[f / 4] >> (8 * (f % 4))) & 0xFFu);
-                const uint2 c = slut[(f % R) * 32 + code];
-                hv[f] = (uint16_t)c.x;
-                hv[NF + f] = (uint16_t)(c.x >> 16);
-                hv[2 * NF + f] = (uint16_t)c.y;
-            }
-            const int o = M + p * PP - g0;                              // in (M - PP, M + 512)
-            if (o & 1) {  // a leading half, then dword pairs (the stage is 16-byte aligned)
-                stage[o] = hv[0];
-                uint32_t* s32 = reinterpret_cast<uint32_t*>(stage + o + 1);
+                for (int q = 0; q < CS / 4; ++q) cw[q] = reinterpret_cast<const uint32_t*>(scode + (size_t)p * CS)[q];
+                // the pixel's static class per camera (ground face or background), shown where no body is
+                int cl0 = cls[p], cl1 = C > 1 ? cls[(size_t)npx + p] : cl0;
+                cl0 = cl0 < 6 ? cl0 : CODE_BG;
+                cl1 = cl1 < 6 ? cl1 : CODE_BG;
+                uint16_t hv[PP];
 #pragma unroll
-                for (int j = 0; j < (PP - 1) / 2; ++j)
-                    s32[j] = (uint32_t)hv[1 + 2 * j] | ((uint32_t)hv[2 + 2 * j] << 16);
-                if ((PP - 1) & 1) stage[o + PP - 1] = hv[PP - 1];
-            } else {
-                uint32_t* s32 = reinterpret_cast<uint32_t*>(stage + o);
+                for (int f = 0; f < NF; ++f) {
+                    int code = (int)((cw[f / 4] >> (8 * (f % 4))) & 0xFFu);
+                    if (code == CODE_NONE) code = f < R ? cl0 : cl1;
+                    const uint2 c = slut[(f % R) * 32 + code];
+                    hv[f] = (uint16_t)c.x;
+                    hv[NF + f] = (uint16_t)(c.x >> 16);
+                    hv[2 * NF + f] = (uint16_t)c.y;
+                }
+                const int o = M + p * PP - g0;                          // in (M - PP, M + 512)
+                if (o & 1) {  // a leading half, then dword pairs (the stage is 16-byte aligned)
+                    st[o] = hv[0];
+                    uint32_t* s32 = reinterpret_cast<uint32_t*>(st + o + 1);
 #pragma unroll
-                for (int j = 0; j < PP / 2; ++j) s32[j] = (uint32_t)hv[2 * j] | ((uint32_t)hv[2 * j + 1] << 16);
-                if (PP & 1) stage[o + PP - 1] = hv[PP - 1];
+                    for (int j = 0; j < (PP - 1) / 2; ++j)
+                        s32[j] = (uint32_t)hv[1 + 2 * j] | ((uint32_t)hv[2 + 2 * j] << 16);
+                    if ((PP - 1) & 1) st[o + PP - 1] = hv[PP - 1];
+                } else {
+                    uint32_t* s32 = reinterpret_cast<uint32_t*>(st + o);
+#pragma unroll
+                    for (int j = 0; j < PP / 2; ++j) s32[j] = (uint32_t)hv[2 * j] | ((uint32_t)hv[2 * j + 1] << 16);
+                    if (PP & 1) st[o + PP - 1] = hv[PP - 1];
+                }
             }
         }
         wave_sync();
-        const int q = s0 + lane;
-        const int e0 = q * 8 - sh;                                      // the chunk's first value
-        if (q < Q) {
-            const uint16_t* src = stage + M + lane * 8;
-            if (e0 >= 0 && e0 + 8 <= N) {
-                store_stream(&d4[q], *reinterpret_cast<const uint4*>(src));
-            } else {  // the env's first / last chunk: its values only (the neighbour env owns the rest)
-                for (int e = 0; e < 8; ++e)
-                    if (e0 + e >= 0 && e0 + e < N) out[e0 + e] = src[e];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int q = s0 + u * RENDER_WAVES * WAVE_R + lane;
+            const int e0 = q * 8 - sh;                                  // the chunk's first value
+#ifdef CP_RV_NO_STORE
+            if (q < 0) {
+#else
+            if (q < Q) {
+#endif
+                const uint16_t* src = stage + u * SH + M + lane * 8;
+                if (e0 >= 0 && e0 + 8 <= N) {
+                    store_stream(&d4[q], *reinterpret_cast<const uint4*>(src));
+                } else {  // the env's first / last chunk: its values only (the neighbour env owns the rest)
+                    for (int e = 0; e < 8; ++e)
+                        if (e0 + e >= 0 && e0 + e < N) out[e0 + e] = src[e];
+                }
             }
         }
         wave_sync();
