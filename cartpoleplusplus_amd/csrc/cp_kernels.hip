@@ -442,20 +442,23 @@ static int launch_render(cp_handle* h, const int32_t* list, const int32_t* count
     const uint8_t* cls = reinterpret_cast<const uint8_t*>(h->b.rtable + (size_t)C * npx);
     const size_t small = (size_t)cp::render_small_lds(C, R, npx).total;
     const int F = C * R;
-    // v2 of the small-frame kernel for the common frame counts (compile-time C * R)
-    auto small2 = [&](auto nf) -> bool {
-        constexpr int NF = decltype(nf)::value;
-        if (F != NF || h->render_v1) return false;
-        const size_t lds = (size_t)cp::render_small2_lds<NF>(C, R, npx).total;
+    // v2 of the small-frame kernel for the common (cameras, repeats) pairs, both compile-time
+    auto small2 = [&](auto cc, auto rr) -> bool {
+        constexpr int CC = decltype(cc)::value, RR = decltype(rr)::value;
+        if (C != CC || R != RR || h->render_v1) return false;
+        const size_t lds = (size_t)cp::render_small2_lds<CC * RR>(C, R, npx).total;
         if (lds > (size_t)cp::SMALL_LDS_MAX) return false;
-        hipLaunchKernelGGL(cp::cp_render_small2_kernel<NF>, dim3((unsigned)h->cfg.num_envs),
-                           dim3(cp::RENDER_WAVES * cp::WAVE_R), lds, st, h->raster, h->cfg.phys, R, list, count,
+        hipLaunchKernelGGL((cp::cp_render_small2_kernel<CC, RR>), dim3((unsigned)h->cfg.num_envs),
+                           dim3(cp::RENDER_WAVES * cp::WAVE_R), lds, st, h->raster, h->cfg.phys, list, count,
                            h->b.rposes, h->b.rtable, cls, h->pixels);
         return true;
     };
-    if (small2(std::integral_constant<int, 3>{}) || small2(std::integral_constant<int, 2>{}) ||
-        small2(std::integral_constant<int, 1>{}) || small2(std::integral_constant<int, 4>{}) ||
-        small2(std::integral_constant<int, 6>{})) {
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using I4 = std::integral_constant<int, 4>;
+    if (small2(I1{}, I3{}) || small2(I1{}, I2{}) || small2(I1{}, I1{}) || small2(I1{}, I4{}) ||
+        small2(std::integral_constant<int, 1>{}, std::integral_constant<int, 6>{}) || small2(I2{}, I1{}) || small2(I2{}, I2{}) || small2(I2{}, I3{})) {
         // launched
     } else if (small <= (size_t)cp::SMALL_LDS_MAX) {  // one block per env, dense ray tests
         hipLaunchKernelGGL(cp::cp_render_small_kernel, dim3((unsigned)h->cfg.num_envs),

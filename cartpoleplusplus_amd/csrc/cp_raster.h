@@ -602,10 +602,11 @@ __host__ __device__ inline Small2Lds render_small2_lds(int C, int R, int npx) {
     return s;
 }
 
-template <int NF>
+template <int CC, int RR>
 __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel(
-    cp_raster_config rc, cp_physics P, int R, const int32_t* list, const int32_t* count, const float* poses,
+    cp_raster_config rc, cp_physics P, const int32_t* list, const int32_t* count, const float* poses,
     const float4* tabd, const uint8_t* cls, uint16_t* pixels) {
+    constexpr int R = RR, NF = CC * RR;  // cameras and repeats at compile time (the launcher checks them)
     constexpr int CS = (NF + 3) & ~3, PP = 3 * NF, NT = RENDER_WAVES * WAVE_R;
     extern __shared__ __align__(16) unsigned char render_lds_raw[];
     if ((int)blockIdx.x >= *count) return;  // block-uniform
@@ -614,7 +615,8 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
     if (env >= 0) return;
 #endif
     const int tid = threadIdx.x, wave = tid / WAVE_R, lane = tid % WAVE_R;
-    const int W = rc.width, H = rc.height, C = rc.num_cameras, npx = W * H;
+    constexpr int C = CC;
+    const int W = rc.width, H = rc.height, npx = W * H;
     const Small2Lds L = render_small2_lds<NF>(C, R, npx);
     unsigned char* base = render_lds_raw;
     float* sax = reinterpret_cast<float*>(base + L.w.ax);
@@ -781,18 +783,28 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
                     hv[2 * NF + f] = (uint16_t)c.y;
                 }
                 const int o = M + p * PP - g0;                          // in (M - PP, M + 512)
-                if (o & 1) {  // a leading half, then dword pairs (the stage is 16-byte aligned)
-                    st[o] = hv[0];
-                    uint32_t* s32 = reinterpret_cast<uint32_t*>(st + o + 1);
+                // the PP values at st[o ..): without a branch on the parity a = o & 1 (PP is odd when
+                // NF is, so neighbouring lanes differ): the full dwords hold values (2k + a, 2k + 1 + a)
+                // at dword (o + a) / 2 + k; what is left over is one value (odd PP: the last one if a = 0,
+                // the first if a = 1) or, for even PP and a = 1, the first and the last
+                const int a = o & 1;
+                uint32_t* s32 = reinterpret_cast<uint32_t*>(st) + ((o + a) >> 1);
+                constexpr int NFULL = (PP - 1) / 2;
 #pragma unroll
-                    for (int j = 0; j < (PP - 1) / 2; ++j)
-                        s32[j] = (uint32_t)hv[1 + 2 * j] | ((uint32_t)hv[2 + 2 * j] << 16);
-                    if ((PP - 1) & 1) st[o + PP - 1] = hv[PP - 1];
-                } else {
-                    uint32_t* s32 = reinterpret_cast<uint32_t*>(st + o);
-#pragma unroll
-                    for (int j = 0; j < PP / 2; ++j) s32[j] = (uint32_t)hv[2 * j] | ((uint32_t)hv[2 * j + 1] << 16);
-                    if (PP & 1) st[o + PP - 1] = hv[PP - 1];
+                for (int k = 0; k < NFULL; ++k) {
+                    const uint32_t e = (uint32_t)hv[2 * k] | ((uint32_t)hv[2 * k + 1] << 16);
+                    const uint32_t d = (uint32_t)hv[2 * k + 1] | ((uint32_t)hv[2 * k + 2] << 16);
+                    s32[k] = a ? d : e;
+                }
+                if constexpr (PP & 1) {
+                    st[a ? o : o + PP - 1] = a ? hv[0] : hv[PP - 1];
+                } else {  // even PP: a = 0 leaves one more full pair, a = 1 the first and the last value
+                    if (a) {
+                        st[o] = hv[0];
+                        st[o + PP - 1] = hv[PP - 1];
+                    } else {
+                        s32[NFULL] = (uint32_t)hv[PP - 2] | ((uint32_t)hv[PP - 1] << 16);
+                    }
                 }
             }
         }
