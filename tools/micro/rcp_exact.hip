@@ -1,0 +1,74 @@
+// rcp_exact.hip -- is a hardware reciprocal plus one FMA Newton step the correctly rounded 1 / x?
+// The dense ray tests (cp_raster.h ray_box_o) take 1.0f / d three times per pixel and body; the IEEE
+// division sequence is ~10 VALU.  This checks, for every float32 x (both signs, every exponent, every
+// mantissa: 2^32 values), the short form
+//     y = v_rcp_f32(x);  e = fma(-x, y, 1);  r = fma(e, y, y)
+// against the compiler's correctly rounded 1.0f / x, bit for bit, and prints the mismatches per
+// biased exponent.  A shortcut is usable for the exponents with zero mismatches (and both sides
+// finite), with the IEEE division kept for the rest.
+// build: hipcc -O3 --offload-arch=gfx950 -std=c++17 rcp_exact.hip -o rcp_exact
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x)                                                                    \
+    do {                                                                         \
+        hipError_t e_ = (x);                                                     \
+        if (e_ != hipSuccess) {                                                  \
+            std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));         \
+            std::exit(1);                                                        \
+        }                                                                        \
+    } while (0)
+
+__global__ void __launch_bounds__(256) check(unsigned long long* bad, unsigned int* first) {
+    // grid.x covers the 2^23 mantissas (x 2 signs via grid.y's low bit), grid.y >> 1 is the exponent
+    const unsigned m = blockIdx.x * 256u + threadIdx.x;
+    const unsigned ex = blockIdx.y >> 1, sg = blockIdx.y & 1u;
+    const unsigned bits = (sg << 31) | (ex << 23) | m;
+    const float x = __uint_as_float(bits);
+    volatile float one = 1.0f;
+    const float ref = one / x;
+    const float y = __builtin_amdgcn_rcpf(x);
+    const float e = __builtin_fmaf(-x, y, 1.0f);
+    const float r = __builtin_fmaf(e, y, y);
+    const bool same = __float_as_uint(r) == __float_as_uint(ref);
+    const unsigned long long n = __ballot(!same);
+    if (n && (threadIdx.x & 63u) == 0) {
+        atomicAdd(bad + ex, (unsigned long long)__popcll(n));
+        atomicMin(first + ex, bits);
+    }
+}
+
+int main() {
+    unsigned long long* bad;
+    unsigned int* first;
+    CK(hipMalloc(&bad, 256 * 8));
+    CK(hipMalloc(&first, 256 * 4));
+    CK(hipMemset(bad, 0, 256 * 8));
+    CK(hipMemset(first, 0xFF, 256 * 4));
+    hipLaunchKernelGGL(check, dim3((1u << 23) / 256, 512), dim3(256), 0, 0, bad, first);
+    CK(hipDeviceSynchronize());
+    unsigned long long hb[256];
+    unsigned int hf[256];
+    CK(hipMemcpy(hb, bad, sizeof hb, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hf, first, sizeof hf, hipMemcpyDeviceToHost));
+    int lo = -1, hi = -1;
+    unsigned long long total = 0;
+    for (int e = 0; e < 256; ++e) {
+        total += hb[e];
+        if (hb[e] == 0) {
+            if (lo < 0 || (hi >= 0 && hi != e - 1)) lo = (lo < 0 ? e : lo);
+            if (hi == e - 1 || hi < 0) hi = e;
+        }
+    }
+    std::printf("{\"total_mismatches\": %llu, \"per_exponent\": {", total);
+    bool c = false;
+    for (int e = 0; e < 256; ++e)
+        if (hb[e]) {
+            std::printf("%s\"%d\": [%llu, \"0x%08x\"]", c ? ", " : "", e, hb[e], hf[e]);
+            c = true;
+        }
+    std::printf("}}\n");
+    return 0;
+}
