@@ -99,6 +99,24 @@ CP_DEV void box_rect(const Cam& k, V3 cc, const Axes& A, V3 h, float sxk, float 
     out[3] = (int16_t)fminf(lim, ceilf(y1) + 1.0f);
 }
 
+// 1.0f / x, correctly rounded.  CP_RCP_SHORT: the hardware reciprocal and one FMA Newton step, which
+// is the correctly rounded result for every x whose biased exponent lies in [RCP_EXP_LO, RCP_EXP_HI]
+// (checked for all 2^32 floats on gfx950, tools/micro/rcp_exact.hip); other x (zero, denormal, huge,
+// inf, NaN) take the IEEE division.  3 VALU instead of ~10 in the common case.
+#ifdef CP_RCP_SHORT
+constexpr unsigned RCP_EXP_LO = CP_RCP_EXP_LO, RCP_EXP_HI = CP_RCP_EXP_HI;
+#endif
+CP_DEV float rcp_rn(float x) {
+#ifdef CP_RCP_SHORT
+    const unsigned ex = (__float_as_uint(x) >> 23) & 0xFFu;
+    if (ex - RCP_EXP_LO <= RCP_EXP_HI - RCP_EXP_LO) {
+        const float y = __builtin_amdgcn_rcpf(x);
+        return __builtin_fmaf(__builtin_fmaf(-x, y, 1.0f), y, y);
+    }
+#endif
+    return 1.0f / x;
+}
+
 // Ray (eye + t d) against a box with axes A and half extents h, given the origin-side
 // dot products o_i = (eye - c) . a_i (oracle: ray_box computes them per ray; the same
 // values): slab test, entry t, its axis and the face sign.  Returns false on a miss.
@@ -109,7 +127,7 @@ CP_DEV bool ray_box_o(V3 d, const float o[3], const Axes& A, V3 h, float& t, int
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         dd[i] = dot(d, ax[i]);
-        const float inv = 1.0f / dd[i];
+        const float inv = rcp_rn(dd[i]);
         const float t1 = (-hh[i] - o[i]) * inv, t2 = (hh[i] - o[i]) * inv;
         const bool lt = t1 < t2;
         lo[i] = lt ? t1 : t2;
@@ -751,6 +769,73 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
     if (Q > 0) return;
 #endif
     constexpr int SH = small2_stage_halves<NF>();
+#ifdef CP_RV_PAIRS
+    // pixel pairs: strips of 128 output chunks (1,024 values, the wave's two stages as one), each lane
+    // computes two consecutive pixels (<= 58 pairs overlap a strip at 3 * NF >= 9), so a lane's 2 * 3 * NF values start
+    // at the same parity in every lane of the strip: dword writes without per-lane selects
+    constexpr int MP = (2 * PP + 7) / 8 * 8;                             // margin: a pair's values, 16-byte multiple
+    static_assert(2 * MP + 16 * WAVE_R <= 2 * SH, "small2_stage_halves: a 128-chunk strip and its margins");
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    for (int sa = wv * 2 * WAVE_R; sa < Q; sa += 2 * RENDER_WAVES * WAVE_R) {  // wave-uniform
+        const int g0 = sa * 8 - sh;                                      // the strip's first value
+        const int glo = g0 > 0 ? g0 : 0;
+        const int ghi = (g0 + 16 * WAVE_R < N ? g0 + 16 * WAVE_R : N) - 1;
+        const int plo = glo / PP, phi = ghi / PP;                       // pixels overlapping the strip
+        const int a = (MP + plo * PP - g0) & 1;                          // the parity of every pair's start
+        for (int j = lane; 2 * j <= phi - plo; j += WAVE_R) {             // one pass for 3 * NF >= 9
+            const int p = plo + 2 * j;
+            const int pn = p + 1 < npx ? p + 1 : p;                     // past the env's last pixel: a copy
+            uint16_t hv[2 * PP];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int pp = k ? pn : p;
+                uint32_t cw[CS / 4];
+#pragma unroll
+                for (int q = 0; q < CS / 4; ++q) cw[q] = reinterpret_cast<const uint32_t*>(scode + (size_t)pp * CS)[q];
+                int cl0 = cls[pp], cl1 = C > 1 ? cls[(size_t)npx + pp] : cl0;
+                cl0 = cl0 < 6 ? cl0 : CODE_BG;
+                cl1 = cl1 < 6 ? cl1 : CODE_BG;
+#pragma unroll
+                for (int f = 0; f < NF; ++f) {
+                    int code = (int)((cw[f / 4] >> (8 * (f % 4))) & 0xFFu);
+                    if (code == CODE_NONE) code = f < R ? cl0 : cl1;
+                    const uint2 c = slut[(f % R) * 32 + code];
+                    hv[k * PP + f] = (uint16_t)c.x;
+                    hv[k * PP + NF + f] = (uint16_t)(c.x >> 16);
+                    hv[k * PP + 2 * NF + f] = (uint16_t)c.y;
+                }
+            }
+            const int o = MP + p * PP - g0;                              // in [MP - PP, MP + 1024)
+            uint32_t* s32 = reinterpret_cast<uint32_t*>(stage) + ((o + a) >> 1);
+            if (a == 0) {
+#pragma unroll
+                for (int k = 0; k < PP; ++k) s32[k] = (uint32_t)hv[2 * k] | ((uint32_t)hv[2 * k + 1] << 16);
+            } else {
+                stage[o] = hv[0];
+#pragma unroll
+                for (int k = 0; k < PP - 1; ++k) s32[k] = (uint32_t)hv[2 * k + 1] | ((uint32_t)hv[2 * k + 2] << 16);
+                stage[o + 2 * PP - 1] = hv[2 * PP - 1];
+            }
+        }
+        wave_sync();
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int q = sa + u * WAVE_R + lane;
+            const int e0 = q * 8 - sh;                                   // the chunk's first value
+            if (q < Q) {
+                const uint16_t* src = stage + MP + (u * WAVE_R + lane) * 8;
+                if (e0 >= 0 && e0 + 8 <= N) {
+                    store_stream(&d4[q], *reinterpret_cast<const uint4*>(src));
+                } else {  // the env's first / last chunk: its values only (the neighbour env owns the rest)
+                    for (int e = 0; e < 8; ++e)
+                        if (e0 + e >= 0 && e0 + e < N) out[e0 + e] = src[e];
+                }
+            }
+        }
+        wave_sync();
+    }
+    if (Q >= 0) return;
+#endif
     // two strips per trip (stage u = 0, 1): two independent load / LUT / stage chains between syncs;
     // wave w takes strips w, w + 4, w + 8, ... (in units of 64 chunks)
     for (int s0 = wave * WAVE_R; s0 < Q; s0 += 2 * RENDER_WAVES * WAVE_R) {

@@ -6,6 +6,8 @@
 // against the compiler's correctly rounded 1.0f / x, bit for bit, and prints the mismatches per
 // biased exponent.  A shortcut is usable for the exponents with zero mismatches (and both sides
 // finite), with the IEEE division kept for the rest.
+// Result on gfx950 (profiles/rd4e_rcp_exact.json): mismatches only at biased exponents 0 (zero and
+// denormal x), 253-254 (1 / x denormal or flushed) and 255 (inf, NaN): exact for exponents 1..252.
 // build: hipcc -O3 --offload-arch=gfx950 -std=c++17 rcp_exact.hip -o rcp_exact
 #include <hip/hip_runtime.h>
 
@@ -53,15 +55,8 @@ int main() {
     unsigned int hf[256];
     CK(hipMemcpy(hb, bad, sizeof hb, hipMemcpyDeviceToHost));
     CK(hipMemcpy(hf, first, sizeof hf, hipMemcpyDeviceToHost));
-    int lo = -1, hi = -1;
     unsigned long long total = 0;
-    for (int e = 0; e < 256; ++e) {
-        total += hb[e];
-        if (hb[e] == 0) {
-            if (lo < 0 || (hi >= 0 && hi != e - 1)) lo = (lo < 0 ? e : lo);
-            if (hi == e - 1 || hi < 0) hi = e;
-        }
-    }
+    for (int e = 0; e < 256; ++e) total += hb[e];
     std::printf("{\"total_mismatches\": %llu, \"per_exponent\": {", total);
     bool c = false;
     for (int e = 0; e < 256; ++e)
