@@ -28,6 +28,8 @@ def kernel_key(name):
         return f"{ns}cp_rollout_kernel<{kind}>"
     if "cp_reset_kernel" in name:
         return f"{ns}cp_reset_kernel"
+    if "cp_render_small2_kernel" in name:
+        return "cp_render_small2_kernel"
     for k in ("cp_init_kernel", "cp_mask_to_list_kernel", "cp_render_small_kernel",
               "cp_render_kernel", "cp_raster_table_kernel", "cp_event_kernel"):
         if k in name:
