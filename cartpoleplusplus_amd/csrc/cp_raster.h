@@ -99,21 +99,17 @@ CP_DEV void box_rect(const Cam& k, V3 cc, const Axes& A, V3 h, float sxk, float 
     out[3] = (int16_t)fminf(lim, ceilf(y1) + 1.0f);
 }
 
-// 1.0f / x, correctly rounded.  CP_RCP_SHORT: the hardware reciprocal and one FMA Newton step, which
-// is the correctly rounded result for every x whose biased exponent lies in [RCP_EXP_LO, RCP_EXP_HI]
-// (checked for all 2^32 floats on gfx950, tools/micro/rcp_exact.hip); other x (zero, denormal, huge,
-// inf, NaN) take the IEEE division.  3 VALU instead of ~10 in the common case.
-#ifdef CP_RCP_SHORT
-constexpr unsigned RCP_EXP_LO = CP_RCP_EXP_LO, RCP_EXP_HI = CP_RCP_EXP_HI;
-#endif
+// 1.0f / x, correctly rounded (the oracle's 1.0f / d): the hardware reciprocal and one FMA Newton
+// step, which is the correctly rounded result for every x whose biased exponent lies in [1, 252]
+// (checked for all 2^32 floats on gfx950: tools/micro/rcp_exact.hip, profiles/rd4e_rcp_exact.json);
+// other x (zero, denormal, |x| >= 2^126, inf, NaN) take the IEEE division.  3 VALU instead of ~10.
+constexpr unsigned RCP_EXP_LO = 1, RCP_EXP_HI = 252;
 CP_DEV float rcp_rn(float x) {
-#ifdef CP_RCP_SHORT
     const unsigned ex = (__float_as_uint(x) >> 23) & 0xFFu;
     if (ex - RCP_EXP_LO <= RCP_EXP_HI - RCP_EXP_LO) {
         const float y = __builtin_amdgcn_rcpf(x);
         return __builtin_fmaf(__builtin_fmaf(-x, y, 1.0f), y, y);
     }
-#endif
     return 1.0f / x;
 }
 
@@ -397,7 +393,6 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_kernel(
 // pass maps codes to colours through a per-repeat LUT and streams strips of 64
 // pixels out as cp_render_kernel does.
 constexpr int CODE_BG = 30;  // background; codes 0..29 = body * 6 + face (body 0 = ground)
-constexpr int CODE_NONE = 0xFF;  // cp_render_small2_kernel: no dynamic body seen yet (ground / background)
 struct SmallLds {
     int lut, best, code, stage, total;
     RenderLds w;  // the scene part (its own face / stage fields unused)
@@ -589,9 +584,10 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small_kernel(
 }
 
 // ---- small frames, v2 (round 4): the same images as cp_render_small_kernel, fewer instructions.
-// For NF = C * R frames known at compile time: the code buffer is pixel-major, [npx][CS] bytes
-// (CS = NF rounded up to 4), so the colour pass reads a pixel's codes with CS / 4 dword loads
-// instead of NF byte loads and the initialisation writes dwords; the pixel's 3 * NF float16 values
+// For NF = C * R frames known at compile time: the code buffer holds one word per pixel with the
+// pixel's NF codes in 5-bit fields (frame f at bits 5 f, 31 = no body yet; 16 bits for NF <= 3, 32 for
+// NF <= 6), so the colour pass reads a pixel's codes with one load, and the buffer (5 KB at 50 x 50,
+// NF = 3) leaves room for 8 blocks (32 waves) per CU; the pixel's 3 * NF float16 values
 // are assembled in registers and staged with dword writes (one 16-bit write at an odd start) instead
 // of 3 * NF 16-bit writes; the box rectangles use the hardware reciprocal (box_rect<true>).  The dense
 // ray tests, the colour LUT and the strip stores are cp_render_small_kernel's.
@@ -599,13 +595,17 @@ struct Small2Lds {
     int lut, best, code, stage, total;
     RenderLds w;
 };
+constexpr int CODE5_NONE = 31;  // a code field no body has written (the pixel shows its static class)
+template <bool SHORT> struct CodeWordT { using T = uint32_t; };
+template <> struct CodeWordT<true> { using T = uint16_t; };
+template <int NF> using CodeWord = typename CodeWordT<(NF <= 3)>::T;
 // per wave: the strip's 512 values between two 24-value margins (a pixel's 3 * NF <= 24 values overhang a
 // strip edge by less than that; 16-byte multiples)
 template <int NF>
 __host__ __device__ constexpr int small2_stage_halves() { return 24 + WAVE_R * 8 + 24; }
 template <int NF>
 __host__ __device__ inline Small2Lds render_small2_lds(int C, int R, int npx) {
-    constexpr int CS = (NF + 3) & ~3;
+    static_assert(NF <= 6, "five-bit code fields: at most 6 frames in a word");
     Small2Lds s;
     s.w = render_lds(C, R);
     int o = s.w.face;
@@ -615,7 +615,7 @@ __host__ __device__ inline Small2Lds render_small2_lds(int C, int R, int npx) {
     const int stage_bytes = RENDER_WAVES * 2 * small2_stage_halves<NF>() * 2;
     s.best = o;
     s.stage = o; o = (o + (npx * 4 > stage_bytes ? npx * 4 : stage_bytes) + 15) & ~15;
-    s.code = o;  o = (o + npx * CS + 15) & ~15;
+    s.code = o;  o = (o + npx * (int)sizeof(CodeWord<NF>) + 15) & ~15;
     s.total = o;
     return s;
 }
@@ -625,7 +625,8 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
     cp_raster_config rc, cp_physics P, const int32_t* list, const int32_t* count, const float* poses,
     const float4* tabd, const uint8_t* cls, uint16_t* pixels) {
     constexpr int R = RR, NF = CC * RR;  // cameras and repeats at compile time (the launcher checks them)
-    constexpr int CS = (NF + 3) & ~3, PP = 3 * NF, NT = RENDER_WAVES * WAVE_R;
+    constexpr int PP = 3 * NF, NT = RENDER_WAVES * WAVE_R;
+    using CWord = CodeWord<NF>;
     extern __shared__ __align__(16) unsigned char render_lds_raw[];
     if ((int)blockIdx.x >= *count) return;  // block-uniform
     const int env = list[blockIdx.x];
@@ -643,7 +644,7 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
     int16_t* srect = reinterpret_cast<int16_t*>(base + L.w.rect);
     uint2* slut = reinterpret_cast<uint2*>(base + L.lut);
     float* sbest = reinterpret_cast<float*>(base + L.best);
-    uint8_t* scode = reinterpret_cast<uint8_t*>(base + L.code);
+    CWord* scw = reinterpret_cast<CWord*>(base + L.code);
     uint16_t* stage = reinterpret_cast<uint16_t*>(base + L.stage) + wave * 2 * small2_stage_halves<NF>();
 
     const float* pe = poses + (size_t)env * R * CP_NUM_DYN * 7;
@@ -656,12 +657,12 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
         a9[6] = A.a2.x; a9[7] = A.a2.y; a9[8] = A.a2.z;
         sc[tid * 3 + 0] = q[0]; sc[tid * 3 + 1] = q[1]; sc[tid * 3 + 2] = q[2];
     }
-    // every frame starts as "no body hit" (CODE_NONE): the dense pass compares such a pixel against the
-    // ground's t from the table and the colour pass shows its static class (cls, L1-resident): a memset
-    // instead of copying the class table into every block
+    // every frame starts as "no body hit" (CODE5_NONE in every field): the dense pass compares such a
+    // pixel against the ground's t from the table and the colour pass shows its static class (cls,
+    // L1-resident): a memset instead of copying the class table into every block
     {
-        uint4* c16 = reinterpret_cast<uint4*>(scode);
-        const int n16 = (npx * CS + 15) >> 4;
+        uint4* c16 = reinterpret_cast<uint4*>(scw);
+        const int n16 = (npx * (int)sizeof(CWord) + 15) >> 4;
         for (int k = tid; k < n16; k += NT) c16[k] = make_uint4(~0u, ~0u, ~0u, ~0u);
     }
     __syncthreads();
@@ -718,7 +719,6 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
 #pragma unroll 1
     for (int f = 0; f < NF; ++f) {
         const int cam = f / R, r = f % R;
-        uint8_t* cf = scode + f;
         for (int b = 1; b < CP_NUM_BODIES; ++b) {
             const int item = f * CP_NUM_DYN + b - 1;
             const int x0 = srect[item * 4 + 0], x1 = srect[item * 4 + 1];
@@ -740,11 +740,13 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
                 float t, sg;
                 int ax;
                 if (ray_box_o(mk(t0.x, t0.y, t0.z), ol, A, h, t, ax, sg)) {
-                    const int cur = cf[(size_t)p * CS];
-                    const float best = cur == CODE_NONE ? t0.w : sbest[p];
+                    const uint32_t w = scw[p];
+                    const int cur = (int)((w >> (5 * f)) & 31u);
+                    const float best = cur == CODE5_NONE ? t0.w : sbest[p];
                     if (t < best) {
                         sbest[p] = t;
-                        cf[(size_t)p * CS] = (uint8_t)(b * 6 + ax * 2 + (sg > 0.0f ? 1 : 0));
+                        const uint32_t c = (uint32_t)(b * 6 + ax * 2 + (sg > 0.0f ? 1 : 0));
+                        scw[p] = (CWord)((w & ~(31u << (5 * f))) | (c << (5 * f)));
                     }
                 }
             }
@@ -769,73 +771,6 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
     if (Q > 0) return;
 #endif
     constexpr int SH = small2_stage_halves<NF>();
-#ifdef CP_RV_PAIRS
-    // pixel pairs: strips of 128 output chunks (1,024 values, the wave's two stages as one), each lane
-    // computes two consecutive pixels (<= 58 pairs overlap a strip at 3 * NF >= 9), so a lane's 2 * 3 * NF values start
-    // at the same parity in every lane of the strip: dword writes without per-lane selects
-    constexpr int MP = (2 * PP + 7) / 8 * 8;                             // margin: a pair's values, 16-byte multiple
-    static_assert(2 * MP + 16 * WAVE_R <= 2 * SH, "small2_stage_halves: a 128-chunk strip and its margins");
-    const int wv = __builtin_amdgcn_readfirstlane(wave);
-    for (int sa = wv * 2 * WAVE_R; sa < Q; sa += 2 * RENDER_WAVES * WAVE_R) {  // wave-uniform
-        const int g0 = sa * 8 - sh;                                      // the strip's first value
-        const int glo = g0 > 0 ? g0 : 0;
-        const int ghi = (g0 + 16 * WAVE_R < N ? g0 + 16 * WAVE_R : N) - 1;
-        const int plo = glo / PP, phi = ghi / PP;                       // pixels overlapping the strip
-        const int a = (MP + plo * PP - g0) & 1;                          // the parity of every pair's start
-        for (int j = lane; 2 * j <= phi - plo; j += WAVE_R) {             // one pass for 3 * NF >= 9
-            const int p = plo + 2 * j;
-            const int pn = p + 1 < npx ? p + 1 : p;                     // past the env's last pixel: a copy
-            uint16_t hv[2 * PP];
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const int pp = k ? pn : p;
-                uint32_t cw[CS / 4];
-#pragma unroll
-                for (int q = 0; q < CS / 4; ++q) cw[q] = reinterpret_cast<const uint32_t*>(scode + (size_t)pp * CS)[q];
-                int cl0 = cls[pp], cl1 = C > 1 ? cls[(size_t)npx + pp] : cl0;
-                cl0 = cl0 < 6 ? cl0 : CODE_BG;
-                cl1 = cl1 < 6 ? cl1 : CODE_BG;
-#pragma unroll
-                for (int f = 0; f < NF; ++f) {
-                    int code = (int)((cw[f / 4] >> (8 * (f % 4))) & 0xFFu);
-                    if (code == CODE_NONE) code = f < R ? cl0 : cl1;
-                    const uint2 c = slut[(f % R) * 32 + code];
-                    hv[k * PP + f] = (uint16_t)c.x;
-                    hv[k * PP + NF + f] = (uint16_t)(c.x >> 16);
-                    hv[k * PP + 2 * NF + f] = (uint16_t)c.y;
-                }
-            }
-            const int o = MP + p * PP - g0;                              // in [MP - PP, MP + 1024)
-            uint32_t* s32 = reinterpret_cast<uint32_t*>(stage) + ((o + a) >> 1);
-            if (a == 0) {
-#pragma unroll
-                for (int k = 0; k < PP; ++k) s32[k] = (uint32_t)hv[2 * k] | ((uint32_t)hv[2 * k + 1] << 16);
-            } else {
-                stage[o] = hv[0];
-#pragma unroll
-                for (int k = 0; k < PP - 1; ++k) s32[k] = (uint32_t)hv[2 * k + 1] | ((uint32_t)hv[2 * k + 2] << 16);
-                stage[o + 2 * PP - 1] = hv[2 * PP - 1];
-            }
-        }
-        wave_sync();
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int q = sa + u * WAVE_R + lane;
-            const int e0 = q * 8 - sh;                                   // the chunk's first value
-            if (q < Q) {
-                const uint16_t* src = stage + MP + (u * WAVE_R + lane) * 8;
-                if (e0 >= 0 && e0 + 8 <= N) {
-                    store_stream(&d4[q], *reinterpret_cast<const uint4*>(src));
-                } else {  // the env's first / last chunk: its values only (the neighbour env owns the rest)
-                    for (int e = 0; e < 8; ++e)
-                        if (e0 + e >= 0 && e0 + e < N) out[e0 + e] = src[e];
-                }
-            }
-        }
-        wave_sync();
-    }
-    if (Q >= 0) return;
-#endif
     // two strips per trip (stage u = 0, 1): two independent load / LUT / stage chains between syncs;
     // wave w takes strips w, w + 4, w + 8, ... (in units of 64 chunks)
     for (int s0 = wave * WAVE_R; s0 < Q; s0 += 2 * RENDER_WAVES * WAVE_R) {
@@ -850,9 +785,7 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
             const int plo = glo / PP, np = ghi / PP - plo + 1;          // pixels overlapping the strip
             for (int i = lane; i < np; i += WAVE_R) {                   // one pass for 3 * NF >= 9
                 const int p = plo + i;
-                uint32_t cw[CS / 4];
-#pragma unroll
-                for (int q = 0; q < CS / 4; ++q) cw[q] = reinterpret_cast<const uint32_t*>(scode + (size_t)p * CS)[q];
+                const uint32_t cw = scw[p];
                 // the pixel's static class per camera (ground face or background), shown where no body is
                 int cl0 = cls[p], cl1 = C > 1 ? cls[(size_t)npx + p] : cl0;
                 cl0 = cl0 < 6 ? cl0 : CODE_BG;
@@ -860,8 +793,8 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
                 uint16_t hv[PP];
 #pragma unroll
                 for (int f = 0; f < NF; ++f) {
-                    int code = (int)((cw[f / 4] >> (8 * (f % 4))) & 0xFFu);
-                    if (code == CODE_NONE) code = f < R ? cl0 : cl1;
+                    int code = (int)((cw >> (5 * f)) & 31u);
+                    if (code == CODE5_NONE) code = f < R ? cl0 : cl1;
                     const uint2 c = slut[(f % R) * 32 + code];
                     hv[f] = (uint16_t)c.x;
                     hv[NF + f] = (uint16_t)(c.x >> 16);
