@@ -585,17 +585,17 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small_kernel(
 
 // ---- small frames, v2 (round 4): the same images as cp_render_small_kernel, fewer instructions.
 // For NF = C * R frames known at compile time: the code buffer holds one word per pixel with the
-// pixel's NF codes in 5-bit fields (frame f at bits 5 f, 31 = no body yet; 16 bits for NF <= 3, 32 for
-// NF <= 6), so the colour pass reads a pixel's codes with one load, and the buffer (5 KB at 50 x 50,
-// NF = 3) leaves room for 8 blocks (32 waves) per CU; the pixel's 3 * NF float16 values
-// are assembled in registers and staged with dword writes (one 16-bit write at an odd start) instead
-// of 3 * NF 16-bit writes; the box rectangles use the hardware reciprocal (box_rect<true>).  The dense
-// ray tests, the colour LUT and the strip stores are cp_render_small_kernel's.
+// pixel's NF codes in 5-bit fields (frame f at bits 5 f, seeded with the static class; 16 bits for
+// NF <= 3, 32 for NF <= 6), so the colour pass reads a pixel's codes with one load and no class
+// lookup, and the buffer (5 KB at 50 x 50, NF = 3) leaves room for 8 blocks (32 waves) per CU; the
+// pixel's 3 * NF float16 values are assembled in registers and staged with dword writes (one 16-bit
+// write at an odd start) instead of 3 * NF 16-bit writes; the box rectangles use the hardware
+// reciprocal (box_rect<true>).  The dense ray tests, the colour LUT and the strip stores are
+// cp_render_small_kernel's.
 struct Small2Lds {
     int lut, best, code, stage, total;
     RenderLds w;
 };
-constexpr int CODE5_NONE = 31;  // a code field no body has written (the pixel shows its static class)
 template <bool SHORT> struct CodeWordT { using T = uint32_t; };
 template <> struct CodeWordT<true> { using T = uint16_t; };
 template <int NF> using CodeWord = typename CodeWordT<(NF <= 3)>::T;
@@ -657,13 +657,18 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
         a9[6] = A.a2.x; a9[7] = A.a2.y; a9[8] = A.a2.z;
         sc[tid * 3 + 0] = q[0]; sc[tid * 3 + 1] = q[1]; sc[tid * 3 + 2] = q[2];
     }
-    // every frame starts as "no body hit" (CODE5_NONE in every field): the dense pass compares such a
-    // pixel against the ground's t from the table and the colour pass shows its static class (cls,
-    // L1-resident): a memset instead of copying the class table into every block
-    {
-        uint4* c16 = reinterpret_cast<uint4*>(scw);
-        const int n16 = (npx * (int)sizeof(CWord) + 15) >> 4;
-        for (int k = tid; k < n16; k += NT) c16[k] = make_uint4(~0u, ~0u, ~0u, ~0u);
+    // every frame starts as its static class (the ground face the pixel's ray hits, or the background;
+    // cls, L1-resident): field f of pixel p = class of p in camera f / R.  The dense pass compares a
+    // pixel whose field still holds a static class against the ground's t from the table
+#pragma unroll 4
+    for (int k = tid; k < npx; k += NT) {
+        uint32_t c0 = cls[k], c1 = C > 1 ? cls[(size_t)npx + k] : c0;
+        c0 = c0 < 6 ? c0 : CODE_BG;
+        c1 = c1 < 6 ? c1 : CODE_BG;
+        uint32_t w = 0;
+#pragma unroll
+        for (int f = 0; f < NF; ++f) w |= (f < R ? c0 : c1) << (5 * f);
+        scw[k] = (CWord)w;
     }
     __syncthreads();
     const float syk = rc.tan_half_fov;
@@ -742,7 +747,7 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
                 if (ray_box_o(mk(t0.x, t0.y, t0.z), ol, A, h, t, ax, sg)) {
                     const uint32_t w = scw[p];
                     const int cur = (int)((w >> (5 * f)) & 31u);
-                    const float best = cur == CODE5_NONE ? t0.w : sbest[p];
+                    const float best = (cur < 6 || cur == CODE_BG) ? t0.w : sbest[p];
                     if (t < best) {
                         sbest[p] = t;
                         const uint32_t c = (uint32_t)(b * 6 + ax * 2 + (sg > 0.0f ? 1 : 0));
@@ -787,14 +792,10 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
                 const int p = plo + i;
                 const uint32_t cw = scw[p];
                 // the pixel's static class per camera (ground face or background), shown where no body is
-                int cl0 = cls[p], cl1 = C > 1 ? cls[(size_t)npx + p] : cl0;
-                cl0 = cl0 < 6 ? cl0 : CODE_BG;
-                cl1 = cl1 < 6 ? cl1 : CODE_BG;
                 uint16_t hv[PP];
 #pragma unroll
                 for (int f = 0; f < NF; ++f) {
-                    int code = (int)((cw >> (5 * f)) & 31u);
-                    if (code == CODE5_NONE) code = f < R ? cl0 : cl1;
+                    const int code = (int)((cw >> (5 * f)) & 31u);
                     const uint2 c = slut[(f % R) * 32 + code];
                     hv[f] = (uint16_t)c.x;
                     hv[NF + f] = (uint16_t)(c.x >> 16);
