@@ -670,12 +670,21 @@ def secondary_lines(dev, R, W=20):
         autoreset = kw.pop("autoreset", "same_step")
         next_step = autoreset == "next_step"
         w = W + (40 if kw.get("done_on_bounds") else 0)
+        if rollout:   # warm-up = one full-window launch, so the timed launch (from the window boundary) has
+            w = WINDOW  # the same K: kernel, output buffers and the rollout's temporaries all warm
         env = BatchedCartpole(B, dev.index, action_repeats=R, steps_per_repeat=1, max_episode_len=WINDOW,
                               initial_force=55.0, autoreset=autoreset, seed=SEED, **kw)
         actions = make_actions(continuous, B, 0, w + K, SEED, dev)
         env.reset()
-        for t in range(w):
-            env.step(actions[t])
+        if rollout:   # warm-up through the kernel itself, its output buffers allocated up front (~2 GB)
+            env.reserve_rollout(rollout)
+            env.rollout(actions[:w])
+        else:
+            for t in range(w):
+                env.step(actions[t])
+        r_, _ = env.episode_returns()   # the return-gather path warm (a window boundary falls in every leg)
+        return_histogram(gather_returns(r_), WINDOW)
+        del r_
         torch.cuda.synchronize()
         ep0 = episodes(env)
         p0 = pending(env) if next_step else 0
@@ -839,8 +848,13 @@ def main():
     n_med = 1 if args.no_median else 5
     actions = make_actions(args.continuous, B, spec["env_id_offset"], W + n_med * (K + ss_steps), SEED, dev)
     env.reset()
-    for t in range(W):
-        env.step(actions[t])
+    if args.rollout and args.streams == 1:   # the rollout kernel loaded, its output buffers allocated (~2 GB)
+        env.reserve_rollout(args.rollout)
+        if W:
+            env.rollout(actions[:W])
+    else:
+        for t in range(W):
+            env.step(actions[t])
     # warm the return-gather path too (cp_episode_returns, the RCCL all-gather, torch's bincount):
     # their first call in a process loads code objects and sets up buffers, ~17 ms once, which would
     # otherwise land in whichever timed window holds the first 200-step boundary

@@ -153,7 +153,7 @@ class BatchedCartpole:
         With autoreset, self.rollout_terminal_obs (K,B,R,2,7) holds the finishing obs of the
         episodes that ended (terminal=False skips it).  Afterwards self.obs / reward / done (and
         terminal_obs when collected) hold step K-1's values, as after K step() calls.  The returned
-        tensors are reused (overwritten) by the next rollout of the same K: clone them to keep them."""
+        tensors are views of buffers reused (overwritten) by the next rollout: clone them to keep them."""
         if not isinstance(actions, torch.Tensor):
             actions = torch.as_tensor(actions)
         if actions.dim() < 3:
@@ -168,14 +168,7 @@ class BatchedCartpole:
                 raise ValueError(f"actions: int8 indices (K, B, 2) or float (K, B, 2, 2), got {actions.dtype}")
             actions = _device_buffer(actions, (K, self.B, 2, 2), torch.float32, self.device, "continuous actions")
         want_term = bool(self.cfg.autoreset if terminal is None else terminal)
-        key = (K, want_term)
-        if getattr(self, "_roll_key", None) != key:   # output buffers reused across rollouts of one K
-            f32 = dict(device=self.device, dtype=torch.float32)
-            self._roll_bufs = (torch.empty((K, self.B, self.R, 2, 7), **f32), torch.empty((K, self.B), **f32),
-                               torch.empty((K, self.B), device=self.device, dtype=torch.uint8),
-                               torch.zeros((K, self.B, self.R, 2, 7), **f32) if want_term else None)
-            self._roll_key = key
-        obs, rew, done, self.rollout_terminal_obs = self._roll_bufs
+        obs, rew, done, self.rollout_terminal_obs = self._roll_buffers(K, want_term)
         native.check(self.h, self.lib.cp_rollout(self.h, K, _ptr(actions), kind, _ptr(obs), _ptr(rew), _ptr(done),
                                                  _ptr(self.rollout_terminal_obs), self._stream()), "cp_rollout")
         # the handle is K steps on: the step()-level attributes follow it (the last step's values)
@@ -190,6 +183,26 @@ class BatchedCartpole:
             last = self.rollout_terminal_obs[k_last.long(), torch.arange(self.B, device=self.device)]
             self.terminal_obs[fin] = last[fin]
         return obs, rew, done
+
+    def reserve_rollout(self, K, terminal=None):
+        """Allocate rollout()'s output buffers for up to K steps now: at C3 size they are ~2 GB, and a
+        first allocation inside a timed region costs tens of milliseconds."""
+        self._roll_buffers(int(K), bool(self.cfg.autoreset if terminal is None else terminal))
+
+    def _roll_buffers(self, K, want_term):
+        """Views [:K] of grow-only output buffers (any rollout of at most the largest K so far reuses them)."""
+        cap, term = getattr(self, "_roll_cap", (0, False))
+        if K > cap or (want_term and not term):
+            K_cap = max(K, cap)
+            f32 = dict(device=self.device, dtype=torch.float32)
+            self._roll_bufs = None   # free the old buffers before allocating the larger ones
+            self._roll_bufs = (torch.empty((K_cap, self.B, self.R, 2, 7), **f32),
+                               torch.empty((K_cap, self.B), **f32),
+                               torch.empty((K_cap, self.B), device=self.device, dtype=torch.uint8),
+                               torch.zeros((K_cap, self.B, self.R, 2, 7), **f32) if (want_term or term) else None)
+            self._roll_cap = (K_cap, want_term or term)
+        obs, rew, done, term_obs = self._roll_bufs
+        return obs[:K], rew[:K], done[:K], (term_obs[:K] if want_term else None)
 
     def set_kernel_shape(self, step="auto", reset="auto"):
         """Override the step / autoreset kernel shapes ("auto", "throughput" or "latency";

@@ -197,3 +197,20 @@ def test_rollout_full_size_c3_k200_across_the_burst(oracle_mod, shape):
                 _assert_same(bt[k][od.astype(bool)], ot[od.astype(bool)], f"block {lo} terminal obs step {k}")
         _assert_same(gst[:, lo:lo + 128], orc.get_state(), f"block {lo} final state")
     roll.close()
+
+
+def test_rollout_buffers_reserved_and_grow_only():
+    """reserve_rollout(K) allocates the outputs up front; a shorter rollout returns views of the same
+    buffers (no allocation inside a timed region), a longer one grows them."""
+    env = BatchedCartpole(16, 0, action_repeats=2, autoreset=True)
+    env.reset()
+    env.reserve_rollout(8)
+    o1, r1, d1 = env.rollout(torch.zeros((5, 16, 2), dtype=torch.int8, device="cuda"))
+    p = o1.data_ptr()
+    o2, r2, d2 = env.rollout(torch.zeros((3, 16, 2), dtype=torch.int8, device="cuda"))
+    assert o2.shape == (3, 16, 2, 2, 7) and r2.shape == (3, 16) and d2.shape == (3, 16)
+    assert o2.data_ptr() == p and env.rollout_terminal_obs.shape == (3, 16, 2, 2, 7)
+    assert torch.equal(env.obs, o2[-1])
+    o3, _, _ = env.rollout(torch.zeros((10, 16, 2), dtype=torch.int8, device="cuda"))
+    assert o3.shape[0] == 10 and torch.isfinite(o3).all()
+    env.close()
