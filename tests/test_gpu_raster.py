@@ -150,11 +150,14 @@ def test_full_size_c5_properties_and_subset(oracle_mod):
         _check_env(oracle_mod, env, pix, st, k, 2)
 
 
-@pytest.mark.parametrize("R,C,W,H", [(3, 1, 50, 50), (2, 1, 50, 50), (1, 1, 37, 23), (2, 2, 50, 50), (3, 2, 37, 23)])
+@pytest.mark.parametrize("R,C,W,H", [(3, 1, 50, 50), (2, 1, 50, 50), (1, 1, 37, 23), (4, 1, 41, 29), (6, 1, 30, 20),
+                                     (1, 2, 50, 50), (2, 2, 50, 50), (3, 2, 37, 23)])
 def test_render_v2_equals_v1_every_pixel(monkeypatch, R, C, W, H):
-    """cp_render_small2_kernel<C*R> (round 4: pixel-major codes, packed stage writes, reciprocal
-    rectangles) against the round-3 small-frame kernel (CP_RENDER_V1=1 at cp_create): every pixel of
-    every env, frame and step equal, bit for bit (both are held to the oracle by the tests above)."""
+    """cp_render_small2_kernel<C, R> (round 4: code words of 5-bit fields, 16-bit at C * R <= 3 and
+    32-bit up to 6, packed stage writes, reciprocal rectangles, the exact short reciprocal) against the
+    round-3 small-frame kernel (CP_RENDER_V1=1 at cp_create), every (C, R) it is instantiated for:
+    every pixel of every env, frame and step equal, bit for bit (both are held to the oracle by the
+    tests above)."""
     B, T = 64, 12
     out = []
     for v1 in ("1", "0"):
