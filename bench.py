@@ -138,6 +138,23 @@ def render_kernel_bytes(H, W, C, R):
     return 2 * H * W * 3 * C * R + 4 * R * 4 * 7 + 4
 
 
+SMALL2_PAIRS = {(1, 1), (1, 2), (1, 3), (1, 4), (1, 6), (2, 1), (2, 2), (2, 3)}   # cp_kernels.hip launch_render
+
+
+def render_kernel_name(H, W, C, R):
+    """The render kernel cp_step launches for this raster configuration (launch_render's choice:
+    the compile-time (C, R) pairs of cp_render_small2_kernel when its LDS fits 48 KB, unless
+    CP_RENDER_V1=1; else the round-3 one-block-per-env kernel, or the wave kernel for large frames)."""
+    npx, nf = H * W, C * R
+    def al(x):
+        return (x + 15) & ~15
+    head = al(al(al(al(R * 4 * 9 * 4) + R * 4 * 3 * 4) + C * R * 4 * 3 * 4) + C * R * 4 * 4 * 2)
+    small2 = al(al(head + R * 32 * 8) + max(npx * 4, 4 * 2 * (24 + 64 * 8 + 24) * 2)) + npx * (2 if nf <= 3 else 4)
+    if (C, R) in SMALL2_PAIRS and os.environ.get("CP_RENDER_V1") != "1" and small2 <= 48 * 1024:
+        return "cp_render_small2_kernel"
+    return "cp_render_small_kernel"
+
+
 def _pmc_files():
     import glob
     return list(reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))))
@@ -935,7 +952,7 @@ def main():
         per_launch_s = tm["render_ms"] / max(1, tm["render_launches"]) / 1e3  # one launch per step
         bytes_launch = B * render_kernel_bytes(rc.height, rc.width, rc.num_cameras, R)
         achieved = bytes_launch / per_launch_s / 1e9
-        kernel = "cp_render_small_kernel"
+        kernel = render_kernel_name(rc.height, rc.width, rc.num_cameras, R)
         traffic, traffic_src = pmc_traffic(kernel, B, R, kind)
     valu = None
     if not args.raster:

@@ -639,7 +639,6 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
     const Small2Lds L = render_small2_lds<NF>(C, R, npx);
     unsigned char* base = render_lds_raw;
     float* sax = reinterpret_cast<float*>(base + L.w.ax);
-    float* sc = reinterpret_cast<float*>(base + L.w.c);
     float* soloc = reinterpret_cast<float*>(base + L.w.oloc);
     int16_t* srect = reinterpret_cast<int16_t*>(base + L.w.rect);
     uint2* slut = reinterpret_cast<uint2*>(base + L.lut);
@@ -647,6 +646,10 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
     CWord* scw = reinterpret_cast<CWord*>(base + L.code);
     uint16_t* stage = reinterpret_cast<uint16_t*>(base + L.stage) + wave * 2 * small2_stage_halves<NF>();
 
+    // the scene in one phase (one barrier): wave 0 the box axes for the dense pass, wave 1 the camera-space
+    // terms and screen rectangles, waves 2-3 (then 0-1) the colour LUT, all threads the class seeding;
+    // the rectangle and LUT threads take their boxes' axes from the poses themselves (quat_axes, the
+    // same arithmetic as wave 0's, so the same bits) instead of waiting for wave 0's LDS writes
     const float* pe = poses + (size_t)env * R * CP_NUM_DYN * 7;
     if (tid < R * CP_NUM_DYN) {
         const float* q = pe + tid * 7;
@@ -655,45 +658,62 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
         a9[0] = A.a0.x; a9[1] = A.a0.y; a9[2] = A.a0.z;
         a9[3] = A.a1.x; a9[4] = A.a1.y; a9[5] = A.a1.z;
         a9[6] = A.a2.x; a9[7] = A.a2.y; a9[8] = A.a2.z;
-        sc[tid * 3 + 0] = q[0]; sc[tid * 3 + 1] = q[1]; sc[tid * 3 + 2] = q[2];
     }
     // every frame starts as its static class (the ground face the pixel's ray hits, or the background;
     // cls, L1-resident): field f of pixel p = class of p in camera f / R.  The dense pass compares a
     // pixel whose field still holds a static class against the ground's t from the table
-#pragma unroll 4
-    for (int k = tid; k < npx; k += NT) {
-        uint32_t c0 = cls[k], c1 = C > 1 ? cls[(size_t)npx + k] : c0;
+    auto seed_word = [&](uint32_t c0, uint32_t c1) -> uint32_t {
         c0 = c0 < 6 ? c0 : CODE_BG;
         c1 = c1 < 6 ? c1 : CODE_BG;
         uint32_t w = 0;
 #pragma unroll
         for (int f = 0; f < NF; ++f) w |= (f < R ? c0 : c1) << (5 * f);
-        scw[k] = (CWord)w;
+        return w;
+    };
+    if ((npx & 3) == 0) {  // four pixels per class load (both cameras' rows 4-byte aligned), one LDS write
+        const uint32_t* c32 = reinterpret_cast<const uint32_t*>(cls);
+        for (int k = tid; k < (npx >> 2); k += NT) {
+            const uint32_t a0 = c32[k], a1 = C > 1 ? c32[(npx >> 2) + k] : a0;
+            uint32_t w[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) w[j] = seed_word((a0 >> (8 * j)) & 0xFFu, (a1 >> (8 * j)) & 0xFFu);
+            if constexpr (sizeof(CWord) == 2) {
+                reinterpret_cast<uint2*>(scw)[k] = make_uint2(w[0] | (w[1] << 16), w[2] | (w[3] << 16));
+            } else {
+                reinterpret_cast<uint4*>(scw)[k] = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+        }
+    } else {
+#pragma unroll 4
+        for (int k = tid; k < npx; k += NT) {
+            const uint32_t c0 = cls[k];
+            scw[k] = (CWord)seed_word(c0, C > 1 ? cls[(size_t)npx + k] : c0);
+        }
     }
-    __syncthreads();
     const float syk = rc.tan_half_fov;
     const float sxk = rc.tan_half_fov * ((float)W / (float)H);
-    if (tid < NF * CP_NUM_DYN) {
-        const int cam = tid / (R * CP_NUM_DYN), rb = tid % (R * CP_NUM_DYN), b = rb % CP_NUM_DYN;
+    static_assert(NF * CP_NUM_DYN <= WAVE_R, "one rectangle per lane of wave 1");
+    if (tid >= WAVE_R && tid < WAVE_R + NF * CP_NUM_DYN) {
+        const int item = tid - WAVE_R;
+        const int cam = item / (R * CP_NUM_DYN), rb = item % (R * CP_NUM_DYN), b = rb % CP_NUM_DYN;
         const Cam k = make_cam(rc, cam);
-        const float* a9 = sax + rb * 9;
-        Axes A;
-        A.a0 = mk(a9[0], a9[1], a9[2]); A.a1 = mk(a9[3], a9[4], a9[5]); A.a2 = mk(a9[6], a9[7], a9[8]);
-        const V3 c = mk(sc[rb * 3 + 0], sc[rb * 3 + 1], sc[rb * 3 + 2]);
+        const float* qp = pe + rb * 7;
+        const Axes A = quat_axes(qp[3], qp[4], qp[5], qp[6]);
+        const V3 c = mk(qp[0], qp[1], qp[2]);
         const V3 oc = sub(k.eye, c);
-        soloc[tid * 3 + 0] = dot(oc, A.a0);
-        soloc[tid * 3 + 1] = dot(oc, A.a1);
-        soloc[tid * 3 + 2] = dot(oc, A.a2);
+        soloc[item * 3 + 0] = dot(oc, A.a0);
+        soloc[item * 3 + 1] = dot(oc, A.a1);
+        soloc[item * 3 + 2] = dot(oc, A.a2);
         int16_t q[4];
         box_rect<true>(k, c, A, mk(P.half_extents[b + 1][0], P.half_extents[b + 1][1], P.half_extents[b + 1][2]),
                        sxk, syk, W, H, q);
-        srect[tid * 4 + 0] = q[0] < 0 ? 0 : q[0];
-        srect[tid * 4 + 1] = q[1] > W - 1 ? (int16_t)(W - 1) : q[1];
-        srect[tid * 4 + 2] = q[2] < 0 ? 0 : q[2];
-        srect[tid * 4 + 3] = q[3] > H - 1 ? (int16_t)(H - 1) : q[3];
+        srect[item * 4 + 0] = q[0] < 0 ? 0 : q[0];
+        srect[item * 4 + 1] = q[1] > W - 1 ? (int16_t)(W - 1) : q[1];
+        srect[item * 4 + 2] = q[2] < 0 ? 0 : q[2];
+        srect[item * 4 + 3] = q[3] > H - 1 ? (int16_t)(H - 1) : q[3];
     }
     const V3 light = mk(rc.light[0], rc.light[1], rc.light[2]);
-    for (int it = tid; it < R * 32; it += NT) {  // colour LUT [r][code] (cp_render_small_kernel's)
+    for (int it = (tid + 2 * WAVE_R) % NT; it < R * 32; it += NT) {  // colour LUT [r][code] (cp_render_small_kernel's)
         const int r = it / 32, code = it % 32;
         uint16_t h[3];
         if (code < CP_NUM_BODIES * 6) {
@@ -703,8 +723,9 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
             if (b == 0) {
                 an = ax == 0 ? mk(1.0f, 0.0f, 0.0f) : (ax == 1 ? mk(0.0f, 1.0f, 0.0f) : mk(0.0f, 0.0f, 1.0f));
             } else {
-                const float* a9 = sax + (r * CP_NUM_DYN + b - 1) * 9 + 3 * ax;
-                an = mk(a9[0], a9[1], a9[2]);
+                const float* qp = pe + (r * CP_NUM_DYN + b - 1) * 7;
+                const Axes A = quat_axes(qp[3], qp[4], qp[5], qp[6]);
+                an = ax == 0 ? A.a0 : (ax == 1 ? A.a1 : A.a2);
             }
             const float ndl = dot(scl(an, sg), light);
             const float sh = fmaf_(rc.diffuse, ndl > 0.0f ? ndl : 0.0f, rc.ambient);
