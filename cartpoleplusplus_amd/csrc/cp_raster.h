@@ -603,6 +603,10 @@ template <int NF> using CodeWord = typename CodeWordT<(NF <= 3)>::T;
 // strip edge by less than that; 16-byte multiples)
 template <int NF>
 __host__ __device__ constexpr int small2_stage_halves() { return 24 + WAVE_R * 8 + 24; }
+#ifndef CP_RV_SPT
+#define CP_RV_SPT 2
+#endif
+constexpr int SMALL2_SPT = CP_RV_SPT;  // strips per trip of the colour pass (independent chains between syncs)
 template <int NF>
 __host__ __device__ inline Small2Lds render_small2_lds(int C, int R, int npx) {
     static_assert(NF <= 6, "five-bit code fields: at most 6 frames in a word");
@@ -612,7 +616,7 @@ __host__ __device__ inline Small2Lds render_small2_lds(int C, int R, int npx) {
     s.lut = o;   o = (o + R * 32 * 8 + 15) & ~15;
     // the dense pass's depth buffer and, after it, the colour pass's stages (two strips per wave) share
     // one region: they are never live together
-    const int stage_bytes = RENDER_WAVES * 2 * small2_stage_halves<NF>() * 2;
+    const int stage_bytes = RENDER_WAVES * SMALL2_SPT * small2_stage_halves<NF>() * 2;
     s.best = o;
     s.stage = o; o = (o + (npx * 4 > stage_bytes ? npx * 4 : stage_bytes) + 15) & ~15;
     s.code = o;  o = (o + npx * (int)sizeof(CodeWord<NF>) + 15) & ~15;
@@ -644,7 +648,7 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
     uint2* slut = reinterpret_cast<uint2*>(base + L.lut);
     float* sbest = reinterpret_cast<float*>(base + L.best);
     CWord* scw = reinterpret_cast<CWord*>(base + L.code);
-    uint16_t* stage = reinterpret_cast<uint16_t*>(base + L.stage) + wave * 2 * small2_stage_halves<NF>();
+    uint16_t* stage = reinterpret_cast<uint16_t*>(base + L.stage) + wave * SMALL2_SPT * small2_stage_halves<NF>();
 
     // the scene in one phase (one barrier): wave 0 the box axes for the dense pass, wave 1 the camera-space
     // terms and screen rectangles, waves 2-3 (then 0-1) the colour LUT, all threads the class seeding;
@@ -799,9 +803,9 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
     constexpr int SH = small2_stage_halves<NF>();
     // two strips per trip (stage u = 0, 1): two independent load / LUT / stage chains between syncs;
     // wave w takes strips w, w + 4, w + 8, ... (in units of 64 chunks)
-    for (int s0 = wave * WAVE_R; s0 < Q; s0 += 2 * RENDER_WAVES * WAVE_R) {
+    for (int s0 = wave * WAVE_R; s0 < Q; s0 += SMALL2_SPT * RENDER_WAVES * WAVE_R) {
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < SMALL2_SPT; ++u) {
             const int sa = s0 + u * RENDER_WAVES * WAVE_R;
             if (sa >= Q) break;  // wave-uniform
             uint16_t* st = stage + u * SH;
@@ -850,7 +854,7 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
         }
         wave_sync();
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < SMALL2_SPT; ++u) {
             const int q = s0 + u * RENDER_WAVES * WAVE_R + lane;
             const int e0 = q * 8 - sh;                                  // the chunk's first value
 #ifdef CP_RV_NO_STORE
