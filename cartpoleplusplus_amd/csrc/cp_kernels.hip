@@ -441,7 +441,6 @@ static int launch_render(cp_handle* h, const int32_t* list, const int32_t* count
     const int C = h->raster.num_cameras, R = h->cfg.action_repeats, npx = h->raster.width * h->raster.height;
     const uint8_t* cls = reinterpret_cast<const uint8_t*>(h->b.rtable + (size_t)C * npx);
     const size_t small = (size_t)cp::render_small_lds(C, R, npx).total;
-    const int F = C * R;
     // v2 of the small-frame kernel for the common (cameras, repeats) pairs, both compile-time
     auto small2 = [&](auto cc, auto rr) -> bool {
         constexpr int CC = decltype(cc)::value, RR = decltype(rr)::value;
@@ -457,8 +456,9 @@ static int launch_render(cp_handle* h, const int32_t* list, const int32_t* count
     using I2 = std::integral_constant<int, 2>;
     using I3 = std::integral_constant<int, 3>;
     using I4 = std::integral_constant<int, 4>;
-    if (small2(I1{}, I3{}) || small2(I1{}, I2{}) || small2(I1{}, I1{}) || small2(I1{}, I4{}) ||
-        small2(std::integral_constant<int, 1>{}, std::integral_constant<int, 6>{}) || small2(I2{}, I1{}) || small2(I2{}, I2{}) || small2(I2{}, I3{})) {
+    using I6 = std::integral_constant<int, 6>;
+    if (small2(I1{}, I3{}) || small2(I1{}, I2{}) || small2(I1{}, I1{}) || small2(I1{}, I4{}) || small2(I1{}, I6{}) ||
+        small2(I2{}, I1{}) || small2(I2{}, I2{}) || small2(I2{}, I3{})) {
         // launched
     } else if (small <= (size_t)cp::SMALL_LDS_MAX) {  // one block per env, dense ray tests
         hipLaunchKernelGGL(cp::cp_render_small_kernel, dim3((unsigned)h->cfg.num_envs),
