@@ -9,7 +9,8 @@
         --master-port P bench.py --gpus N --steps K --warmup W            # C4, externally launched
 
 Multi-GPU launch: with --gpus N > 1 and no WORLD_SIZE in the environment, this process counts the
-visible devices (torch.cuda.device_count(), which does not initialise the GPU), refuses with a
+visible devices (dist.visible_gpu_count(): KFD sysfs topology + accessible render nodes, never the HIP
+runtime), refuses with a
 clear error when fewer than N are visible, and otherwise starts torch.distributed.run with N
 ranks on 127.0.0.1 as a CHILD process (no exec, no GPU call in this parent) and exits with its
 code; the ranks run this same file.  Under an external launcher WORLD_SIZE must equal --gpus.
@@ -62,7 +63,7 @@ sys.path.insert(0, ROOT)
 
 from cartpoleplusplus_amd import abi  # noqa: E402
 from cartpoleplusplus_amd.batched import BatchedCartpole  # noqa: E402
-from cartpoleplusplus_amd.dist import gather_returns, return_histogram, shard_spec  # noqa: E402
+from cartpoleplusplus_amd.dist import gather_returns, return_histogram, shard_spec, visible_gpu_count  # noqa: E402
 
 METRIC = "env-steps/sec at batch=65,536, 1→8 MI355X; max |pose−pybullet| over 200 steps"
 HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s spec, 6.29 measured)
@@ -731,16 +732,22 @@ def _free_port():
 def launch_ranks(n, argv, dry_run=False):
     """`--gpus N` without an external launcher: run this file as N ranks under
     torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) in a CHILD process and
-    return its exit code.  Nothing here touches the GPU: torch.cuda.device_count() counts the
-    devices without initialising them, so the ranks own the GPUs from the start (and no
-    process that initialised the GPU ever execs).  Fewer visible devices than N is an error."""
+    return its exit code.  Nothing here touches the GPU: dist.visible_gpu_count() counts the
+    devices from the KFD topology in sysfs and the render nodes this process may open (amdsmi
+    when sysfs has none), never through the HIP runtime, so the ranks own the GPUs from the start
+    and no process that initialised the GPU ever execs.  The parent checks that HIP is still
+    uninitialised right before the spawn and says so on a status line.  Fewer visible devices
+    than N is an error (exit 2)."""
     import subprocess
     if not dry_run:
-        visible = torch.cuda.device_count()
+        visible, source = visible_gpu_count()
+        hip_init = bool(torch.cuda.is_initialized())
+        log(f"bench.py launcher: visible_gpus={visible} source={source} hip_initialized={hip_init}")
         if visible < n:
             log(f"bench.py: --gpus {n} needs {n} visible GPUs, {visible} visible "
                 f"(HIP_VISIBLE_DEVICES={os.environ.get('HIP_VISIBLE_DEVICES')!r}); not launching")
             return 2
+        assert not torch.cuda.is_initialized(), "the launcher parent must not initialise HIP before the spawn"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
     env = dict(os.environ)

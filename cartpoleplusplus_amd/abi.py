@@ -5,7 +5,7 @@ library's entry points with these types.
 """
 import ctypes as C
 
-CP_ABI_VERSION = 5
+CP_ABI_VERSION = 6
 
 CP_BODY_GROUND, CP_BODY_CART, CP_BODY_POLE, CP_BODY_CART2, CP_BODY_POLE2 = range(5)
 CP_NUM_BODIES = 5
@@ -79,6 +79,7 @@ class cp_physics(C.Structure):
         ("friction", C.c_float * CP_NUM_BODIES),
         ("spawn_pos", _F3 * CP_NUM_BODIES),
         ("model_flags", C.c_int32),
+        ("max_coord_velocity", C.c_float),
     ]
 
 

@@ -248,6 +248,7 @@ void cp_default_config(cp_config* c) {
     p->edge_bias = 1e-4f;
     p->max_angular_step = (float)(0.25 * 3.141592653589793);
     p->warmstart = 0.85f;
+    p->max_coord_velocity = 100.0f;   /* btMultiBody m_maxCoordinateVelocity [ext] */
     // models/ground.urdf, cart.urdf, pole.urdf, cart2.urdf, pole2.urdf
     static const double he[5][3] = {{1.5, 1.5, 0.05}, {0.1, 0.1, 0.025}, {0.005, 0.005, 0.25},
                                     {0.1, 0.1, 0.025}, {0.005, 0.005, 0.25}};

@@ -1152,6 +1152,20 @@ CP_DEV Dyn dyn_sel(bool second, const Body& a, const Sym& Ma, const Body& b, con
     return d;
 }
 
+// btMultiBody::applyDeltaVeeMultiDof [ext]: every base velocity coordinate (world angular, then
+// linear) clamped to +-m_maxCoordinateVelocity after each velocity change.  btClamp's
+// compares, not v_med3 / v_min / v_max: a NaN passes through, as in the oracle (clamp_velocities)
+CP_DEV real clamp_coord(real a, real lim) { return a < -lim ? -lim : (lim < a ? lim : a); }
+CP_DEV void clamp_velocities(Sim& S, const cp_physics& P) {
+    const real lim = real(P.max_coord_velocity);
+    if (!(lim > real(0.0))) return;  // uniform (a kernel argument)
+#pragma unroll
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        S.b[d].w = mk(clamp_coord(S.b[d].w.x, lim), clamp_coord(S.b[d].w.y, lim), clamp_coord(S.b[d].w.z, lim));
+        S.b[d].v = mk(clamp_coord(S.b[d].v.x, lim), clamp_coord(S.b[d].v.y, lim), clamp_coord(S.b[d].v.z, lim));
+    }
+}
+
 // whole-env view for the cross rows: positions, velocities and inverse inertias of
 // the own island's bodies from this lane, the other island's from the partner lane
 // (both lanes of a merged env are active wherever this runs).
@@ -2340,6 +2354,7 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
         S.b[d].v = madd(v, acc, dt);
         S.b[d].w = madd(w, accw, dt);
     }
+    clamp_velocities(S, P);  // the unconstrained update goes through applyDeltaVeeMultiDof(output, dt)
     S.f0 = mk(real(0.0), real(0.0), real(0.0));  // 6. external forces are consumed by the step
     S.f2 = mk(real(0.0), real(0.0), real(0.0));
     // 4. solve setup.  No cross-island contact: each lane solves its own island
@@ -2402,6 +2417,7 @@ CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx
         S.b[3].v = lane_of3<1>(I.d2.v);
         S.b[3].w = lane_of3<1>(I.d2.w);
     }
+    clamp_velocities(S, P);  // the solver's write-back goes through applyDeltaVeeMultiDof too
     // refresh the warm-start cache of the lane's island.  A pair with no point before or after
     // the substep holds 0 impulses and keeps them: it is not rewritten (the id word is a 0xFF-padded prefix,
     // the impulses past it 0, in every state the kernels and cp_init write; oracle: every slot

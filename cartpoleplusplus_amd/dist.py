@@ -38,3 +38,66 @@ def gather_returns(returns, group=None):
 def return_histogram(returns, max_len=200):
     """Histogram of integer episode returns (reward 1.0 per step), bins 0..max_len."""
     return torch.bincount(returns.to(torch.int64).clamp(0, max_len), minlength=max_len + 1)
+
+
+def _visible_filter():
+    """The device list a HIP process would see (HIP_VISIBLE_DEVICES, then ROCR_VISIBLE_DEVICES,
+    then CUDA_VISIBLE_DEVICES, as the ROCm runtime reads them): None = no filter."""
+    import os
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return var, [x for x in v.split(",") if x.strip() != ""]
+    return None, None
+
+
+def visible_gpu_count(sysfs="/sys/class/kfd/kfd/topology/nodes", dev_dri="/dev/dri"):
+    """Count the GPUs this process could open WITHOUT initialising the HIP runtime (bench.py's
+    --gpus N launcher runs it in the parent, which must never initialise the GPU before starting
+    the ranks).  Source, in order:
+      1. the KFD topology in sysfs: nodes with a non-zero gfx_target_version (CPU nodes have 0)
+         whose render node /dev/dri/renderD<drm_render_minor> exists and is read/writable by this
+         process (a container lists every GPU of the host in sysfs but maps only its own render
+         nodes);
+      2. amdsmi (the kernel driver's SMI interface, no HIP), when sysfs has no topology;
+    then capped by the length of HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES.
+    Never torch.cuda.device_count(): on ROCm it falls back to hipGetDeviceCount, which initialises
+    the runtime, whenever amdsmi does not answer.  Returns (count, source)."""
+    import os
+    count, source = None, None
+    if os.path.isdir(sysfs):
+        n = 0
+        for node in sorted(os.listdir(sysfs)):
+            props = {}
+            try:
+                with open(os.path.join(sysfs, node, "properties")) as f:
+                    for line in f:
+                        k, _, v = line.strip().partition(" ")
+                        props[k] = v.strip()
+            except OSError:
+                continue
+            if int(props.get("gfx_target_version", "0") or 0) == 0:
+                continue
+            minor = props.get("drm_render_minor")
+            if minor is None:
+                continue
+            path = os.path.join(dev_dri, f"renderD{int(minor)}")
+            if os.path.exists(path) and os.access(path, os.R_OK | os.W_OK):
+                n += 1
+        count, source = n, "kfd-sysfs"
+    else:
+        try:
+            import amdsmi
+            amdsmi.amdsmi_init()
+            try:
+                count = len(amdsmi.amdsmi_get_processor_handles())
+            finally:
+                amdsmi.amdsmi_shut_down()
+            source = "amdsmi"
+        except Exception:   # no driver interface at all: nothing visible
+            count, source = 0, "none"
+    var, lst = _visible_filter()
+    if lst is not None:
+        count = min(count, len(lst))
+        source += f"+{var}"
+    return count, source

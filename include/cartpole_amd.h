@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CP_ABI_VERSION 5
+#define CP_ABI_VERSION 6
 
 /* Bodies, in the reference's loadURDF order (bullet_cartpole.py:154-160). */
 #define CP_BODY_GROUND 0
@@ -106,6 +106,10 @@ typedef struct cp_physics {
     float friction[CP_NUM_BODIES];        /* lateral friction; pair mu = product */
     float spawn_pos[CP_NUM_BODIES][3];    /* bullet_cartpole.py:154-160,319-323  */
     int32_t model_flags;      /* CP_MODEL_* alternatives to the default model (0) */
+    /* btMultiBody::m_maxCoordinateVelocity (100): applyDeltaVeeMultiDof clamps every base
+     * velocity coordinate (world angular x,y,z and linear x,y,z) to +-this after the
+     * unconstrained update and after the solver's write-back [ext]; <= 0: off */
+    float max_coord_velocity;
 } cp_physics;
 
 /* Alternatives to the default contact model (cp_physics.model_flags), for the sensitivity

@@ -344,6 +344,7 @@ void orc_default_config(cp_config* c) {
     p->edge_bias = 1e-4f;
     p->max_angular_step = (float)(0.25 * 3.141592653589793);
     p->warmstart = 0.85f;
+    p->max_coord_velocity = 100.0f;   /* btMultiBody m_maxCoordinateVelocity [ext] */
     /* models/ground.urdf: static box 3 x 3 x 0.1, no <contact> -> default friction 0.5 */
     const double he[5][3] = {{1.5, 1.5, 0.05}, {0.1, 0.1, 0.025}, {0.005, 0.005, 0.25},
                              {0.1, 0.1, 0.025}, {0.005, 0.005, 0.25}};
@@ -906,6 +907,21 @@ static int persistent_manifold(pman_t* M, const box_t* A, const box_t* B, const 
     return M->cnt;
 }
 
+/* btMultiBody::applyDeltaVeeMultiDof [ext]: every base velocity coordinate (world angular
+ * x, y, z, then linear x, y, z) is clamped to +-m_maxCoordinateVelocity whenever a velocity
+ * change is applied to it (btClamp: `if (a < lb) a = lb; else if (ub < a) a = ub;`, so a NaN
+ * passes through).  Bounds the loose pole's yaw spin, whose explicit gyroscopic term otherwise
+ * diverges. */
+static inline real clamp_coord(real a, real lim) { return a < -lim ? -lim : (lim < a ? lim : a); }
+static void clamp_velocities(sim_t* S, const cp_physics* P) {
+    const real lim = (real)P->max_coord_velocity;
+    if (!(lim > RC(0))) return;
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        S->w[d] = mk(clamp_coord(S->w[d].x, lim), clamp_coord(S->w[d].y, lim), clamp_coord(S->w[d].z, lim));
+        S->v[d] = mk(clamp_coord(S->v[d].x, lim), clamp_coord(S->v[d].y, lim), clamp_coord(S->v[d].z, lim));
+    }
+}
+
 /* one p.stepSimulation() of the scene (DESIGN.md §Physics model, steps 1-8) */
 static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* iters_out, int32_t* npts_out,
                     int32_t* isl_iters, int32_t* merged_out) {
@@ -1001,6 +1017,7 @@ static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* i
         S->v[d] = madd(v, acc, dt);
         S->w[d] = madd(w, accw, dt);
     }
+    clamp_velocities(S, P);  /* the unconstrained update goes through applyDeltaVeeMultiDof(output, dt) */
     /* 3b. friction rows (the rows' masses depend on positions only, so setting them up after
      *     the velocity update changes no value of the default model).  Directions: btPlaneSpace1
      *     of the normal; CP_MODEL_VEL_FRICTION: the lateral relative velocity at the point when
@@ -1137,6 +1154,8 @@ static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* i
             S->ws_id[p][j] = idw;
         }
     }
+    /* 4d. the solver's velocity change is written back through applyDeltaVeeMultiDof too */
+    clamp_velocities(S, P);
     /* 5. integrate positions (semi-implicit) and orientation (exponential map) */
     const real hdt = RC(0.5) * dt;
     const real c3 = ((dt * dt) * dt) * RC(0.020833333333);

@@ -240,3 +240,34 @@ def test_one_stop_decision_per_env(oracle_mod):
         joint = _settle(oracle_mod, prec, n=30)
         alone = _settle(oracle_mod, prec, n=30, lift2=True)
         assert all(j >= a for j, a in zip(joint, alone))
+
+
+def _spin(O, prec, lim, omega, steps):
+    cfg = O.default_config()
+    cfg.phys.max_coord_velocity = lim
+    w = O.World(cfg, precision=prec)
+    w.reset_pose(1, (0.0, 0.0, 50.0), (0, 0, 0, 1))        # cart and pole far above the plate: free flight
+    w.reset_pose(2, (0.0, 0.0, 60.0), (0, 0, 0, 1))
+    for k in range(3):
+        w.w.omega[1][k] = omega[k]
+    out = []
+    for _ in range(steps):
+        w.step()
+        out.append(w.velocity(2)[3:].copy())
+    return np.array(out)
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_coordinate_velocity_clamp(oracle_mod, prec):
+    """btMultiBody::applyDeltaVeeMultiDof clamps each base velocity coordinate to +-100
+    (m_maxCoordinateVelocity [ext]).  A pole spinning at 150 rad/s about its own axis
+    in free flight: quadratic damping alone gives 150 - dt 150 k (1 + 150) after one step; the clamp
+    caps it at exactly 100 (the clamp comes after the damping, in the same velocity update).  With a
+    transverse rate added, every coordinate stays within +-100 for 400 steps of free flight."""
+    w1 = _spin(oracle_mod, prec, 100.0, (0.0, 0.0, 150.0), 1)[0]
+    w0 = _spin(oracle_mod, prec, 0.0, (0.0, 0.0, 150.0), 1)[0]
+    dt, k = float(np.float32(DT)), float(np.float32(0.04))
+    assert w1[2] == 100.0 and w1[0] == 0.0 and w1[1] == 0.0
+    assert w0[2] == pytest.approx(150.0 - dt * 150.0 * k * (1.0 + 150.0), rel=1e-5)
+    clamped = _spin(oracle_mod, prec, 100.0, (30.0, 0.0, 150.0), 400)
+    assert np.isfinite(clamped).all() and np.abs(clamped).max() <= 100.0
