@@ -219,6 +219,8 @@ def workload(args, world):
         s += f", kernel shape {args.shape}"
     if getattr(args, "persistent", False):
         s += ", CP_MODEL_PERSISTENT contact model (Bullet's persistent manifold; model-fidelity variant)"
+    if getattr(args, "sleeping", False):
+        s += ", CP_MODEL_SLEEPING (Bullet's deactivation of resting islands; model-fidelity variant)"
     if getattr(args, "rollout", 0):
         s += f", cp_rollout launches of up to {args.rollout} steps (not the per-step cp_step headline)"
     if getattr(args, "autoreset", "same_step") == "next_step":
@@ -810,6 +812,9 @@ def main():
                          "GPU; each env computes what it computes in one handle)")
     ap.add_argument("--shape", choices=("auto", "throughput", "latency"), default="auto",
                     help="kernel shapes (cp_set_kernel_shape) of the step and autoreset kernels")
+    ap.add_argument("--sleeping", action="store_true",
+                    help="the CP_MODEL_SLEEPING model (Bullet's deactivation: resting islands sleep after 2 s; "
+                         "latency-shaped kernels; a model-fidelity variant, not the headline)")
     ap.add_argument("--persistent", action="store_true",
                     help="the CP_MODEL_PERSISTENT contact model (Bullet's persistent manifold; latency-shaped "
                          "kernels; a model-fidelity variant, not the headline)")
@@ -859,7 +864,8 @@ def main():
     env_kw = dict(action_repeats=R, steps_per_repeat=1, max_episode_len=WINDOW, initial_force=55.0,
                   autoreset=args.autoreset, seed=spec["seed"], done_on_bounds=args.done_on_bounds, precision=args.dtype,
                   **({} if args.solver_iterations is None else {"solver_iterations": args.solver_iterations}),
-                  **({"model_flags": abi.CP_MODEL_PERSISTENT} if args.persistent else {}))
+                  **({"model_flags": (abi.CP_MODEL_PERSISTENT if args.persistent else 0)
+                      | (abi.CP_MODEL_SLEEPING if args.sleeping else 0)} if (args.persistent or args.sleeping) else {}))
     if args.streams > 1:
         env = StreamShards(args.streams, B, local, spec["env_id_offset"], **env_kw)
     else:
@@ -1015,13 +1021,14 @@ def main():
         "episode_return_hist_nonzero": None if hist is None else int((hist > 0).sum().item()),
         "done_on_bounds": bool(args.done_on_bounds),
         "nonfinite_envs": int(nf.item()),
-        "nonfinite_note": "envs (over all ranks) whose state went non-finite during the run (cp_nonfinite_counts; the "
-                          "loose-pole yaw-spin divergence of DESIGN.md §3, reproduced by the oracle); they keep "
-                          "stepping and count in value",
+        "nonfinite_note": "envs (over all ranks) whose state went non-finite during the run (cp_nonfinite_counts); 0 "
+                          "since the coordinate-velocity clamp (btMultiBody m_maxCoordinateVelocity, DESIGN.md §3) "
+                          "bounds the loose-pole yaw spin that used to diverge",
     }
     env.close()
     del actions
     headline = not (args.rollout or args.continuous or args.dtype != "f32" or args.done_on_bounds or args.persistent
+                    or args.sleeping
                     or args.streams > 1 or args.raster or next_step or args.shape != "auto"
                     or args.solver_iterations is not None or args.batch != 65536 or args.repeats != 3)
     if rank == 0 and world == 1 and headline and not (args.no_secondary or args.no_cpu_baseline):

@@ -42,7 +42,16 @@ def CP_SF_WS_LAM(isl, j, k):
     return CP_SF_STEPS + 3 + CP_NUM_PAIRS + (isl * CP_ISLAND_PAIRS + j) * 4 + k
 
 
-CP_STATE_FIELDS = CP_SF_STEPS + 3 + CP_NUM_PAIRS * 5
+def CP_SF_SLEEP_ACT(dyn):
+    return CP_SF_STEPS + 3 + CP_NUM_PAIRS * 5 + dyn
+
+
+def CP_SF_SLEEP_TIMER(dyn):
+    return CP_SF_STEPS + 3 + CP_NUM_PAIRS * 5 + CP_NUM_DYN + dyn
+
+
+CP_STATE_FIELDS = CP_SF_STEPS + 3 + CP_NUM_PAIRS * 5 + 2 * CP_NUM_DYN
+CP_ACT_ACTIVE, CP_ACT_SLEEPING, CP_ACT_WANTS, CP_ACT_AWAKE = 1, 2, 3, 16
 
 CP_AUTORESET_OFF, CP_AUTORESET_SAME_STEP, CP_AUTORESET_NEXT_STEP = 0, 1, 2
 
@@ -80,6 +89,8 @@ class cp_physics(C.Structure):
         ("spawn_pos", _F3 * CP_NUM_BODIES),
         ("model_flags", C.c_int32),
         ("max_coord_velocity", C.c_float),
+        ("sleep_epsilon", C.c_float),
+        ("sleep_timeout", C.c_float),
     ]
 
 
@@ -88,7 +99,8 @@ class cp_physics(C.Structure):
 CP_MODEL_SPLIT_ISLANDS = 0x1
 CP_MODEL_VEL_FRICTION = 0x2
 CP_MODEL_PERSISTENT = 0x4
-CP_MODEL_GPU_FLAGS = 0x4
+CP_MODEL_SLEEPING = 0x8
+CP_MODEL_GPU_FLAGS = 0xC
 
 # kernel shapes (cp_set_kernel_shape)
 CP_SHAPE_AUTO = -1

@@ -142,6 +142,22 @@ CP_DEV void store_sim(const Sim& S, const Soa& st, uint32_t o) {
     st.st(CP_SF_PENDING(1, 2), o, S.f2.z);
 }
 
+// CP_MODEL_SLEEPING state of the 4 bodies (SLP kernels only; the other models never touch these fields)
+CP_DEV void load_sleep(Sim& S, const Soa& st, uint32_t o) {
+#pragma unroll
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        S.slp_a[d] = to_bits(st.ld(CP_SF_SLEEP_ACT(d), o));
+        S.slp_t[d] = st.ld(CP_SF_SLEEP_TIMER(d), o);
+    }
+}
+CP_DEV void store_sleep(const Sim& S, const Soa& st, uint32_t o) {
+#pragma unroll
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        st.st(CP_SF_SLEEP_ACT(d), o, bits_to<real>(S.slp_a[d]));
+        st.st(CP_SF_SLEEP_TIMER(d), o, S.slp_t[d]);
+    }
+}
+
 CP_DEV int32_t ldi(const Soa& st, int f, uint32_t o) { return (int32_t)to_bits(st.ld(f, o)); }
 CP_DEV void sti(const Soa& st, int f, uint32_t o, int32_t v) { st.st(f, o, bits_to<real>((uint32_t)v)); }
 
@@ -292,6 +308,8 @@ __global__ void __launch_bounds__(256) cp_init_kernel(cp_config cfg, Bufs b) {
     for (int p = 0; p < CP_NUM_ISLANDS; ++p)
 #pragma unroll
         for (int j = 0; j < CP_ISLAND_PAIRS; ++j) sti(st, CP_SF_WS_ID(p, j), o, -1);
+#pragma unroll
+    for (int d = 0; d < CP_NUM_DYN; ++d) sti(st, CP_SF_SLEEP_ACT(d), o, CP_ACT_ACTIVE | CP_ACT_AWAKE);
     sti(st, CP_SF_DONE, o, 1);  // not reset yet: reference raises, batched API reports done
     b.ret_acc[i] = 0.0f;
     b.last_ret[i] = 0.0f;
@@ -304,7 +322,7 @@ __global__ void __launch_bounds__(256) cp_init_kernel(cp_config cfg, Bufs b) {
 // (fixed-length episodes end together).  LAT = true: one wave per SIMD with 512 registers and
 // fast-form rows, for the short lists of desynchronised episodes (bounds termination), where
 // the 130 serial substeps of one wave are the whole latency of the step.
-template <bool LAT, bool PM = false>
+template <bool LAT, bool PM = false, bool SLP = false>
 __global__ void __launch_bounds__(WAVE)
 __attribute__((amdgpu_waves_per_eu(LAT ? 1 : CP_WAVES_PER_EU, LAT ? 1 : CP_WAVES_PER_EU)))
 cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
@@ -338,6 +356,7 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
         S.b[d].v = mk(real(0.0), real(0.0), real(0.0));
         S.b[d].w = mk(real(0.0), real(0.0), real(0.0));
     }
+    if constexpr (SLP) sleep_wake_all(S);  // the teleported bodies are awake
 #pragma unroll
     for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {  // the lane's island's warm-start cache
         G.sw(CP_SF_WS_ID(0, j), bits_to<real>(0xFFFFFFFFu));
@@ -347,7 +366,7 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     int ov = 0;
     const int nsub = cfg.settle_steps + cfg.initial_force_steps;
     for (int s = 0; s < nsub; ++s) {
-        substep<LAT && !kF64, true, true, PM>(S, cfg.phys, L, pool, pool0, ov, G, ST);
+        substep<LAT && !kF64, true, true, PM, SLP>(S, cfg.phys, L, pool, pool0, ov, G, ST);
         const int k = s - cfg.settle_steps;
         if (k >= 0) {
             real fx, fy;
@@ -365,6 +384,7 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
 #endif
     if (!lead) return;
     store_sim(S, G.st, G.off);
+    if constexpr (SLP) store_sleep(S, G.st, G.off);
     b.overflow[i] += ov;
     if (!sim_finite(S)) b.nonfinite[i] += 1;
     float row[14];
@@ -384,7 +404,7 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
 
 // LAT: the latency shape of cp_reset_kernel<true> (1 wave per SIMD, 512 registers, fast-form
 // rows) for batches whose waves all get a SIMD of their own (<= 32,768 envs)
-template <int KIND, bool LQR, bool LAT, bool PM = false>
+template <int KIND, bool LQR, bool LAT, bool PM = false, bool SLP = false>
 __global__ void __launch_bounds__(WAVE)
 __attribute__((amdgpu_waves_per_eu(LAT ? 1 : CP_WAVES_PER_EU, LAT ? 1 : CP_WAVES_PER_EU)))
 cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float* reward_out, uint8_t* done_out,
@@ -438,6 +458,7 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
             const real f00 = a00 * F, f01 = a01 * F, f10 = a10 * F, f11 = a11 * F;
             Sim S;
             load_sim(S, G.st, G.off);
+            if constexpr (SLP) load_sleep(S, G.st, G.off);
             int ov = 0;
             real u[2][2] = {{real(0.0), real(0.0)}, {real(0.0), real(0.0)}};  // LQR forces from the last observed state
             bool lqr_done = false;
@@ -448,8 +469,8 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
             }
             for (int r = 0; r < R; ++r) {
                 for (int s = 0; s < SR; ++s) {
-                    substep<LAT && !kF64, kC44Step && !LAT && !kF64 && !PM, kAllinStep, PM>(S, cfg.phys, L, pool, pool0,
-                                                                                              ov, G, ST);
+                    substep<LAT && !kF64, kC44Step && !LAT && !kF64 && !PM, kAllinStep, PM, SLP>(S, cfg.phys, L, pool,
+                                                                                                   pool0, ov, G, ST);
                     if constexpr (LQR) {  // disturbance + control (:897-901), control from the pre-step state
                         apply_force_link<0>(S, f00 + u[0][0], f01 + u[0][1]);
                         apply_force_link<1>(S, f10 + u[1][0], f11 + u[1][1]);
@@ -483,6 +504,7 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
             if (LQR && lqr_done) done = true;
             if (lead) {
                 store_sim(S, G.st, G.off);
+                if constexpr (SLP) store_sleep(S, G.st, G.off);
                 if (!sim_finite(S)) b.nonfinite[i] += 1;
                 sti(G.st, CP_SF_STEPS, G.off, steps);
                 put_out(&reward_out[i], 1.0f);  // bullet_cartpole.py:260
@@ -571,7 +593,7 @@ enum : uint32_t { RF_DONE = 1u, RF_RESETTING = 2u, RF_LAST_SIM = 4u, RF_LQR_DONE
 static_assert(RC_END - RC_K == CP_SCR_RC_FIELDS, "rollout state rows of the scratch SoA (cp_common.h)");
 static_assert(RC_K >= CP_SCR_HDR_FIELDS, "rollout state must not overlap the CP_HDR_SCRATCH manifold headers");
 
-template <int KIND, bool LQR, bool LAT, bool PM = false>
+template <int KIND, bool LQR, bool LAT, bool PM = false, bool SLP = false>
 __global__ void __launch_bounds__(WAVE)
 __attribute__((amdgpu_waves_per_eu(LAT ? 1 : CP_WAVES_PER_EU, LAT ? 1 : CP_WAVES_PER_EU)))
 cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_out, float* reward_out,
@@ -599,6 +621,7 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
     Stamps ST;
     Sim S;
     load_sim(S, G.st, G.off);
+    if constexpr (SLP) load_sleep(S, G.st, G.off);
     int ov = 0;
     real u[2][2];
     // the next simulated step from k on: steps of an env that is done before them only return its
@@ -631,7 +654,7 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
                            ldi(G.st, CP_SF_DONE, G.off) != 0 ? RF_DONE : 0u, b.ret_acc[i]);
     while (__ballot(work) != 0ull) {
         if (!work) continue;
-        substep<LAT && !kF64, false, kAllinStep, PM>(S, cfg.phys, L, pool, pool0, ov, G, ST);
+        substep<LAT && !kF64, false, kAllinStep, PM, SLP>(S, cfg.phys, L, pool, pool0, ov, G, ST);
         int k = ldc(RC_K), sub = ldc(RC_SUB);
         uint32_t flags = (uint32_t)ldc(RC_FLAGS);
         if (!(flags & RF_RESETTING)) {
@@ -696,6 +719,7 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
                         S.b[d].v = mk(real(0.0), real(0.0), real(0.0));
                         S.b[d].w = mk(real(0.0), real(0.0), real(0.0));
                     }
+                    if constexpr (SLP) sleep_wake_all(S);
 #pragma unroll
                     for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
                         G.sw(CP_SF_WS_ID(0, j), bits_to<real>(0xFFFFFFFFu));
@@ -743,6 +767,7 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
     if (!lead) return;
     const uint32_t flags = (uint32_t)ldc(RC_FLAGS);
     store_sim(S, G.st, G.off);
+    if constexpr (SLP) store_sleep(S, G.st, G.off);
     sti(G.st, CP_SF_STEPS, G.off, ldc(RC_STEPS));
     sti(G.st, CP_SF_EPISODE, G.off, ldc(RC_EPISODE));
     sti(G.st, CP_SF_DONE, G.off, (flags & RF_DONE) ? 1 : 0);
@@ -825,6 +850,10 @@ void launch_reset(bool lat, const cp_config& cfg, const Bufs& b, float* obs_out,
         hipLaunchKernelGGL((cp_reset_kernel<true, true>), grid, block, 0, st, cfg, b, obs_out);
         return;
     }
+    if (cfg.phys.model_flags & CP_MODEL_SLEEPING) {  // the sleeping model: latency shape only
+        hipLaunchKernelGGL((cp_reset_kernel<true, false, true>), grid, block, 0, st, cfg, b, obs_out);
+        return;
+    }
     if constexpr (kF64) {
         (void)lat;
         hipLaunchKernelGGL(cp_reset_kernel<true>, grid, block, 0, st, cfg, b, obs_out);
@@ -843,6 +872,13 @@ static void launch_step_t(bool lat, const cp_config& cfg, const Bufs& b, const v
         hipLaunchKernelGGL((cp_step_kernel<K, Q, true, true>), grid, block, 0, st, cfg, b, actions, obs_out,
                            reward_out, done_out, term_out, readback, rb_bug, lq);
         return;
+    }
+    if constexpr (!Q) {  // the sleeping model: latency shape only, no LQR policy (cp_set_lqr rejects it)
+        if (cfg.phys.model_flags & CP_MODEL_SLEEPING) {
+            hipLaunchKernelGGL((cp_step_kernel<K, false, true, false, true>), grid, block, 0, st, cfg, b, actions,
+                               obs_out, reward_out, done_out, term_out, readback, rb_bug, lq);
+            return;
+        }
     }
     if constexpr (kF64) {
         (void)lat;
@@ -863,6 +899,13 @@ static void launch_rollout_t(bool lat, const cp_config& cfg, const Bufs& b, int 
                              float* obs_out, float* reward_out, uint8_t* done_out, float* term_out, const Lqr& lq,
                              hipStream_t st) {
     const dim3 grid(env_grid(2 * cfg.num_envs, WAVE)), block(WAVE);  // two lanes per env
+    if constexpr (!Q) {
+        if (cfg.phys.model_flags & CP_MODEL_SLEEPING) {
+            hipLaunchKernelGGL((cp_rollout_kernel<K, false, true, false, true>), grid, block, 0, st, cfg, b, steps,
+                               actions, obs_out, reward_out, done_out, term_out, lq);
+            return;
+        }
+    }
     if (cfg.phys.model_flags & CP_MODEL_PERSISTENT)
         hipLaunchKernelGGL((cp_rollout_kernel<K, Q, true, true>), grid, block, 0, st, cfg, b, steps, actions, obs_out,
                            reward_out, done_out, term_out, lq);

@@ -249,6 +249,8 @@ void cp_default_config(cp_config* c) {
     p->max_angular_step = (float)(0.25 * 3.141592653589793);
     p->warmstart = 0.85f;
     p->max_coord_velocity = 100.0f;   /* btMultiBody m_maxCoordinateVelocity [ext] */
+    p->sleep_epsilon = 0.05f;         /* btMultiBody SLEEP_EPSILON [ext] (CP_MODEL_SLEEPING) */
+    p->sleep_timeout = 2.0f;          /* btMultiBody SLEEP_TIMEOUT [ext] */
     // models/ground.urdf, cart.urdf, pole.urdf, cart2.urdf, pole2.urdf
     static const double he[5][3] = {{1.5, 1.5, 0.05}, {0.1, 0.1, 0.025}, {0.005, 0.005, 0.25},
                                     {0.1, 0.1, 0.025}, {0.005, 0.005, 0.25}};
@@ -301,6 +303,8 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     if (cfg->phys.model_flags & ~CP_MODEL_GPU_FLAGS)
         return fail(nullptr, "cp_create: phys.model_flags names a model alternative the HIP kernels do not "
                              "implement (oracle-only, DESIGN.md §3)");
+    if ((cfg->phys.model_flags & CP_MODEL_PERSISTENT) && (cfg->phys.model_flags & CP_MODEL_SLEEPING))
+        return fail(nullptr, "cp_create: CP_MODEL_PERSISTENT and CP_MODEL_SLEEPING together are oracle-only");
     if (!(cfg->phys.residual_threshold >= 0.0f)) return fail(nullptr, "cp_create: negative residual_threshold");
     if (cfg->autoreset != CP_AUTORESET_OFF && cfg->autoreset != CP_AUTORESET_SAME_STEP &&
         cfg->autoreset != CP_AUTORESET_NEXT_STEP)
@@ -501,7 +505,8 @@ static void choose_reset_shape(cp_handle* h) {
     if (h->reset_req != CP_SHAPE_AUTO) h->reset_lat = h->reset_req == CP_SHAPE_LATENCY;
     if (h->step_req != CP_SHAPE_AUTO) h->step_lat = h->step_req == CP_SHAPE_LATENCY;
     if (h->f64) h->reset_lat = h->step_lat = 1;  // fp64: the 512-register shape only
-    if (h->cfg.phys.model_flags & CP_MODEL_PERSISTENT) h->reset_lat = h->step_lat = 1;  // PM: latency shape only
+    if (h->cfg.phys.model_flags & (CP_MODEL_PERSISTENT | CP_MODEL_SLEEPING))
+        h->reset_lat = h->step_lat = 1;  // PM, SLEEPING: latency shape only
 }
 
 static int launch_reset_list(cp_handle* h, const cpc::Bufs& b, float* obs_out, hipStream_t st) {
@@ -662,6 +667,8 @@ int cp_set_lqr(cp_handle* h, const float* gains, int per_env, float* state8_out,
                float done_angle) {
     if (!h) return fail(h, "cp_set_lqr: null handle");
     if (!gains && state8_out) return fail(h, "cp_set_lqr: the 8-state readback needs the LQR policy on");
+    if (gains && (h->cfg.phys.model_flags & CP_MODEL_SLEEPING))
+        return fail(h, "cp_set_lqr: the LQR policy is not built for CP_MODEL_SLEEPING handles (oracle-only)");
     h->lqr.gains = gains;
     h->lqr.per_env = per_env ? 1 : 0;
     h->lqr.state8 = state8_out;
@@ -690,9 +697,10 @@ int cp_set_kernel_shape(cp_handle* h, int step_shape, int reset_shape) {
     auto ok = [](int v) { return v == CP_SHAPE_AUTO || v == CP_SHAPE_THROUGHPUT || v == CP_SHAPE_LATENCY; };
     if (!ok(step_shape) || !ok(reset_shape))
         return fail(h, "cp_set_kernel_shape: shapes must be CP_SHAPE_AUTO, CP_SHAPE_THROUGHPUT or CP_SHAPE_LATENCY");
-    if ((h->f64 || (h->cfg.phys.model_flags & CP_MODEL_PERSISTENT)) &&
+    if ((h->f64 || (h->cfg.phys.model_flags & (CP_MODEL_PERSISTENT | CP_MODEL_SLEEPING))) &&
         (step_shape == CP_SHAPE_THROUGHPUT || reset_shape == CP_SHAPE_THROUGHPUT))
-        return fail(h, "cp_set_kernel_shape: fp64 and persistent-manifold handles have the latency shape only");
+        return fail(h, "cp_set_kernel_shape: fp64, persistent-manifold and sleeping-model handles have the latency "
+                       "shape only");
     h->step_req = step_shape;
     h->reset_req = reset_shape;
     choose_reset_shape(h);

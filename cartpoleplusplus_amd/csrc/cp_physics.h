@@ -72,6 +72,8 @@ struct Body {
 struct Sim {
     Body b[CP_NUM_DYN];   // cart, pole, cart2, pole2
     V3 f0, f2;            // pending world force on cart / cart2 (pybullet force accumulator)
+    uint32_t slp_a[CP_NUM_DYN];  // CP_MODEL_SLEEPING (SLP kernels only): activation word (CP_ACT_* | CP_ACT_AWAKE)
+    real slp_t[CP_NUM_DYN];      //   and sleep timer per body
 };
 
 // Per-env global memory touched once per substep (cold data kept out of VGPRs):
@@ -1166,6 +1168,88 @@ CP_DEV void clamp_velocities(Sim& S, const cp_physics& P) {
     }
 }
 
+// ---- CP_MODEL_SLEEPING (the SLP kernels): Bullet's deactivation, operation for operation the oracle's
+// body_aabb / sleep_islands / sleep_update (oracle/cp_oracle.c).  Both lanes of an env run
+// them on the whole env, like the velocity update, so they agree without a DPP exchange.
+// AABB of dynamic body D: btTransformAabb of the box grown by the contact breaking threshold
+template <int D>
+CP_DEV void body_aabb(const Sim& S, const cp_physics& P, V3& lo, V3& hi) {
+    const Axes A = quat_axes(S.b[D].q[0], S.b[D].q[1], S.b[D].q[2], S.b[D].q[3]);
+    const real h0 = P.half_extents[D + 1][0], h1 = P.half_extents[D + 1][1], h2 = P.half_extents[D + 1][2];
+    const real thr = P.contact_margin;
+    const real ex = (h0 * abs_(A.a0.x) + h1 * abs_(A.a1.x)) + h2 * abs_(A.a2.x);
+    const real ey = (h0 * abs_(A.a0.y) + h1 * abs_(A.a1.y)) + h2 * abs_(A.a2.y);
+    const real ez = (h0 * abs_(A.a0.z) + h1 * abs_(A.a1.z)) + h2 * abs_(A.a2.z);
+    const V3 c = S.b[D].x;
+    lo = mk((c.x - ex) - thr, (c.y - ey) - thr, (c.z - ez) - thr);
+    hi = mk((c.x + ex) + thr, (c.y + ey) + thr, (c.z + ez) + thr);
+}
+CP_DEV bool aabb_overlap(const V3& la, const V3& ha, const V3& lb, const V3& hb) {
+    return !(la.x > hb.x || ha.x < lb.x || la.y > hb.y || ha.y < lb.y || la.z > hb.z || ha.z < lb.z);
+}
+// the start of a step: islands of AABB-overlapping bodies and btSimulationIslandManager::buildIslands'
+// activation pass; returns the mask of bodies that sleep this step (bit d = dynamic body d)
+CP_DEV uint32_t sleep_islands(Sim& S, const cp_physics& P) {
+    V3 lo[CP_NUM_DYN], hi[CP_NUM_DYN];
+    body_aabb<0>(S, P, lo[0], hi[0]);
+    body_aabb<1>(S, P, lo[1], hi[1]);
+    body_aabb<2>(S, P, lo[2], hi[2]);
+    body_aabb<3>(S, P, lo[3], hi[3]);
+    int root[CP_NUM_DYN] = {0, 1, 2, 3};
+#pragma unroll
+    for (int a = 0; a < CP_NUM_DYN; ++a)
+#pragma unroll
+        for (int b = a + 1; b < CP_NUM_DYN; ++b) {
+            const bool ov = aabb_overlap(lo[a], hi[a], lo[b], hi[b]);
+            const int ra = root[a], rb = root[b];
+            const int lr = ra < rb ? ra : rb, hr = ra < rb ? rb : ra;
+#pragma unroll
+            for (int d = 0; d < CP_NUM_DYN; ++d) root[d] = (ov && root[d] == hr) ? lr : root[d];
+        }
+    uint32_t mask = 0u;
+#pragma unroll
+    for (int r = 0; r < CP_NUM_DYN; ++r) {
+        bool any_active = false;
+#pragma unroll
+        for (int d = 0; d < CP_NUM_DYN; ++d) any_active |= root[d] == r && (S.slp_a[d] & 15u) == CP_ACT_ACTIVE;
+#pragma unroll
+        for (int d = 0; d < CP_NUM_DYN; ++d) {
+            const uint32_t aw = S.slp_a[d] & (uint32_t)CP_ACT_AWAKE;
+            const bool mine = root[d] == r;
+            const uint32_t na = !any_active ? ((uint32_t)CP_ACT_SLEEPING | aw)
+                              : ((S.slp_a[d] & 15u) == CP_ACT_SLEEPING ? ((uint32_t)CP_ACT_WANTS | aw) : S.slp_a[d]);
+            S.slp_a[d] = mine ? na : S.slp_a[d];
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < CP_NUM_DYN; ++d) mask |= ((S.slp_a[d] & 15u) == CP_ACT_SLEEPING ? 1u : 0u) << d;
+    return mask;
+}
+// the end of a step: btMultiBody::checkMotionAndSleepIfRequired + updateActivationState
+CP_DEV void sleep_update(Sim& S, const cp_physics& P) {
+    const real dt = P.dt, eps = P.sleep_epsilon, tmo = P.sleep_timeout;
+#pragma unroll
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        const V3 w = S.b[d].w, v = S.b[d].v;
+        const real motion = ((((w.x * w.x + w.y * w.y) + w.z * w.z) + v.x * v.x) + v.y * v.y) + v.z * v.z;
+        uint32_t a = S.slp_a[d];
+        const bool still = motion < eps;
+        const real t = still ? S.slp_t[d] + dt : real(0.0);
+        S.slp_t[d] = t;
+        a = still ? (t > tmo ? (a & ~(uint32_t)CP_ACT_AWAKE) : a) : (a | (uint32_t)CP_ACT_AWAKE);
+        a = (a & (uint32_t)CP_ACT_AWAKE) ? ((uint32_t)CP_ACT_ACTIVE | (uint32_t)CP_ACT_AWAKE)
+            : ((a & 15u) == CP_ACT_ACTIVE ? (uint32_t)CP_ACT_WANTS : a);
+        S.slp_a[d] = a;
+    }
+}
+CP_DEV void sleep_wake_all(Sim& S) {  // resetBasePositionAndOrientation [ext, low confidence]
+#pragma unroll
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        S.slp_a[d] = (uint32_t)CP_ACT_ACTIVE | (uint32_t)CP_ACT_AWAKE;
+        S.slp_t[d] = real(0.0);
+    }
+}
+
 // whole-env view for the cross rows: positions, velocities and inverse inertias of
 // the own island's bodies from this lane, the other island's from the partner lane
 // (both lanes of a merged env are active wherever this runs).
@@ -1225,6 +1309,7 @@ struct Ctx {
     bool merged, active;
     bool xfric;      // merged, and a cross pair of the env has friction rows (only pole-pole contacts do:
                      // the carts' friction is 0); else the friction half of the cross block is a no-op
+    uint32_t slp;    // CP_MODEL_SLEEPING: the bodies that sleep this step (bit d = dynamic body d); else 0
 };
 
 // One PGS sweep range [it0, it1) over the lane's island (+ the cross rows of a merged
@@ -2139,7 +2224,7 @@ CP_DEV void pm_refresh(PMan& M, const Box& A, const Box& B, real thr) {
 // row setup of the lane's island, unconstrained velocity update of the whole env,
 // the island view and the warm start.  A lane with live == false (done env, padding)
 // makes no contacts and writes nothing.
-template <bool ALLIN = false, bool PM = false>
+template <bool ALLIN = false, bool PM = false, bool SLP = false>
 CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool, real* pool0, int& overflow,
                          const Mem& G, Stamps& ST, bool live, Ctx& c) {
     const real dt = P.dt, inv_dt = P.inv_dt;
@@ -2154,6 +2239,13 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
         constexpr bool GROUND = decltype(ground_tag)::value;
         const int g = island_pair(L.isl, j);
         const int a = GROUND ? 0 : pair_a(g);
+        // CP_MODEL_SLEEPING: a pair with a sleeping body (a sleeping island) makes no contact and keeps its
+        // warm-start cache (oracle: skip[p][j])
+        bool plive = live;
+        if constexpr (SLP) {
+            const int bb = pair_b(g);
+            plive = live && !(((c.slp >> (bb - 1)) & 1u) || (a > 0 && ((c.slp >> (a - 1)) & 1u)));
+        }
         CP_STAMP(n0);
         // warm-start cache of the pair, loaded first: its latency overlaps the narrowphase
         uint32_t oid = 0xFFFFFFFFu;
@@ -2193,7 +2285,7 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
         // PM: Bullet's box-box detector reports overlapping boxes only (margin 0); the manifold keeps
         // the points within the pair's relative breaking threshold
         const real newmargin = PM ? real(0.0) : real(P.contact_margin);
-        if (live && !face_separated(A, Bx, newmargin)) box_box<ALLIN>(A, Bx, newmargin, P.edge_bias, C);
+        if (plive && !face_separated(A, Bx, newmargin)) box_box<ALLIN>(A, Bx, newmargin, P.edge_bias, C);
         PMan M;
         M.cnt = 0;
         if constexpr (PM) {
@@ -2294,7 +2386,7 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
         const int om = (oid & 0xFFu) == 0xFFu ? 0 : ((oid >> 8) & 0xFFu) == 0xFFu ? 1
                      : ((oid >> 16) & 0xFFu) == 0xFFu ? 2 : ((oid >> 24) & 0xFFu) == 0xFFu ? 3 : 4;
         const uint32_t pk = (uint32_t)m | ((uint32_t)base << 3) | ((uint32_t)fm << 8) | ((uint32_t)fbase << 11) |
-                            ((uint32_t)(m > om ? m : om) << 16);
+                            ((uint32_t)(plive ? (m > om ? m : om) : 0) << 16);
 #ifdef CP_HDR_SCRATCH
         G.sx(4 * j + 0, C.n.x);
         G.sx(4 * j + 1, C.n.y);
@@ -2310,7 +2402,7 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
             T.pk[q] = h ? pk : T.pk[q];
         }
 #endif
-        if (!PM && live && nid != oid) G.sw(CP_SF_WS_ID(0, j), bits_to<real>(nid));  // unchanged: no write
+        if (!PM && plive && nid != oid) G.sw(CP_SF_WS_ID(0, j), bits_to<real>(nid));  // unchanged: no write
     };
 #ifdef CP_NO_GROUND_PEEL
 #pragma unroll 1
@@ -2351,8 +2443,14 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
         real wlen = sqrt_(dot(w, w));
         real dw = fma_(ka, wlen, ka);
         V3 accw = mk(fma_(-w.x, dw, aw.x), fma_(-w.y, dw, aw.y), fma_(-w.z, dw, aw.z));
-        S.b[d].v = madd(v, acc, dt);
-        S.b[d].w = madd(w, accw, dt);
+        if constexpr (SLP) {  // CP_MODEL_SLEEPING: no gravity, forces or damping for a sleeping body
+            const bool sd = ((c.slp >> d) & 1u) != 0u;
+            S.b[d].v = selv(sd, v, madd(v, acc, dt));
+            S.b[d].w = selv(sd, w, madd(w, accw, dt));
+        } else {
+            S.b[d].v = madd(v, acc, dt);
+            S.b[d].w = madd(w, accw, dt);
+        }
     }
     clamp_velocities(S, P);  // the unconstrained update goes through applyDeltaVeeMultiDof(output, dt)
     S.f0 = mk(real(0.0), real(0.0), real(0.0));  // 6. external forces are consumed by the step
@@ -2400,7 +2498,7 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
 // Phase 3: whole-env velocities from the two lanes' islands (both lanes of every
 // env active), the warm-start cache refresh and the integration (DESIGN.md
 // §Physics model 5b-7).
-template <bool PM = false>
+template <bool PM = false, bool SLP = false>
 CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx& c, real* pool, const Mem& G,
                            Stamps& ST, bool live) {
     const real dt = P.dt, inv_dt = P.inv_dt;
@@ -2449,7 +2547,8 @@ CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx
 #pragma unroll
     for (int d = 0; d < CP_NUM_DYN; ++d) {
         V3 v = S.b[d].v, w = S.b[d].w;
-        S.b[d].x = madd(S.b[d].x, v, dt);
+        const V3 x0 = S.b[d].x;
+        S.b[d].x = madd(x0, v, dt);
         real ang = sqrt_(dot(w, w));
         if (ang * dt > maxang) ang = maxang * inv_dt;
         real half = hdt * ang;
@@ -2465,11 +2564,24 @@ CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx
         real rz = fma_(dw, qz, fma_(dz, qw, fma_(dx, qy, -(dy * qx))));
         real n2 = fma_(rx, rx, fma_(ry, ry, fma_(rz, rz, rw * rw)));
         real inv = real(1.0) / sqrt_(n2);
-        S.b[d].q[0] = rx * inv;
-        S.b[d].q[1] = ry * inv;
-        S.b[d].q[2] = rz * inv;
-        S.b[d].q[3] = rw * inv;
+        if constexpr (SLP) {  // btMultiBodyDynamicsWorld::integrateTransforms: a sleeping body keeps its pose,
+            const bool sd = ((c.slp >> d) & 1u) != 0u;  // its velocities are cleared
+            const V3 z = mk(real(0.0), real(0.0), real(0.0));
+            S.b[d].x = selv(sd, x0, S.b[d].x);
+            S.b[d].v = selv(sd, z, v);
+            S.b[d].w = selv(sd, z, w);
+            S.b[d].q[0] = sd ? qx : rx * inv;
+            S.b[d].q[1] = sd ? qy : ry * inv;
+            S.b[d].q[2] = sd ? qz : rz * inv;
+            S.b[d].q[3] = sd ? qw : rw * inv;
+        } else {
+            S.b[d].q[0] = rx * inv;
+            S.b[d].q[1] = ry * inv;
+            S.b[d].q[2] = rz * inv;
+            S.b[d].q[3] = rw * inv;
+        }
     }
+    if constexpr (SLP) sleep_update(S, P);  // updateActivationState, after the integration
     CP_STAMP(t4);
 #ifndef CP_STAMP_C44
     CP_ACC(integ, t3, t4);
@@ -2485,16 +2597,19 @@ CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx
 // C44: the latency-shaped reset kernel's options: the guard-free settle-structure loop
 // (sweeps_c44) and the all-inside face-contact exit (face_contact<ALLIN>).
 // PM: CP_MODEL_PERSISTENT (Bullet's persistent manifold, per-row normals in the pool).
-template <bool FAST = false, bool C44 = false, bool ALLIN = C44, bool PM = false>
+// SLP: CP_MODEL_SLEEPING (Bullet's deactivation: sleeping islands are neither integrated nor solved).
+template <bool FAST = false, bool C44 = false, bool ALLIN = C44, bool PM = false, bool SLP = false>
 CP_DEV void substep(Sim& S, const cp_physics& P, const Lane& L, real* pool, real* pool0, int& overflow,
                     const Mem& G, Stamps& ST, bool live = true) {
     Ctx c;
-    substep_prep<ALLIN, PM>(S, P, L, pool, pool0, overflow, G, ST, live, c);
+    c.slp = 0u;
+    if constexpr (SLP) c.slp = sleep_islands(S, P);
+    substep_prep<ALLIN, PM, SLP>(S, P, L, pool, pool0, overflow, G, ST, live, c);
     CP_STAMP(t2);
     solve_range<FAST, C44, PM>(c, S, P, pool, pool0, L.isl != 0, 0, P.solver_iterations, ST);
     CP_STAMP(t3);
     CP_ACC(solve, t2, t3);
-    substep_finish<PM>(S, P, L, c, pool, G, ST, live);
+    substep_finish<PM, SLP>(S, P, L, c, pool, G, ST, live);
 }
 
 // LINK_FRAME force at the COM on cart (C = 0) or cart2 (C = 1): world = R(q) f

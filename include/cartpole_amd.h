@@ -71,7 +71,17 @@ extern "C" {
  * slot), and the 4 accumulated normal impulses of the last substep */
 #define CP_SF_WS_ID(isl, j)      (CP_SF_STEPS + 3 + (isl) * CP_ISLAND_PAIRS + (j))
 #define CP_SF_WS_LAM(isl, j, k)  (CP_SF_STEPS + 3 + CP_NUM_PAIRS + ((isl) * CP_ISLAND_PAIRS + (j)) * 4 + (k))
-#define CP_STATE_FIELDS (CP_SF_STEPS + 3 + CP_NUM_PAIRS * 5)
+/* CP_MODEL_SLEEPING state per dynamic body (untouched by the other models): the activation word
+ * (int bits: CP_ACT_* | CP_ACT_AWAKE) and the sleep timer (seconds) */
+#define CP_SF_SLEEP_ACT(dyn)    (CP_SF_STEPS + 3 + CP_NUM_PAIRS * 5 + (dyn))
+#define CP_SF_SLEEP_TIMER(dyn)  (CP_SF_STEPS + 3 + CP_NUM_PAIRS * 5 + CP_NUM_DYN + (dyn))
+#define CP_STATE_FIELDS (CP_SF_STEPS + 3 + CP_NUM_PAIRS * 5 + 2 * CP_NUM_DYN)
+/* activation states (btCollisionObject.h: ACTIVE_TAG 1, ISLAND_SLEEPING 2, WANTS_DEACTIVATION 3) and
+ * btMultiBody::m_awake as bit 4 */
+#define CP_ACT_ACTIVE   1
+#define CP_ACT_SLEEPING 2
+#define CP_ACT_WANTS    3
+#define CP_ACT_AWAKE    16
 
 /* Contact pools per island (LDS-resident in the kernel; same caps in the oracle). */
 #define CP_ISLAND_POINTS   10     /* normal-contact rows per island per substep */
@@ -110,6 +120,11 @@ typedef struct cp_physics {
      * velocity coordinate (world angular x,y,z and linear x,y,z) to +-this after the
      * unconstrained update and after the solver's write-back [ext]; <= 0: off */
     float max_coord_velocity;
+    /* CP_MODEL_SLEEPING only: btMultiBody::checkMotionAndSleepIfRequired's constants [ext] -- a
+     * body whose motion |w|^2 + |v|^2 stays below sleep_epsilon (0.05, a squared velocity) for more
+     * than sleep_timeout (2 s) stops being awake; an island of bodies none of which is awake sleeps */
+    float sleep_epsilon;
+    float sleep_timeout;
 } cp_physics;
 
 /* Alternatives to the default contact model (cp_physics.model_flags), for the sensitivity
@@ -122,8 +137,15 @@ typedef struct cp_physics {
 #define CP_MODEL_PERSISTENT      0x4  /* Bullet's persistent manifold (getCacheEntry matching,
                                          replaceContactPoint, sortCachedPoints,
                                          refreshContactPoints) instead of feature-id matching   */
-#define CP_MODEL_GPU_FLAGS       0x4  /* the flags the HIP kernels implement (PERSISTENT: latency-shaped
-                                         kernels only; its manifolds are not part of the state SoA) */
+#define CP_MODEL_SLEEPING        0x8  /* Bullet's deactivation (sleeping) of resting bodies, on when pybullet
+                                         loads a URDF with URDF_ENABLE_SLEEPING (off by default in pybullet
+                                         since that flag exists; bullet_cartpole.py:154-160 passes no flags):
+                                         per body a sleep timer and an activation state in the state SoA
+                                         (CP_SF_SLEEP_*), islands from the bodies' contact-threshold AABBs,
+                                         a sleeping island is neither integrated nor solved */
+#define CP_MODEL_GPU_FLAGS       0xC  /* the flags the HIP kernels implement (PERSISTENT, SLEEPING: latency-
+                                         shaped kernels only, not together, no LQR policy; the persistent
+                                         manifolds are not part of the state SoA) */
 
 typedef struct cp_config {
     int32_t num_envs;            /* B                                          */

@@ -345,6 +345,8 @@ void orc_default_config(cp_config* c) {
     p->max_angular_step = (float)(0.25 * 3.141592653589793);
     p->warmstart = 0.85f;
     p->max_coord_velocity = 100.0f;   /* btMultiBody m_maxCoordinateVelocity [ext] */
+    p->sleep_epsilon = 0.05f;         /* btMultiBody SLEEP_EPSILON [ext] (CP_MODEL_SLEEPING) */
+    p->sleep_timeout = 2.0f;          /* btMultiBody SLEEP_TIMEOUT [ext] */
     /* models/ground.urdf: static box 3 x 3 x 0.1, no <contact> -> default friction 0.5 */
     const double he[5][3] = {{1.5, 1.5, 0.05}, {0.1, 0.1, 0.025}, {0.005, 0.005, 0.25},
                              {0.1, 0.1, 0.025}, {0.005, 0.005, 0.25}};
@@ -395,6 +397,8 @@ typedef struct {
     uint32_t ws_id[CP_NUM_ISLANDS][CP_ISLAND_PAIRS];   /* warm-start cache (4 packed feature ids) */
     real ws_lam[CP_NUM_ISLANDS][CP_ISLAND_PAIRS][4];
     pman_t pm[CP_NUM_ISLANDS][CP_ISLAND_PAIRS];        /* CP_MODEL_PERSISTENT only */
+    int32_t slp_a[CP_NUM_DYN];  /* CP_MODEL_SLEEPING: activation word (CP_ACT_* | CP_ACT_AWAKE) */
+    real slp_t[CP_NUM_DYN];     /*                    btMultiBody::m_sleepTimer */
 } sim_t;
 
 typedef struct { v3 n; int cnt, base, fcnt, fbase; real mu; } manifold_t;
@@ -922,6 +926,80 @@ static void clamp_velocities(sim_t* S, const cp_physics* P) {
     }
 }
 
+/* ---- CP_MODEL_SLEEPING: Bullet's deactivation, restated [ext].
+ * Islands: btSimulationIslandManager::findUnions unites the non-static bodies of every broadphase
+ * pair, i.e. every pair whose AABBs overlap; an AABB is btTransformAabb of the box (world extent
+ * along axis k = sum_c |R_kc| h_c) grown by gContactBreakingThreshold (btCollisionWorld::
+ * updateSingleAabb; here contact_margin, 0.02 m).  The static ground joins nothing. */
+static void body_aabb(const sim_t* S, const cp_physics* P, int d, v3* lo, v3* hi) {
+    const float* h = P->half_extents[d + 1];
+    const v3* ax = S->ax[d];   /* ax[c] = world coordinates of local axis c: R_kc = ax[c].k */
+    const real thr = (real)P->contact_margin;
+    const real ex = ((real)h[0] * FABS(ax[0].x) + (real)h[1] * FABS(ax[1].x)) + (real)h[2] * FABS(ax[2].x);
+    const real ey = ((real)h[0] * FABS(ax[0].y) + (real)h[1] * FABS(ax[1].y)) + (real)h[2] * FABS(ax[2].y);
+    const real ez = ((real)h[0] * FABS(ax[0].z) + (real)h[1] * FABS(ax[1].z)) + (real)h[2] * FABS(ax[2].z);
+    const v3 c = S->x[d];
+    *lo = mk((c.x - ex) - thr, (c.y - ey) - thr, (c.z - ez) - thr);
+    *hi = mk((c.x + ex) + thr, (c.y + ey) + thr, (c.z + ez) + thr);
+}
+/* btSimulationIslandManager::buildIslands' activation pass: an island none of whose bodies is
+ * ACTIVE_TAG goes to ISLAND_SLEEPING as a whole; in an island with an ACTIVE_TAG body, the sleeping
+ * ones become WANTS_DEACTIVATION (simulated again).  Run at the start of the step, from the poses
+ * and the states left by the previous step's updateActivationState (the narrowphase does not
+ * change either). */
+static void sleep_islands(sim_t* S, const cp_physics* P) {
+    v3 lo[CP_NUM_DYN], hi[CP_NUM_DYN];
+    for (int d = 0; d < CP_NUM_DYN; ++d) body_aabb(S, P, d, &lo[d], &hi[d]);
+    int root[CP_NUM_DYN] = {0, 1, 2, 3};
+    for (int a = 0; a < CP_NUM_DYN; ++a)
+        for (int b = a + 1; b < CP_NUM_DYN; ++b) {
+            const int ov = !(lo[a].x > hi[b].x || hi[a].x < lo[b].x || lo[a].y > hi[b].y || hi[a].y < lo[b].y ||
+                             lo[a].z > hi[b].z || hi[a].z < lo[b].z);   /* btAabbOverlap */
+            if (!ov) continue;
+            const int ra = root[a], rb = root[b];
+            if (ra == rb) continue;
+            const int lo_r = ra < rb ? ra : rb, hi_r = ra < rb ? rb : ra;
+            for (int d = 0; d < CP_NUM_DYN; ++d) if (root[d] == hi_r) root[d] = lo_r;
+        }
+    for (int r = 0; r < CP_NUM_DYN; ++r) {
+        int any_active = 0;
+        for (int d = 0; d < CP_NUM_DYN; ++d)
+            if (root[d] == r && (S->slp_a[d] & 15) == CP_ACT_ACTIVE) any_active = 1;
+        for (int d = 0; d < CP_NUM_DYN; ++d) {
+            if (root[d] != r) continue;
+            const int32_t aw = S->slp_a[d] & CP_ACT_AWAKE;
+            if (!any_active) S->slp_a[d] = CP_ACT_SLEEPING | aw;
+            else if ((S->slp_a[d] & 15) == CP_ACT_SLEEPING) S->slp_a[d] = CP_ACT_WANTS | aw;
+        }
+    }
+}
+/* the end of the step: btMultiBody::checkMotionAndSleepIfRequired (motion = the squared base
+ * velocity coordinates, angular then linear, summed in order; below SLEEP_EPSILON the sleep timer
+ * runs and past SLEEP_TIMEOUT the body stops being awake, else the timer restarts and the body is
+ * awake), then btMultiBodyDynamicsWorld::updateActivationState (not awake and ACTIVE_TAG ->
+ * WANTS_DEACTIVATION; awake -> ACTIVE_TAG) */
+static void sleep_update(sim_t* S, const cp_physics* P) {
+    const real dt = (real)P->dt, eps = (real)P->sleep_epsilon, tmo = (real)P->sleep_timeout;
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        const v3 w = S->w[d], v = S->v[d];
+        const real motion = ((((w.x * w.x + w.y * w.y) + w.z * w.z) + v.x * v.x) + v.y * v.y) + v.z * v.z;
+        int32_t a = S->slp_a[d];
+        if (motion < eps) {
+            S->slp_t[d] = S->slp_t[d] + dt;
+            if (S->slp_t[d] > tmo) a &= ~CP_ACT_AWAKE;
+        } else {
+            S->slp_t[d] = RC(0);
+            a |= CP_ACT_AWAKE;
+        }
+        if (a & CP_ACT_AWAKE) a = CP_ACT_ACTIVE | CP_ACT_AWAKE;
+        else if ((a & 15) == CP_ACT_ACTIVE) a = CP_ACT_WANTS;
+        S->slp_a[d] = a;
+    }
+}
+static void sleep_wake_all(sim_t* S) {   /* resetBasePositionAndOrientation [ext, low confidence] */
+    for (int d = 0; d < CP_NUM_DYN; ++d) { S->slp_a[d] = CP_ACT_ACTIVE | CP_ACT_AWAKE; S->slp_t[d] = RC(0); }
+}
+
 /* one p.stepSimulation() of the scene (DESIGN.md §Physics model, steps 1-8) */
 static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* iters_out, int32_t* npts_out,
                     int32_t* isl_iters, int32_t* merged_out) {
@@ -931,6 +1009,14 @@ static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* i
         quat_axes(S->q[d], S->ax[d]);
         world_inv_inertia(S->ax[d], P->inv_inertia[d + 1], S->M[d]);
     }
+    /* 1b. CP_MODEL_SLEEPING: this step's island activation; a sleeping body is not simulated */
+    const int sleeping = (P->model_flags & CP_MODEL_SLEEPING) != 0;
+    int sl[CP_NUM_DYN] = {0, 0, 0, 0};
+    if (sleeping) {
+        sleep_islands(S, P);
+        for (int d = 0; d < CP_NUM_DYN; ++d) sl[d] = (S->slp_a[d] & 15) == CP_ACT_SLEEPING;
+    }
+    int skip[CP_NUM_ISLANDS][CP_ISLAND_PAIRS];   /* pairs of a sleeping island: no contact, cache kept */
     /* 2. narrowphase + row setup at the start-of-step poses, per island: its 3 own
      *    pairs then its 2 cross pairs, into its own capped pool */
     const int persistent = (P->model_flags & CP_MODEL_PERSISTENT) != 0;
@@ -948,7 +1034,11 @@ static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* i
             real dist[4];
             int ids[4], pmi[4];
             int cnt;
-            if (!persistent) {
+            skip[p][j] = sl[b - 1] || (a > 0 && sl[a - 1]);
+            if (skip[p][j]) {
+                cnt = 0;
+                n = mk(RC(0), RC(0), RC(1));
+            } else if (!persistent) {
                 cnt = box_box(&A, &B, (real)P->contact_margin, (real)P->edge_bias, &n, pts, dist, ids);
                 for (int k = 0; k < cnt; ++k) { pn[k] = n; pmi[k] = -1; }
             } else {
@@ -997,6 +1087,7 @@ static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* i
      *    damping (-m v (k + k|v|), -I w (k + k|w|)) + gyroscopic term */
     const real kl = (real)P->lin_damping, ka = (real)P->ang_damping;
     for (int d = 0; d < CP_NUM_DYN; ++d) {
+        if (sl[d]) continue;   /* CP_MODEL_SLEEPING: no gravity, forces or damping for a sleeping body */
         int g = d + 1;
         real im = (real)P->inv_mass[g];
         v3 v = S->v[d], w = S->w[d], F = S->f[d];
@@ -1140,6 +1231,7 @@ static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* i
         }
     for (int p = 0; p < CP_NUM_ISLANDS && !persistent; ++p) {   /* feature-id cache: default model only */
         for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
+            if (skip[p][j]) continue;   /* a sleeping island's manifolds keep their impulses */
             manifold_t* m = &isl[p].man[j];
             uint32_t idw = 0xFFFFFFFFu;
             for (int k = 0; k < 4; ++k) {
@@ -1161,6 +1253,10 @@ static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* i
     const real c3 = ((dt * dt) * dt) * RC(0.020833333333);
     const real maxang = (real)P->max_angular_step;
     for (int d = 0; d < CP_NUM_DYN; ++d) {
+        if (sl[d]) {   /* btMultiBodyDynamicsWorld::integrateTransforms: a sleeping body's velocities cleared */
+            S->v[d] = S->w[d] = mk(RC(0), RC(0), RC(0));
+            continue;
+        }
         v3 v = S->v[d], w = S->w[d];
         S->x[d] = madd(S->x[d], v, dt);
         real ang = SQRT(dot(w, w));
@@ -1183,6 +1279,8 @@ static void substep(sim_t* S, const cp_physics* P, int32_t* overflow, int32_t* i
     }
     /* 6. external forces are consumed by the step (pybullet clears them) */
     for (int d = 0; d < CP_NUM_DYN; ++d) S->f[d] = mk(RC(0), RC(0), RC(0));
+    /* 7. CP_MODEL_SLEEPING: updateActivationState */
+    if (sleeping) sleep_update(S, P);
     if (iters_out) *iters_out = it_max;
     if (npts_out) *npts_out = isl[0].used + isl[1].used;
 }
@@ -1198,6 +1296,7 @@ static void apply_force_link(sim_t* S, int d, real fx, real fy, real fz) {
 /* ------------------------------------------------------------ world-level API */
 static void world_load(const orc_world* w, sim_t* S) {
     memset(S->pm, 0, sizeof(S->pm));  /* CP_MODEL_PERSISTENT is an env-level (orc_envs) option */
+    sleep_wake_all(S);                /* so is CP_MODEL_SLEEPING (its state lives in the env SoA) */
     for (int d = 0; d < CP_NUM_DYN; ++d) {
         S->x[d] = mk((real)w->pos[d][0], (real)w->pos[d][1], (real)w->pos[d][2]);
         for (int k = 0; k < 4; ++k) S->q[d][k] = (real)w->quat[d][k];
@@ -1290,6 +1389,10 @@ static void env_load(const orc_envs* e, int i, sim_t* S) {
             for (int k = 0; k < 4; ++k) S->ws_lam[p][j][k] = SF(e, CP_SF_WS_LAM(p, j, k), i);
         }
     memcpy(S->pm, (const pman_t*)e->pman + (size_t)i * CP_NUM_PAIRS, sizeof(S->pm));
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        memcpy(&S->slp_a[d], &SF(e, CP_SF_SLEEP_ACT(d), i), 4);
+        S->slp_t[d] = SF(e, CP_SF_SLEEP_TIMER(d), i);
+    }
 }
 static void env_store(orc_envs* e, int i, const sim_t* S) {
     for (int d = 0; d < CP_NUM_DYN; ++d) {
@@ -1315,6 +1418,10 @@ static void env_store(orc_envs* e, int i, const sim_t* S) {
             for (int k = 0; k < 4; ++k) SF(e, CP_SF_WS_LAM(p, j, k), i) = S->ws_lam[p][j][k];
         }
     memcpy((pman_t*)e->pman + (size_t)i * CP_NUM_PAIRS, S->pm, sizeof(S->pm));
+    for (int d = 0; d < CP_NUM_DYN; ++d) {
+        memcpy(&SF(e, CP_SF_SLEEP_ACT(d), i), &S->slp_a[d], 4);
+        SF(e, CP_SF_SLEEP_TIMER(d), i) = S->slp_t[d];
+    }
 }
 static int32_t get_i(const orc_envs* e, int f, int i) {
     int32_t v;
@@ -1358,6 +1465,7 @@ int orc_envs_create(const cp_config* cfg, orc_envs** out) {
         }
         for (int p = 0; p < CP_NUM_ISLANDS; ++p)
             for (int j = 0; j < CP_ISLAND_PAIRS; ++j) set_i(e, CP_SF_WS_ID(p, j), i, -1);
+        for (int d = 0; d < CP_NUM_DYN; ++d) set_i(e, CP_SF_SLEEP_ACT(d), i, CP_ACT_ACTIVE | CP_ACT_AWAKE);
         /* done = 1 until the first reset: step before reset is an error in the
          * reference (AttributeError); the batched API reports done. */
         set_i(e, CP_SF_DONE, i, 1);
@@ -1441,6 +1549,7 @@ static void reset_one(orc_envs* e, int i, float* obs_row /* R*14 */) {
             for (int k = 0; k < 4; ++k) S.ws_lam[p][j][k] = RC(0);
             S.pm[p][j].cnt = 0;   /* resetBasePositionAndOrientation: no contact survives the teleport */
         }
+    sleep_wake_all(&S);           /* CP_MODEL_SLEEPING: the teleported bodies are awake */
     int32_t ov = 0;
     for (int s = 0; s < cfg->settle_steps; ++s) substep(&S, &cfg->phys, &ov, NULL, NULL, NULL, NULL);
     for (int k = 0; k < cfg->initial_force_steps; ++k) {
