@@ -46,14 +46,16 @@ using SoaF = SoaT<float>;
 
 __constant__ float kDiscrete[CP_NUM_DISCRETE][2] = {{0.f, 0.f}, {-1.f, 0.f}, {1.f, 0.f}, {0.f, 1.f}, {0.f, -1.f}};
 
-// raster obs: the repeat-end pose of the 4 bodies (xyz, quat xyzw) for the render kernel
-CP_DEV void write_rposes(const Sim& S, float* dst) {
-#pragma unroll
-    for (int d = 0; d < CP_NUM_DYN; ++d) {
-        float* o = dst + d * 7;
-        o[0] = (float)S.b[d].x.x; o[1] = (float)S.b[d].x.y; o[2] = (float)S.b[d].x.z;
-        o[3] = (float)S.b[d].q[0]; o[4] = (float)S.b[d].q[1]; o[5] = (float)S.b[d].q[2]; o[6] = (float)S.b[d].q[3];
-    }
+// raster obs: the repeat-end pose of the lane's own 2 bodies (xyz, quat xyzw) for the render kernel; dst is
+// the env's [4][7] row, island p's lane writes bodies 2p, 2p + 1
+CP_DEV void write_pose(const Body& B, float* o) {
+    o[0] = (float)B.x.x; o[1] = (float)B.x.y; o[2] = (float)B.x.z;
+    o[3] = (float)B.q[0]; o[4] = (float)B.q[1]; o[5] = (float)B.q[2]; o[6] = (float)B.q[3];
+}
+CP_DEV void write_rposes_own(const Own& O, int isl, float* dst) {
+    float* o = dst + 2 * isl * 7;
+    write_pose(O.c, o);
+    write_pose(O.p, o + 7);
 }
 
 // per-wave stamp accumulation into b.stamps (lane 0 writes; CP_STAMPS builds only)
@@ -106,79 +108,102 @@ CP_DEV void put_out(T* p, T v) {
 #endif
 }
 
-CP_DEV void load_sim(Sim& S, const Soa& st, uint32_t o) {
+// The lane's own island's fields of the state SoA: island p's bodies are dyn 2p, 2p + 1 (CP_SF_BODY(2p + k, c)),
+// its cart's pending force CP_SF_PENDING(p, c), its sleep words CP_SF_SLEEP_*(2p + k).  The island part of
+// the field index goes into the lane's buffer offset, so every field offset stays wave-uniform (SGPR soffset).
+CP_DEV uint32_t isl_off(const Mem& G, int isl, int fields) { return G.off + (uint32_t)(isl * fields) * G.st.fstride; }
+CP_DEV void load_body(Body& B, const Soa& st, int f0, uint32_t o) {
+    B.x = mk(st.ld(f0 + 0, o), st.ld(f0 + 1, o), st.ld(f0 + 2, o));
 #pragma unroll
-    for (int d = 0; d < CP_NUM_DYN; ++d) {
-        S.b[d].x = mk(st.ld(CP_SF_BODY(d, 0), o), st.ld(CP_SF_BODY(d, 1), o), st.ld(CP_SF_BODY(d, 2), o));
-#pragma unroll
-        for (int k = 0; k < 4; ++k) S.b[d].q[k] = st.ld(CP_SF_BODY(d, 3 + k), o);
-        S.b[d].v = mk(st.ld(CP_SF_BODY(d, 7), o), st.ld(CP_SF_BODY(d, 8), o), st.ld(CP_SF_BODY(d, 9), o));
-        S.b[d].w = mk(st.ld(CP_SF_BODY(d, 10), o), st.ld(CP_SF_BODY(d, 11), o), st.ld(CP_SF_BODY(d, 12), o));
-    }
-    S.f0 = mk(st.ld(CP_SF_PENDING(0, 0), o), st.ld(CP_SF_PENDING(0, 1), o), st.ld(CP_SF_PENDING(0, 2), o));
-    S.f2 = mk(st.ld(CP_SF_PENDING(1, 0), o), st.ld(CP_SF_PENDING(1, 1), o), st.ld(CP_SF_PENDING(1, 2), o));
+    for (int k = 0; k < 4; ++k) B.q[k] = st.ld(f0 + 3 + k, o);
+    B.v = mk(st.ld(f0 + 7, o), st.ld(f0 + 8, o), st.ld(f0 + 9, o));
+    B.w = mk(st.ld(f0 + 10, o), st.ld(f0 + 11, o), st.ld(f0 + 12, o));
 }
-
-CP_DEV void store_sim(const Sim& S, const Soa& st, uint32_t o) {
+CP_DEV void store_body(const Body& B, const Soa& st, int f0, uint32_t o) {
+    st.st(f0 + 0, o, B.x.x);
+    st.st(f0 + 1, o, B.x.y);
+    st.st(f0 + 2, o, B.x.z);
 #pragma unroll
-    for (int d = 0; d < CP_NUM_DYN; ++d) {
-        st.st(CP_SF_BODY(d, 0), o, S.b[d].x.x);
-        st.st(CP_SF_BODY(d, 1), o, S.b[d].x.y);
-        st.st(CP_SF_BODY(d, 2), o, S.b[d].x.z);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) st.st(CP_SF_BODY(d, 3 + k), o, S.b[d].q[k]);
-        st.st(CP_SF_BODY(d, 7), o, S.b[d].v.x);
-        st.st(CP_SF_BODY(d, 8), o, S.b[d].v.y);
-        st.st(CP_SF_BODY(d, 9), o, S.b[d].v.z);
-        st.st(CP_SF_BODY(d, 10), o, S.b[d].w.x);
-        st.st(CP_SF_BODY(d, 11), o, S.b[d].w.y);
-        st.st(CP_SF_BODY(d, 12), o, S.b[d].w.z);
-    }
-    st.st(CP_SF_PENDING(0, 0), o, S.f0.x);
-    st.st(CP_SF_PENDING(0, 1), o, S.f0.y);
-    st.st(CP_SF_PENDING(0, 2), o, S.f0.z);
-    st.st(CP_SF_PENDING(1, 0), o, S.f2.x);
-    st.st(CP_SF_PENDING(1, 1), o, S.f2.y);
-    st.st(CP_SF_PENDING(1, 2), o, S.f2.z);
+    for (int k = 0; k < 4; ++k) st.st(f0 + 3 + k, o, B.q[k]);
+    st.st(f0 + 7, o, B.v.x);
+    st.st(f0 + 8, o, B.v.y);
+    st.st(f0 + 9, o, B.v.z);
+    st.st(f0 + 10, o, B.w.x);
+    st.st(f0 + 11, o, B.w.y);
+    st.st(f0 + 12, o, B.w.z);
 }
-
-// CP_MODEL_SLEEPING state of the 4 bodies (SLP kernels only; the other models never touch these fields)
-CP_DEV void load_sleep(Sim& S, const Soa& st, uint32_t o) {
+CP_DEV void load_own(Own& O, const Mem& G, int isl) {
+    const uint32_t ob = isl_off(G, isl, 2 * CP_BODY_FIELDS), of = isl_off(G, isl, 3);
+    load_body(O.c, G.st, CP_SF_BODY(0, 0), ob);
+    load_body(O.p, G.st, CP_SF_BODY(1, 0), ob);
+    O.f = mk(G.st.ld(CP_SF_PENDING(0, 0), of), G.st.ld(CP_SF_PENDING(0, 1), of), G.st.ld(CP_SF_PENDING(0, 2), of));
+}
+CP_DEV void store_own(const Own& O, const Mem& G, int isl) {
+    const uint32_t ob = isl_off(G, isl, 2 * CP_BODY_FIELDS), of = isl_off(G, isl, 3);
+    store_body(O.c, G.st, CP_SF_BODY(0, 0), ob);
+    store_body(O.p, G.st, CP_SF_BODY(1, 0), ob);
+    G.st.st(CP_SF_PENDING(0, 0), of, O.f.x);
+    G.st.st(CP_SF_PENDING(0, 1), of, O.f.y);
+    G.st.st(CP_SF_PENDING(0, 2), of, O.f.z);
+}
+// CP_MODEL_SLEEPING state of the lane's own bodies (SLP kernels only; the other models never touch these fields)
+CP_DEV void load_sleep(Own& O, const Mem& G, int isl) {
+    const uint32_t o = isl_off(G, isl, 2);
 #pragma unroll
-    for (int d = 0; d < CP_NUM_DYN; ++d) {
-        S.slp_a[d] = to_bits(st.ld(CP_SF_SLEEP_ACT(d), o));
-        S.slp_t[d] = st.ld(CP_SF_SLEEP_TIMER(d), o);
+    for (int k = 0; k < 2; ++k) {
+        O.sa[k] = to_bits(G.st.ld(CP_SF_SLEEP_ACT(k), o));
+        O.st[k] = G.st.ld(CP_SF_SLEEP_TIMER(k), o);
     }
 }
-CP_DEV void store_sleep(const Sim& S, const Soa& st, uint32_t o) {
+CP_DEV void store_sleep(const Own& O, const Mem& G, int isl) {
+    const uint32_t o = isl_off(G, isl, 2);
 #pragma unroll
-    for (int d = 0; d < CP_NUM_DYN; ++d) {
-        st.st(CP_SF_SLEEP_ACT(d), o, bits_to<real>(S.slp_a[d]));
-        st.st(CP_SF_SLEEP_TIMER(d), o, S.slp_t[d]);
+    for (int k = 0; k < 2; ++k) {
+        G.st.st(CP_SF_SLEEP_ACT(k), o, bits_to<real>(O.sa[k]));
+        G.st.st(CP_SF_SLEEP_TIMER(k), o, O.st[k]);
     }
+}
+// the reset's pose of the lane's own bodies (resetBasePositionAndOrientation, bullet_cartpole.py:319-323)
+template <int G0, int G1>
+CP_DEV void spawn_body(Body& B, const cp_config& cfg, bool second) {
+    B.x = mk(second ? real(cfg.phys.spawn_pos[G1][0]) : real(cfg.phys.spawn_pos[G0][0]),
+             second ? real(cfg.phys.spawn_pos[G1][1]) : real(cfg.phys.spawn_pos[G0][1]),
+             second ? real(cfg.phys.spawn_pos[G1][2]) : real(cfg.phys.spawn_pos[G0][2]));
+    B.q[0] = real(0.0); B.q[1] = real(0.0); B.q[2] = real(0.0); B.q[3] = real(1.0);
+    B.v = mk(real(0.0), real(0.0), real(0.0));
+    B.w = mk(real(0.0), real(0.0), real(0.0));
+}
+CP_DEV void spawn_own(Own& O, const cp_config& cfg, bool second) {
+    spawn_body<CP_BODY_CART, CP_BODY_CART2>(O.c, cfg, second);
+    spawn_body<CP_BODY_POLE, CP_BODY_POLE2>(O.p, cfg, second);
 }
 
 CP_DEV int32_t ldi(const Soa& st, int f, uint32_t o) { return (int32_t)to_bits(st.ld(f, o)); }
 CP_DEV void sti(const Soa& st, int f, uint32_t o, int32_t v) { st.st(f, o, bits_to<real>((uint32_t)v)); }
 
-// true if every body value (pos, quat, v, w of the 4 bodies) is finite: x * 0 is +-0 for a finite
-// x and NaN for an inf or NaN, so the fma chain stays a zero exactly when all 52 values are finite
-CP_DEV bool sim_finite(const Sim& S) {
+// true if every body value (pos, quat, v, w) of the lane's own bodies is finite: x * 0 is +-0 for a finite
+// x and NaN for an inf or NaN, so the fma chain stays a zero exactly when all 26 values are finite
+CP_DEV bool own_finite(const Own& O) {
 #ifdef CP_NO_NONFINITE  // diagnostic A/B build: the counter's cost (never counts)
-    (void)S;
+    (void)O;
     return true;
 #endif
     real acc = real(0.0);
-#pragma unroll
-    for (int d = 0; d < CP_NUM_DYN; ++d) {
-        const Body& y = S.b[d];
+    auto body = [&](const Body& y) {
         acc = fma_(y.x.x, real(0.0), acc); acc = fma_(y.x.y, real(0.0), acc); acc = fma_(y.x.z, real(0.0), acc);
 #pragma unroll
         for (int k = 0; k < 4; ++k) acc = fma_(y.q[k], real(0.0), acc);
         acc = fma_(y.v.x, real(0.0), acc); acc = fma_(y.v.y, real(0.0), acc); acc = fma_(y.v.z, real(0.0), acc);
         acc = fma_(y.w.x, real(0.0), acc); acc = fma_(y.w.y, real(0.0), acc); acc = fma_(y.w.z, real(0.0), acc);
-    }
+    };
+    body(O.c);
+    body(O.p);
     return acc == real(0.0);
+}
+// the whole env's finiteness on both lanes (DPP: both lanes of the pair active)
+CP_DEV bool env_finite(const Own& O) {
+    const uint32_t f = own_finite(O) ? 1u : 0u;
+    return (f & partner_u(f)) != 0u;
 }
 
 // CP_RESET_CLEAR_NONFINITE_FORCE: a reset zeroes a cart's pending force with a non-finite component
@@ -188,12 +213,13 @@ CP_DEV V3 reset_force(const cp_config& cfg, V3 f) {
     return z == real(0.0) ? f : mk(real(0.0), real(0.0), real(0.0));
 }
 
-CP_DEV void write_obs_row(const Sim& S, float* dst) {
-    dst[0] = (float)S.b[0].x.x; dst[1] = (float)S.b[0].x.y; dst[2] = (float)S.b[0].x.z;
-    dst[3] = (float)S.b[0].q[0]; dst[4] = (float)S.b[0].q[1]; dst[5] = (float)S.b[0].q[2]; dst[6] = (float)S.b[0].q[3];
-    dst[7] = (float)S.b[1].x.x; dst[8] = (float)S.b[1].x.y; dst[9] = (float)S.b[1].x.z;
-    dst[10] = (float)S.b[1].q[0]; dst[11] = (float)S.b[1].q[1]; dst[12] = (float)S.b[1].q[2];
-    dst[13] = (float)S.b[1].q[3];
+// obs row of a repeat (bullet_cartpole.py:298-311): cart and pole, island 0's own bodies (the lead lane's)
+CP_DEV void write_obs_row(const Own& O, float* dst) {
+    dst[0] = (float)O.c.x.x; dst[1] = (float)O.c.x.y; dst[2] = (float)O.c.x.z;
+    dst[3] = (float)O.c.q[0]; dst[4] = (float)O.c.q[1]; dst[5] = (float)O.c.q[2]; dst[6] = (float)O.c.q[3];
+    dst[7] = (float)O.p.x.x; dst[8] = (float)O.p.x.y; dst[9] = (float)O.p.x.z;
+    dst[10] = (float)O.p.q[0]; dst[11] = (float)O.p.q[1]; dst[12] = (float)O.p.q[2];
+    dst[13] = (float)O.p.q[3];
 }
 
 // 12-state pole readback (bullet_cartpole.py:212-229)
@@ -209,10 +235,8 @@ CP_DEV void readback_pole(const Sim& S, float* dst) {
 }
 
 // ---- closed-loop LQR policy (random_action_agent.py:60-135)
-// pole 8-state of pair P (:121-135): x - x0, x', y, y', roll, roll', pitch, pitch'
-template <int P>
-CP_DEV void pole_state8(const Sim& S, real x0, real s[8]) {
-    const Body& p = S.b[2 * P + 1];
+// pole 8-state of a pair (:121-135): x - x0, x', y, y', roll, roll', pitch, pitch'
+CP_DEV void pole_state8(const Body& p, real x0, real s[8]) {
     const V3 rpy = quat_euler(p.q[0], p.q[1], p.q[2], p.q[3]);
     s[0] = p.x.x - x0; s[1] = p.v.x; s[2] = p.x.y; s[3] = p.v.y;
     s[4] = rpy.x; s[5] = p.w.x; s[6] = rpy.y; s[7] = p.w.y;
@@ -234,26 +258,22 @@ CP_DEV bool lqr_out_of_bounds(const real s[8], real pos, real ang) {
     return abs_(s[0]) > pos || abs_(s[2]) > pos || abs_(s[4]) > ang || abs_(s[6]) > ang;
 }
 
-// 8-states of both pairs -> next forces; true if both pairs are out of bounds (:908)
-CP_DEV bool lqr_observe(const Sim& S, const cp_config& cfg, const Lqr& q, const float* K, real u[2][2],
+// the lane's own pair (island p's lane: pole p, cart p): its 8-state (written to s8_out[8 p ..] when given)
+// -> the next control force u of its cart; true on both lanes if both pairs are out of bounds (:908).
+// Both lanes of the env active (DPP).
+CP_DEV bool lqr_observe(const Own& O, bool second, const cp_config& cfg, const Lqr& q, const float* K, real u[2],
                         float* s8_out) {
     real s[8];
-    pole_state8<0>(S, real(cfg.phys.spawn_pos[CP_BODY_POLE][0]), s);
+    pole_state8(O.p, real(cfg.phys.spawn_pos[second ? CP_BODY_POLE2 : CP_BODY_POLE][0]), s);
     if (s8_out)
-        for (int k = 0; k < 8; ++k) s8_out[k] = (float)s[k];
-    lqr_u(K, s, u[0][0], u[0][1]);
-    const bool out0 = lqr_out_of_bounds(s, real(q.done_pos), real(q.done_angle));
-    pole_state8<1>(S, real(cfg.phys.spawn_pos[CP_BODY_POLE2][0]), s);
-    if (s8_out)
-        for (int k = 0; k < 8; ++k) s8_out[k + 8] = (float)s[k];
-    lqr_u(K + 16, s, u[1][0], u[1][1]);
-    const bool out1 = lqr_out_of_bounds(s, real(q.done_pos), real(q.done_angle));
-    return q.done_pos > 0.0f && out0 && out1;
+        for (int k = 0; k < 8; ++k) s8_out[(second ? 8 : 0) + k] = (float)s[k];
+    lqr_u(K + (second ? 16 : 0), s, u[0], u[1]);
+    const uint32_t out = lqr_out_of_bounds(s, real(q.done_pos), real(q.done_angle)) ? 1u : 0u;
+    return q.done_pos > 0.0f && (out & partner_u(out)) != 0u;
 }
 
-// commented-out bounds check of the reference (:243-253), on the pole pose
-CP_DEV bool bounds_exceeded(const Sim& S, const cp_config& cfg) {
-    const Body& p = S.b[1];
+// commented-out bounds check of the reference (:243-253), on the pole pose (island 0's lane's own pole)
+CP_DEV bool bounds_exceeded_pole(const Body& p, const cp_config& cfg) {
     if (abs_(p.x.x) > real(cfg.pos_threshold) || abs_(p.x.y) > real(cfg.pos_threshold)) return true;
     real qx = p.q[0], qy = p.q[1], qz = p.q[2], qw = p.q[3];
     real Y = real(2.0) * fma_(qy, qz, qw * qx);
@@ -262,6 +282,10 @@ CP_DEV bool bounds_exceeded(const Sim& S, const cp_config& cfg) {
     real sarg = real(-2.0) * fma_(qx, qz, -(qw * qy));
     bool pitch_out = abs_(sarg) > real(cfg.sin_angle_threshold);
     return roll_out || pitch_out;
+}
+// the env's bounds decision on both lanes: island 0's lane's pole (DPP broadcast; both lanes active)
+CP_DEV bool bounds_exceeded(const Own& O, const cp_config& cfg) {
+    return lane_of_u<0>(bounds_exceeded_pole(O.p, cfg) ? 1u : 0u) != 0u;
 }
 
 // Bump force k on cart C (LINK frame), bullet_cartpole.py:354-359
@@ -342,21 +366,15 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     Stamps ST;
     CP_STAMP(k0);
     CP_RT(r0);
-    Sim S;
-    load_sim(S, G.st, G.off);  // pending forces survive the reset (pybullet keeps them)
-    S.f0 = reset_force(cfg, S.f0);
-    S.f2 = reset_force(cfg, S.f2);
+    const bool second = isl != 0;
+    Own O;
+    load_own(O, G, isl);  // pending forces survive the reset (pybullet keeps them)
+    O.f = reset_force(cfg, O.f);
     if constexpr (PM)  // resetBasePositionAndOrientation: no cached contact survives the teleport
         for (int j = 0; j < CP_ISLAND_PAIRS; ++j) G.sp(pmf(j, 0), bits_to<real>(0u));
     const int episode = ldi(G.st, CP_SF_EPISODE, G.off);
-#pragma unroll
-    for (int d = 0; d < CP_NUM_DYN; ++d) {
-        S.b[d].x = mk(cfg.phys.spawn_pos[d + 1][0], cfg.phys.spawn_pos[d + 1][1], cfg.phys.spawn_pos[d + 1][2]);
-        S.b[d].q[0] = real(0.0); S.b[d].q[1] = real(0.0); S.b[d].q[2] = real(0.0); S.b[d].q[3] = real(1.0);
-        S.b[d].v = mk(real(0.0), real(0.0), real(0.0));
-        S.b[d].w = mk(real(0.0), real(0.0), real(0.0));
-    }
-    if constexpr (SLP) sleep_wake_all(S);  // the teleported bodies are awake
+    spawn_own(O, cfg, second);
+    if constexpr (SLP) sleep_wake_all(O);  // the teleported bodies are awake
 #pragma unroll
     for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {  // the lane's island's warm-start cache
         G.sw(CP_SF_WS_ID(0, j), bits_to<real>(0xFFFFFFFFu));
@@ -366,14 +384,12 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     int ov = 0;
     const int nsub = cfg.settle_steps + cfg.initial_force_steps;
     for (int s = 0; s < nsub; ++s) {
-        substep<LAT && !kF64, true, true, PM, SLP>(S, cfg.phys, L, pool, pool0, ov, G, ST);
+        substep<LAT && !kF64, true, true, PM, SLP>(O, cfg.phys, L, pool, pool0, ov, G, ST);
         const int k = s - cfg.settle_steps;
-        if (k >= 0) {
+        if (k >= 0) {  // bump the lane's own cart (cart, then cart2 in the reference's draw order)
             real fx, fy;
-            bump_force(cfg, b.bumps, i, episode, k, 0, fx, fy);
-            apply_force_link<0>(S, fx, fy);
-            bump_force(cfg, b.bumps, i, episode, k, 1, fx, fy);
-            apply_force_link<1>(S, fx, fy);
+            bump_force(cfg, b.bumps, i, episode, k, isl, fx, fy);
+            apply_force_link(O, fx, fy);
         }
     }
     ov += (int)partner_u((uint32_t)ov);
@@ -382,16 +398,17 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     CP_RT(r1);
     flush_stamps(ST, b.stamps + 16, k1 - k0, r0, r1);  // the reset kernel's counters: slots 16-26
 #endif
-    if (!lead) return;
-    store_sim(S, G.st, G.off);
-    if constexpr (SLP) store_sleep(S, G.st, G.off);
-    b.overflow[i] += ov;
-    if (!sim_finite(S)) b.nonfinite[i] += 1;
-    float row[14];
-    write_obs_row(S, row);
+    store_own(O, G, isl);  // each lane stores its own island
+    if constexpr (SLP) store_sleep(O, G, isl);
+    const bool fin = env_finite(O);
     const int R = cfg.action_repeats;
     if (b.rposes)  // every repeat slot shows the reset pose (bullet_cartpole.py:342-345)
-        for (int r = 0; r < R; ++r) write_rposes(S, b.rposes + ((size_t)i * R + r) * CP_NUM_DYN * 7);
+        for (int r = 0; r < R; ++r) write_rposes_own(O, isl, b.rposes + ((size_t)i * R + r) * CP_NUM_DYN * 7);
+    if (!lead) return;
+    b.overflow[i] += ov;
+    if (!fin) b.nonfinite[i] += 1;
+    float row[14];
+    write_obs_row(O, row);
     float* o = obs_out + (size_t)i * R * 14;
     for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -455,57 +472,61 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
                 a10 = kDiscrete[k1][0]; a11 = kDiscrete[k1][1];
             }
             const real F = cfg.action_force;
-            const real f00 = a00 * F, f01 = a01 * F, f10 = a10 * F, f11 = a11 * F;
-            Sim S;
-            load_sim(S, G.st, G.off);
-            if constexpr (SLP) load_sleep(S, G.st, G.off);
+            const bool second = isl != 0;
+            // the lane's own cart's action force (action[0] -> cart, action[1] -> cart2, :201-207)
+            const real fa = (second ? a10 : a00) * F, fb = (second ? a11 : a01) * F;
+            Own O;
+            load_own(O, G, isl);
+            if constexpr (SLP) load_sleep(O, G, isl);
             int ov = 0;
-            real u[2][2] = {{real(0.0), real(0.0)}, {real(0.0), real(0.0)}};  // LQR forces from the last observed state
+            real u[2] = {real(0.0), real(0.0)};  // LQR force of the own cart from the last observed state
             bool lqr_done = false;
             const float* K = nullptr;
             if constexpr (LQR) {
                 K = lq.gains + (lq.per_env ? (size_t)i * 32 : 0);
-                lqr_observe(S, cfg, lq, K, u, nullptr);
+                lqr_observe(O, second, cfg, lq, K, u, nullptr);
             }
             for (int r = 0; r < R; ++r) {
                 for (int s = 0; s < SR; ++s) {
-                    substep<LAT && !kF64, kC44Step && !LAT && !kF64 && !PM, kAllinStep, PM, SLP>(S, cfg.phys, L, pool,
+                    substep<LAT && !kF64, kC44Step && !LAT && !kF64 && !PM, kAllinStep, PM, SLP>(O, cfg.phys, L, pool,
                                                                                                    pool0, ov, G, ST);
                     if constexpr (LQR) {  // disturbance + control (:897-901), control from the pre-step state
-                        apply_force_link<0>(S, f00 + u[0][0], f01 + u[0][1]);
-                        apply_force_link<1>(S, f10 + u[1][0], f11 + u[1][1]);
-                        float* s8 = (lq.state8 && lead) ? lq.state8 + (((size_t)i * R + r) * SR + s) * 16 : nullptr;
-                        lqr_done |= lqr_observe(S, cfg, lq, K, u, s8);
+                        apply_force_link(O, fa + u[0], fb + u[1]);
+                        float* s8 = lq.state8 ? lq.state8 + (((size_t)i * R + r) * SR + s) * 16 : nullptr;
+                        lqr_done |= lqr_observe(O, second, cfg, lq, K, u, s8);
                     } else {
-                        apply_force_link<0>(S, f00, f01);
-                        apply_force_link<1>(S, f10, f11);
+                        apply_force_link(O, fa, fb);
                     }
-                    if (readback && lead) {
-                        float* rb = readback + (size_t)i * 2 * R * SR * 12;
-                        readback_pole<1, 1>(S, rb + ((size_t)(0 * R + r) * SR + s) * 12);
-                        if (rb_bug) readback_pole<3, 1>(S, rb + ((size_t)(1 * R + r) * SR + s) * 12);
-                        else readback_pole<3, 3>(S, rb + ((size_t)(1 * R + r) * SR + s) * 12);
+                    if (readback) {  // 12-states of both poles: the whole env on both lanes (DPP), the lead writes
+                        const Sim V = env_view(O);
+                        if (lead) {
+                            float* rb = readback + (size_t)i * 2 * R * SR * 12;
+                            readback_pole<1, 1>(V, rb + ((size_t)(0 * R + r) * SR + s) * 12);
+                            if (rb_bug) readback_pole<3, 1>(V, rb + ((size_t)(1 * R + r) * SR + s) * 12);
+                            else readback_pole<3, 3>(V, rb + ((size_t)(1 * R + r) * SR + s) * 12);
+                        }
                     }
                 }
                 if (lead) {
                     float row[14];
-                    write_obs_row(S, row);
+                    write_obs_row(O, row);
 #pragma unroll
                     for (int f = 0; f < 14; ++f) put_out(&obs[r * 14 + f], row[f]);
-                    if (b.rposes) write_rposes(S, b.rposes + ((size_t)i * R + r) * CP_NUM_DYN * 7);
                 }
+                if (b.rposes) write_rposes_own(O, isl, b.rposes + ((size_t)i * R + r) * CP_NUM_DYN * 7);
             }
             render_me = lead && b.rposes != nullptr;
             ov += (int)partner_u((uint32_t)ov);
             if (ov && lead) b.overflow[i] += ov;
             const int steps = ldi(G.st, CP_SF_STEPS, G.off) + 1;
             bool done = steps >= cfg.max_episode_len;
-            if (cfg.done_on_bounds && bounds_exceeded(S, cfg)) done = true;
+            if (cfg.done_on_bounds && bounds_exceeded(O, cfg)) done = true;
             if (LQR && lqr_done) done = true;
+            store_own(O, G, isl);  // each lane stores its own island
+            if constexpr (SLP) store_sleep(O, G, isl);
+            const bool fin = env_finite(O);
             if (lead) {
-                store_sim(S, G.st, G.off);
-                if constexpr (SLP) store_sleep(S, G.st, G.off);
-                if (!sim_finite(S)) b.nonfinite[i] += 1;
+                if (!fin) b.nonfinite[i] += 1;
                 sti(G.st, CP_SF_STEPS, G.off, steps);
                 put_out(&reward_out[i], 1.0f);  // bullet_cartpole.py:260
                 put_out(&done_out[i], (uint8_t)(done ? 1 : 0));
@@ -619,11 +640,12 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
     auto stc = [&](int f, int v) { G.sx(f, bits_to<real>((uint32_t)v)); };
     auto ldu = [&](int f) { return G.lx(f); };
     Stamps ST;
-    Sim S;
-    load_sim(S, G.st, G.off);
-    if constexpr (SLP) load_sleep(S, G.st, G.off);
+    const bool second = isl != 0;
+    Own O;
+    load_own(O, G, isl);
+    if constexpr (SLP) load_sleep(O, G, isl);
     int ov = 0;
-    real u[2][2];
+    real u[2];  // the own cart's LQR force
     // the next simulated step from k on: steps of an env that is done before them only return its
     // last obs, reward 0, done 1 (:179-181); writes the cold state; false when the K steps are over
     auto begin_step = [&](int k, int steps, int episode, uint32_t flags, float ret_acc) -> bool {
@@ -642,8 +664,8 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
             flags |= RF_LAST_SIM;
             if constexpr (LQR) {
                 flags &= ~RF_LQR_DONE;
-                lqr_observe(S, cfg, lq, lq.gains + (lq.per_env ? (size_t)i * 32 : 0), u, nullptr);
-                G.sx(RC_U0, u[0][0]); G.sx(RC_U1, u[0][1]); G.sx(RC_U2, u[1][0]); G.sx(RC_U3, u[1][1]);
+                lqr_observe(O, second, cfg, lq, lq.gains + (lq.per_env ? (size_t)i * 32 : 0), u, nullptr);
+                G.sx(RC_U0, u[0]); G.sx(RC_U1, u[1]);
             }
         }
         stc(RC_K, k); stc(RC_SUB, 0); stc(RC_STEPS, steps); stc(RC_EPISODE, episode); stc(RC_FLAGS, (int)flags);
@@ -654,29 +676,28 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
                            ldi(G.st, CP_SF_DONE, G.off) != 0 ? RF_DONE : 0u, b.ret_acc[i]);
     while (__ballot(work) != 0ull) {
         if (!work) continue;
-        substep<LAT && !kF64, false, kAllinStep, PM, SLP>(S, cfg.phys, L, pool, pool0, ov, G, ST);
+        substep<LAT && !kF64, false, kAllinStep, PM, SLP>(O, cfg.phys, L, pool, pool0, ov, G, ST);
         int k = ldc(RC_K), sub = ldc(RC_SUB);
         uint32_t flags = (uint32_t)ldc(RC_FLAGS);
         if (!(flags & RF_RESETTING)) {
             real f[4];
             const size_t e = env();
             action_forces<KIND>(actions, (size_t)k * B + e, real(cfg.action_force), f);
+            const real fa = second ? f[2] : f[0], fb = second ? f[3] : f[1];  // the own cart's force
             if constexpr (LQR) {
-                u[0][0] = ldu(RC_U0); u[0][1] = ldu(RC_U1); u[1][0] = ldu(RC_U2); u[1][1] = ldu(RC_U3);
-                apply_force_link<0>(S, f[0] + u[0][0], f[1] + u[0][1]);
-                apply_force_link<1>(S, f[2] + u[1][0], f[3] + u[1][1]);
-                if (lqr_observe(S, cfg, lq, lq.gains + (lq.per_env ? (size_t)i * 32 : 0), u, nullptr))
+                u[0] = ldu(RC_U0); u[1] = ldu(RC_U1);
+                apply_force_link(O, fa + u[0], fb + u[1]);
+                if (lqr_observe(O, second, cfg, lq, lq.gains + (lq.per_env ? (size_t)i * 32 : 0), u, nullptr))
                     flags |= RF_LQR_DONE;
-                G.sx(RC_U0, u[0][0]); G.sx(RC_U1, u[0][1]); G.sx(RC_U2, u[1][0]); G.sx(RC_U3, u[1][1]);
+                G.sx(RC_U0, u[0]); G.sx(RC_U1, u[1]);
             } else {
-                apply_force_link<0>(S, f[0], f[1]);
-                apply_force_link<1>(S, f[2], f[3]);
+                apply_force_link(O, fa, fb);
             }
             ++sub;
             float* obs = obs_out + (size_t)k * obs_step + e * R * 14;
             if (lead && sub % SR == 0) {
                 float row[14];
-                write_obs_row(S, row);
+                write_obs_row(O, row);
                 const int r = sub / SR - 1;
 #pragma unroll
                 for (int q = 0; q < 14; ++q) put_out(&obs[r * 14 + q], row[q]);
@@ -690,11 +711,12 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
             const int steps = ldc(RC_STEPS) + 1;
             const int episode = ldc(RC_EPISODE);
             bool done = steps >= cfg.max_episode_len;
-            if (cfg.done_on_bounds && bounds_exceeded(S, cfg)) done = true;
+            if (cfg.done_on_bounds && bounds_exceeded(O, cfg)) done = true;
             if (LQR && (flags & RF_LQR_DONE)) done = true;
             const float ret = __uint_as_float(to_bits(G.lx(RC_RET))) + 1.0f;
+            const bool fin = env_finite(O);
             if (lead) {
-                if (!sim_finite(S)) b.nonfinite[e] += 1;
+                if (!fin) b.nonfinite[e] += 1;
                 put_out(&reward_out[(size_t)k * B + e], 1.0f);
                 put_out(&done_out[(size_t)k * B + e], (uint8_t)(done ? 1 : 0));
             }
@@ -708,18 +730,9 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
                 }
                 flags |= RF_DONE;
                 if (cfg.autoreset) {  // the reset kernel's prologue: pending forces survive
-                    S.f0 = reset_force(cfg, S.f0);
-                    S.f2 = reset_force(cfg, S.f2);
-#pragma unroll
-                    for (int d = 0; d < CP_NUM_DYN; ++d) {
-                        S.b[d].x = mk(cfg.phys.spawn_pos[d + 1][0], cfg.phys.spawn_pos[d + 1][1],
-                                      cfg.phys.spawn_pos[d + 1][2]);
-                        S.b[d].q[0] = real(0.0); S.b[d].q[1] = real(0.0); S.b[d].q[2] = real(0.0);
-                        S.b[d].q[3] = real(1.0);
-                        S.b[d].v = mk(real(0.0), real(0.0), real(0.0));
-                        S.b[d].w = mk(real(0.0), real(0.0), real(0.0));
-                    }
-                    if constexpr (SLP) sleep_wake_all(S);
+                    O.f = reset_force(cfg, O.f);
+                    spawn_own(O, cfg, second);
+                    if constexpr (SLP) sleep_wake_all(O);
 #pragma unroll
                     for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
                         G.sw(CP_SF_WS_ID(0, j), bits_to<real>(0xFFFFFFFFu));
@@ -741,20 +754,19 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
                 const int episode = ldc(RC_EPISODE);
                 real fx, fy;
                 const int e = (int)env();
-                bump_force(cfg, b.bumps, e, episode, kb, 0, fx, fy);
-                apply_force_link<0>(S, fx, fy);
-                bump_force(cfg, b.bumps, e, episode, kb, 1, fx, fy);
-                apply_force_link<1>(S, fx, fy);
+                bump_force(cfg, b.bumps, e, episode, kb, isl, fx, fy);  // the own cart's bump
+                apply_force_link(O, fx, fy);
             }
             if (++sub < nreset) {
                 stc(RC_SUB, sub);
                 continue;
             }
             // reset end (the reset kernel's epilogue): every repeat slot shows the new pose
+            const bool fin = env_finite(O);
             if (lead) {
-                if (!sim_finite(S)) b.nonfinite[env()] += 1;
+                if (!fin) b.nonfinite[env()] += 1;
                 float row[14];
-                write_obs_row(S, row);
+                write_obs_row(O, row);
                 float* o = obs_out + (size_t)k * obs_step + env() * R * 14;
                 for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -764,10 +776,10 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
         }
     }
     ov += (int)partner_u((uint32_t)ov);  // both lanes of every pair are here
+    store_own(O, G, isl);  // each lane stores its own island
+    if constexpr (SLP) store_sleep(O, G, isl);
     if (!lead) return;
     const uint32_t flags = (uint32_t)ldc(RC_FLAGS);
-    store_sim(S, G.st, G.off);
-    if constexpr (SLP) store_sleep(S, G.st, G.off);
     sti(G.st, CP_SF_STEPS, G.off, ldc(RC_STEPS));
     sti(G.st, CP_SF_EPISODE, G.off, ldc(RC_EPISODE));
     sti(G.st, CP_SF_DONE, G.off, (flags & RF_DONE) ? 1 : 0);

@@ -69,11 +69,23 @@ struct Body {
 };
 
 // Per-env simulation state held in registers for the duration of a kernel.
+// A whole-env view (both lanes of the env hold the same values): assembled by DPP from the two lanes'
+// Own states where a phase needs every body (the env's outputs, the cross rows of a merged solve).
 struct Sim {
     Body b[CP_NUM_DYN];   // cart, pole, cart2, pole2
     V3 f0, f2;            // pending world force on cart / cart2 (pybullet force accumulator)
-    uint32_t slp_a[CP_NUM_DYN];  // CP_MODEL_SLEEPING (SLP kernels only): activation word (CP_ACT_* | CP_ACT_AWAKE)
-    real slp_t[CP_NUM_DYN];      //   and sleep timer per body
+};
+
+// Per-lane state across substeps: the lane's own island only (lane 2e: cart, pole; lane 2e+1: cart2,
+// pole2).  The partner island's bodies come from the partner lane by DPP in the phases that need them
+// (the narrowphase's cross pairs, a merged solve's cross rows, the sleeping islands, the outputs);
+// holding the whole env in both lanes kept ~29 more values live through every substep (round 5,
+// DESIGN.md §4).
+struct Own {
+    Body c, p;        // the island's cart and pole
+    V3 f;             // pending world force on the island's cart (pybullet force accumulator)
+    uint32_t sa[2];   // CP_MODEL_SLEEPING (SLP kernels only): activation words of c, p (CP_ACT_* | CP_ACT_AWAKE)
+    real st[2];       //   and their sleep timers
 };
 
 // Per-env global memory touched once per substep (cold data kept out of VGPRs):
@@ -1071,21 +1083,18 @@ CP_DEV void pair_friction_rows(Sim& S, const Step& T, bool second, const cp_phys
 __host__ __device__ constexpr int island_pair_c(int isl, int j) {
     return (int)(((isl ? 0x87932u : 0x65410u) >> (4 * j)) & 15u);
 }
-// Box of dynamic body G0 (island 0 lanes) or G1 (island 1 lanes), from the pose in S: the
-// axes are rebuilt from the quaternion here rather than kept live through the narrowphase
-// (same arithmetic as the per-body quat_axes / world_inv_inertia).
+// Box of a body with the half extents of dynamic body G0 (island 0 lanes) or G1 (island 1 lanes): the
+// axes are rebuilt from the quaternion here rather than kept live through the narrowphase (same
+// arithmetic as the per-body quat_axes / world_inv_inertia).
 template <int G0, int G1>
-CP_DEV Box box_pick(bool second, const Sim& S, const cp_physics& P) {
+CP_DEV Box box_of(bool second, const V3& x, const real q[4], const cp_physics& P) {
     static_assert(G0 >= 1 && G1 >= 1, "dynamic bodies only");
-    const Body& B0 = S.b[G0 - 1];
-    const Body& B1 = S.b[G1 - 1];
     Box b;
     b.h0 = second ? real(P.half_extents[G1][0]) : real(P.half_extents[G0][0]);
     b.h1 = second ? real(P.half_extents[G1][1]) : real(P.half_extents[G0][1]);
     b.h2 = second ? real(P.half_extents[G1][2]) : real(P.half_extents[G0][2]);
-    b.c = selv(second, B1.x, B0.x);
-    b.ax = quat_axes(second ? B1.q[0] : B0.q[0], second ? B1.q[1] : B0.q[1], second ? B1.q[2] : B0.q[2],
-                     second ? B1.q[3] : B0.q[3]);
+    b.c = x;
+    b.ax = quat_axes(q[0], q[1], q[2], q[3]);
     return b;
 }
 template <int G0, int G1>
@@ -1124,10 +1133,6 @@ CP_DEV bool face_separated(const Box& A, const Box& B, real margin) {
     return (abs_(dot(d, A.ax.a0)) - A.h0 > lim) || (abs_(dot(d, A.ax.a1)) - A.h1 > lim) ||
            (abs_(dot(d, A.ax.a2)) - A.h2 > lim);
 }
-CP_DEV V3 pos_of(int g, const Sim& S) {
-    return sel5v(g, mk(real(0.0), real(0.0), real(0.0)), S.b[0].x, S.b[1].x, S.b[2].x, S.b[3].x);
-}
-
 // row setup for direction t with pair bodies selected at run time (narrowphase)
 CP_DEV real row_k_dyn(int a, real ima, real imb, V3 xa, V3 xb, const Sym& Ma, const Sym& Mb, V3 rb, V3 t) {
     V3 rbt = cross(rb, t);
@@ -1139,48 +1144,63 @@ CP_DEV real row_k_dyn(int a, real ima, real imb, V3 xa, V3 xb, const Sym& Ma, co
     return ((ima + imb) + dot(rat, ia)) + dot(rbt, ib);
 }
 
-// select the island's (cart, pole) out of the env (island 1 -> cart2, pole2)
-CP_DEV Dyn dyn_sel(bool second, const Body& a, const Sym& Ma, const Body& b, const Sym& Mb) {
-    Dyn d;
-    d.x = selv(second, b.x, a.x);
-    d.v = selv(second, b.v, a.v);
-    d.w = selv(second, b.w, a.w);
-    d.M.m0 = second ? Mb.m0 : Ma.m0;
-    d.M.m1 = second ? Mb.m1 : Ma.m1;
-    d.M.m2 = second ? Mb.m2 : Ma.m2;
-    d.M.m3 = second ? Mb.m3 : Ma.m3;
-    d.M.m4 = second ? Mb.m4 : Ma.m4;
-    d.M.m5 = second ? Mb.m5 : Ma.m5;
-    return d;
-}
-
 // btMultiBody::applyDeltaVeeMultiDof [ext]: every base velocity coordinate (world angular, then
 // linear) clamped to +-m_maxCoordinateVelocity after each velocity change.  btClamp's
 // compares, not v_med3 / v_min / v_max: a NaN passes through, as in the oracle (clamp_velocities)
+// a select between two kernel-argument fields by value: the two loads go through an empty asm, so that
+// the optimizer cannot fold them into one load through a selected address (which copies the whole
+// cp_config argument into scratch memory)
+CP_DEV real sel_arg(bool second, float a, float b) {
+    real x = a, y = b;
+    asm volatile("" : "+v"(x), "+v"(y));
+    return second ? y : x;
+}
 CP_DEV real clamp_coord(real a, real lim) { return a < -lim ? -lim : (lim < a ? lim : a); }
-CP_DEV void clamp_velocities(Sim& S, const cp_physics& P) {
+CP_DEV void clamp_body(Body& b, real lim) {
+    b.w = mk(clamp_coord(b.w.x, lim), clamp_coord(b.w.y, lim), clamp_coord(b.w.z, lim));
+    b.v = mk(clamp_coord(b.v.x, lim), clamp_coord(b.v.y, lim), clamp_coord(b.v.z, lim));
+}
+CP_DEV void clamp_velocities(Own& O, const cp_physics& P) {
     const real lim = real(P.max_coord_velocity);
     if (!(lim > real(0.0))) return;  // uniform (a kernel argument)
+    clamp_body(O.c, lim);
+    clamp_body(O.p, lim);
+}
+
+// One body of island ISL (0: the even lane's, 1: the odd lane's) on both lanes of the pair (DPP).
+template <int ISL>
+CP_DEV Body body_of(const Body& b) {
+    Body r;
+    r.x = lane_of3<ISL>(b.x);
+    r.v = lane_of3<ISL>(b.v);
+    r.w = lane_of3<ISL>(b.w);
 #pragma unroll
-    for (int d = 0; d < CP_NUM_DYN; ++d) {
-        S.b[d].w = mk(clamp_coord(S.b[d].w.x, lim), clamp_coord(S.b[d].w.y, lim), clamp_coord(S.b[d].w.z, lim));
-        S.b[d].v = mk(clamp_coord(S.b[d].v.x, lim), clamp_coord(S.b[d].v.y, lim), clamp_coord(S.b[d].v.z, lim));
-    }
+    for (int k = 0; k < 4; ++k) r.q[k] = lane_of<ISL>(b.q[k]);
+    return r;
+}
+// The whole env on both lanes, from the two lanes' Own states (both lanes active).
+CP_DEV Sim env_view(const Own& O) {
+    Sim S;
+    S.b[0] = body_of<0>(O.c);
+    S.b[1] = body_of<0>(O.p);
+    S.b[2] = body_of<1>(O.c);
+    S.b[3] = body_of<1>(O.p);
+    S.f0 = lane_of3<0>(O.f);
+    S.f2 = lane_of3<1>(O.f);
+    return S;
 }
 
 // ---- CP_MODEL_SLEEPING (the SLP kernels): Bullet's deactivation, operation for operation the oracle's
-// body_aabb / sleep_islands / sleep_update (oracle/cp_oracle.c).  Both lanes of an env run
-// them on the whole env, like the velocity update, so they agree without a DPP exchange.
-// AABB of dynamic body D: btTransformAabb of the box grown by the contact breaking threshold
-template <int D>
-CP_DEV void body_aabb(const Sim& S, const cp_physics& P, V3& lo, V3& hi) {
-    const Axes A = quat_axes(S.b[D].q[0], S.b[D].q[1], S.b[D].q[2], S.b[D].q[3]);
-    const real h0 = P.half_extents[D + 1][0], h1 = P.half_extents[D + 1][1], h2 = P.half_extents[D + 1][2];
+// body_aabb / sleep_islands / sleep_update (oracle/cp_oracle.c).  Each lane computes its
+// own bodies' AABBs; the partner's come by DPP, so both lanes run the island pass on identical values.
+// AABB of a body of half extents h: btTransformAabb of the box grown by the contact breaking threshold
+CP_DEV void body_aabb(const Body& B, real h0, real h1, real h2, const cp_physics& P, V3& lo, V3& hi) {
+    const Axes A = quat_axes(B.q[0], B.q[1], B.q[2], B.q[3]);
     const real thr = P.contact_margin;
     const real ex = (h0 * abs_(A.a0.x) + h1 * abs_(A.a1.x)) + h2 * abs_(A.a2.x);
     const real ey = (h0 * abs_(A.a0.y) + h1 * abs_(A.a1.y)) + h2 * abs_(A.a2.y);
     const real ez = (h0 * abs_(A.a0.z) + h1 * abs_(A.a1.z)) + h2 * abs_(A.a2.z);
-    const V3 c = S.b[D].x;
+    const V3 c = B.x;
     lo = mk((c.x - ex) - thr, (c.y - ey) - thr, (c.z - ez) - thr);
     hi = mk((c.x + ex) + thr, (c.y + ey) + thr, (c.z + ez) + thr);
 }
@@ -1188,13 +1208,23 @@ CP_DEV bool aabb_overlap(const V3& la, const V3& ha, const V3& lb, const V3& hb)
     return !(la.x > hb.x || ha.x < lb.x || la.y > hb.y || ha.y < lb.y || la.z > hb.z || ha.z < lb.z);
 }
 // the start of a step: islands of AABB-overlapping bodies and btSimulationIslandManager::buildIslands'
-// activation pass; returns the mask of bodies that sleep this step (bit d = dynamic body d)
-CP_DEV uint32_t sleep_islands(Sim& S, const cp_physics& P) {
+// activation pass; returns the mask of bodies that sleep this step (bit d = dynamic body d, env order)
+CP_DEV uint32_t sleep_islands(Own& O, const cp_physics& P, bool second) {
+    V3 lc, hc, lp, hp;
+    body_aabb(O.c, sel_arg(second, P.half_extents[1][0], P.half_extents[3][0]),
+              sel_arg(second, P.half_extents[1][1], P.half_extents[3][1]),
+              sel_arg(second, P.half_extents[1][2], P.half_extents[3][2]), P, lc, hc);
+    body_aabb(O.p, sel_arg(second, P.half_extents[2][0], P.half_extents[4][0]),
+              sel_arg(second, P.half_extents[2][1], P.half_extents[4][1]),
+              sel_arg(second, P.half_extents[2][2], P.half_extents[4][2]), P, lp, hp);
     V3 lo[CP_NUM_DYN], hi[CP_NUM_DYN];
-    body_aabb<0>(S, P, lo[0], hi[0]);
-    body_aabb<1>(S, P, lo[1], hi[1]);
-    body_aabb<2>(S, P, lo[2], hi[2]);
-    body_aabb<3>(S, P, lo[3], hi[3]);
+    lo[0] = lane_of3<0>(lc); hi[0] = lane_of3<0>(hc);
+    lo[1] = lane_of3<0>(lp); hi[1] = lane_of3<0>(hp);
+    lo[2] = lane_of3<1>(lc); hi[2] = lane_of3<1>(hc);
+    lo[3] = lane_of3<1>(lp); hi[3] = lane_of3<1>(hp);
+    uint32_t act[CP_NUM_DYN];
+    act[0] = lane_of_u<0>(O.sa[0]); act[1] = lane_of_u<0>(O.sa[1]);
+    act[2] = lane_of_u<1>(O.sa[0]); act[3] = lane_of_u<1>(O.sa[1]);
     int root[CP_NUM_DYN] = {0, 1, 2, 3};
 #pragma unroll
     for (int a = 0; a < CP_NUM_DYN; ++a)
@@ -1206,48 +1236,45 @@ CP_DEV uint32_t sleep_islands(Sim& S, const cp_physics& P) {
 #pragma unroll
             for (int d = 0; d < CP_NUM_DYN; ++d) root[d] = (ov && root[d] == hr) ? lr : root[d];
         }
-    uint32_t mask = 0u;
 #pragma unroll
     for (int r = 0; r < CP_NUM_DYN; ++r) {
         bool any_active = false;
 #pragma unroll
-        for (int d = 0; d < CP_NUM_DYN; ++d) any_active |= root[d] == r && (S.slp_a[d] & 15u) == CP_ACT_ACTIVE;
+        for (int d = 0; d < CP_NUM_DYN; ++d) any_active |= root[d] == r && (act[d] & 15u) == CP_ACT_ACTIVE;
 #pragma unroll
         for (int d = 0; d < CP_NUM_DYN; ++d) {
-            const uint32_t aw = S.slp_a[d] & (uint32_t)CP_ACT_AWAKE;
+            const uint32_t aw = act[d] & (uint32_t)CP_ACT_AWAKE;
             const bool mine = root[d] == r;
             const uint32_t na = !any_active ? ((uint32_t)CP_ACT_SLEEPING | aw)
-                              : ((S.slp_a[d] & 15u) == CP_ACT_SLEEPING ? ((uint32_t)CP_ACT_WANTS | aw) : S.slp_a[d]);
-            S.slp_a[d] = mine ? na : S.slp_a[d];
+                              : ((act[d] & 15u) == CP_ACT_SLEEPING ? ((uint32_t)CP_ACT_WANTS | aw) : act[d]);
+            act[d] = mine ? na : act[d];
         }
     }
+    O.sa[0] = second ? act[2] : act[0];
+    O.sa[1] = second ? act[3] : act[1];
+    uint32_t mask = 0u;
 #pragma unroll
-    for (int d = 0; d < CP_NUM_DYN; ++d) mask |= ((S.slp_a[d] & 15u) == CP_ACT_SLEEPING ? 1u : 0u) << d;
+    for (int d = 0; d < CP_NUM_DYN; ++d) mask |= ((act[d] & 15u) == CP_ACT_SLEEPING ? 1u : 0u) << d;
     return mask;
 }
-// the end of a step: btMultiBody::checkMotionAndSleepIfRequired + updateActivationState
-CP_DEV void sleep_update(Sim& S, const cp_physics& P) {
+// the end of a step: btMultiBody::checkMotionAndSleepIfRequired + updateActivationState (own bodies)
+CP_DEV void sleep_body(const Body& B, uint32_t& a, real& t, const cp_physics& P) {
     const real dt = P.dt, eps = P.sleep_epsilon, tmo = P.sleep_timeout;
-#pragma unroll
-    for (int d = 0; d < CP_NUM_DYN; ++d) {
-        const V3 w = S.b[d].w, v = S.b[d].v;
-        const real motion = ((((w.x * w.x + w.y * w.y) + w.z * w.z) + v.x * v.x) + v.y * v.y) + v.z * v.z;
-        uint32_t a = S.slp_a[d];
-        const bool still = motion < eps;
-        const real t = still ? S.slp_t[d] + dt : real(0.0);
-        S.slp_t[d] = t;
-        a = still ? (t > tmo ? (a & ~(uint32_t)CP_ACT_AWAKE) : a) : (a | (uint32_t)CP_ACT_AWAKE);
-        a = (a & (uint32_t)CP_ACT_AWAKE) ? ((uint32_t)CP_ACT_ACTIVE | (uint32_t)CP_ACT_AWAKE)
-            : ((a & 15u) == CP_ACT_ACTIVE ? (uint32_t)CP_ACT_WANTS : a);
-        S.slp_a[d] = a;
-    }
+    const V3 w = B.w, v = B.v;
+    const real motion = ((((w.x * w.x + w.y * w.y) + w.z * w.z) + v.x * v.x) + v.y * v.y) + v.z * v.z;
+    const bool still = motion < eps;
+    t = still ? t + dt : real(0.0);
+    a = still ? (t > tmo ? (a & ~(uint32_t)CP_ACT_AWAKE) : a) : (a | (uint32_t)CP_ACT_AWAKE);
+    a = (a & (uint32_t)CP_ACT_AWAKE) ? ((uint32_t)CP_ACT_ACTIVE | (uint32_t)CP_ACT_AWAKE)
+        : ((a & 15u) == CP_ACT_ACTIVE ? (uint32_t)CP_ACT_WANTS : a);
 }
-CP_DEV void sleep_wake_all(Sim& S) {  // resetBasePositionAndOrientation [ext, low confidence]
-#pragma unroll
-    for (int d = 0; d < CP_NUM_DYN; ++d) {
-        S.slp_a[d] = (uint32_t)CP_ACT_ACTIVE | (uint32_t)CP_ACT_AWAKE;
-        S.slp_t[d] = real(0.0);
-    }
+CP_DEV void sleep_update(Own& O, const cp_physics& P) {
+    sleep_body(O.c, O.sa[0], O.st[0], P);
+    sleep_body(O.p, O.sa[1], O.st[1], P);
+}
+CP_DEV void sleep_wake_all(Own& O) {  // resetBasePositionAndOrientation [ext, low confidence]
+    O.sa[0] = O.sa[1] = (uint32_t)CP_ACT_ACTIVE | (uint32_t)CP_ACT_AWAKE;
+    O.st[0] = O.st[1] = real(0.0);
 }
 
 // whole-env view for the cross rows: positions, velocities and inverse inertias of
@@ -1275,9 +1302,11 @@ CP_DEV Sym lane_of_sym(const Sym& m) {
 CP_DEV void cross_view(Sim& S, Step& T, const Isl& I, bool second) {
     (void)second;
     // island 0's bodies (cart, pole) from the pair's even lane, island 1's (cart2, pole2) from the odd
-    // lane, one DPP move per value on both lanes.  Positions: S.b[*].x already holds them.  Both lanes
-    // of an env load and integrate the whole env identically, and island_view copies the lane's island
-    // out of S, so the partner's island positions equal this lane's S.b[*].x bit for bit.
+    // lane, one DPP move per value on both lanes (S is scratch: each lane holds only its own island)
+    S.b[0].x = lane_of3<0>(opq3(I.d1.x));
+    S.b[1].x = lane_of3<0>(opq3(I.d2.x));
+    S.b[2].x = lane_of3<1>(opq3(I.d1.x));
+    S.b[3].x = lane_of3<1>(opq3(I.d2.x));
     S.b[0].v = lane_of3<0>(I.d1.v);
     S.b[0].w = lane_of3<0>(I.d1.w);
     S.b[1].v = lane_of3<0>(I.d2.v);
@@ -2063,27 +2092,22 @@ CP_DEV void solve_range(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* p
 
 // the lane's island view: its two bodies (cart, pole or cart2, pole2) with their world
 // inverse inertias, and the island's friction products
-CP_DEV void island_view(const Sim& S, const cp_physics& P, int isl_, Ctx& c) {
+CP_DEV void island_view(const Own& O, const cp_physics& P, int isl_, Ctx& c) {
     // the island's constants are rebuilt here from the kernel arguments (a few selects) through
     // an opaque island flag: built once per kernel they stay live across the narrowphase and
     // are spilled there (scratch traffic every substep)
     uint32_t isl = (uint32_t)isl_;
     asm volatile("" : "+v"(isl));
     const Lane L = Lane::make((int)isl, P);
-    const bool second = L.isl != 0;
     Isl& I = c.I;
-    I.d1.x = selv(second, S.b[2].x, S.b[0].x);
-    I.d1.v = selv(second, S.b[2].v, S.b[0].v);
-    I.d1.w = selv(second, S.b[2].w, S.b[0].w);
-    I.d2.x = selv(second, S.b[3].x, S.b[1].x);
-    I.d2.v = selv(second, S.b[3].v, S.b[1].v);
-    I.d2.w = selv(second, S.b[3].w, S.b[1].w);
-    const real cq0 = second ? S.b[2].q[0] : S.b[0].q[0], cq1 = second ? S.b[2].q[1] : S.b[0].q[1];
-    const real cq2 = second ? S.b[2].q[2] : S.b[0].q[2], cq3 = second ? S.b[2].q[3] : S.b[0].q[3];
-    const real pq0 = second ? S.b[3].q[0] : S.b[1].q[0], pq1 = second ? S.b[3].q[1] : S.b[1].q[1];
-    const real pq2 = second ? S.b[3].q[2] : S.b[1].q[2], pq3 = second ? S.b[3].q[3] : S.b[1].q[3];
-    I.d1.M = world_inv_inertia(quat_axes(cq0, cq1, cq2, cq3), L.ii1[0], L.ii1[1], L.ii1[2]);
-    I.d2.M = world_inv_inertia(quat_axes(pq0, pq1, pq2, pq3), L.ii2[0], L.ii2[1], L.ii2[2]);
+    I.d1.x = O.c.x;
+    I.d1.v = O.c.v;
+    I.d1.w = O.c.w;
+    I.d2.x = O.p.x;
+    I.d2.v = O.p.v;
+    I.d2.w = O.p.w;
+    I.d1.M = world_inv_inertia(quat_axes(O.c.q[0], O.c.q[1], O.c.q[2], O.c.q[3]), L.ii1[0], L.ii1[1], L.ii1[2]);
+    I.d2.M = world_inv_inertia(quat_axes(O.p.q[0], O.p.q[1], O.p.q[2], O.p.q[3]), L.ii2[0], L.ii2[1], L.ii2[2]);
     I.im1 = L.im1;
     I.im2 = L.im2;
     c.mu0 = L.mu0;
@@ -2225,7 +2249,7 @@ CP_DEV void pm_refresh(PMan& M, const Box& A, const Box& B, real thr) {
 // the island view and the warm start.  A lane with live == false (done env, padding)
 // makes no contacts and writes nothing.
 template <bool ALLIN = false, bool PM = false, bool SLP = false>
-CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool, real* pool0, int& overflow,
+CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, real* pool, real* pool0, int& overflow,
                          const Mem& G, Stamps& ST, bool live, Ctx& c) {
     const real dt = P.dt, inv_dt = P.inv_dt;
     CP_STAMP(t0);
@@ -2266,17 +2290,49 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
             constexpr int J = decltype(jt)::value;
             constexpr int a0 = pair_a(island_pair_c(0, J)), a1 = pair_a(island_pair_c(1, J));
             constexpr int b0 = pair_b(island_pair_c(0, J)), b1 = pair_b(island_pair_c(1, J));
-            if constexpr (a0 == 0) {  // the static ground: centre 0, identity axes (exact)
-                static_assert(a1 == 0, "ground pairs are ground pairs on both islands");
-                A.c = mk(real(0.0), real(0.0), real(0.0));
+            // the lane's own bodies through opaque copies (each pair rebuilds its boxes: see `sec`)
+            V3 cx = O.c.x, px = O.p.x;
+            real cq[4] = {O.c.q[0], O.c.q[1], O.c.q[2], O.c.q[3]}, pq[4] = {O.p.q[0], O.p.q[1], O.p.q[2], O.p.q[3]};
+            if constexpr (J <= 2) {
+                asm volatile("" : "+v"(cx.x), "+v"(cx.y), "+v"(cx.z), "+v"(cq[0]), "+v"(cq[1]), "+v"(cq[2]), "+v"(cq[3]));
+                asm volatile("" : "+v"(px.x), "+v"(px.y), "+v"(px.z), "+v"(pq[0]), "+v"(pq[1]), "+v"(pq[2]), "+v"(pq[3]));
+            }
+            if constexpr (J == 0 || J == 1) {  // (ground, own cart) / (ground, own pole): the static ground,
+                static_assert(a0 == 0 && a1 == 0, "ground pairs are ground pairs on both islands");  // centre 0,
+                A.c = mk(real(0.0), real(0.0), real(0.0));                                          // identity axes
                 A.ax = quat_axes(real(0.0), real(0.0), real(0.0), real(1.0));
                 A.h0 = P.half_extents[0][0];
                 A.h1 = P.half_extents[0][1];
                 A.h2 = P.half_extents[0][2];
+                if constexpr (J == 0) Bx = box_of<b0, b1>(second, cx, cq, P);
+                else Bx = box_of<b0, b1>(second, px, pq, P);
+            } else if constexpr (J == 2) {     // (own cart, own pole)
+                A = box_of<a0, a1>(second, cx, cq, P);
+                Bx = box_of<b0, b1>(second, px, pq, P);
             } else {
-                A = box_pick<a0, a1>(second, S, P);
+                // cross pairs: island 0 stores (cart, cart2) and (cart, pole2), island 1 (pole, cart2) and
+                // (pole, pole2): A is island 0's own cart or the partner's pole, B the partner's or the own
+                // body; the partner lane's pose by DPP (both lanes execute this uniform branch)
+                V3 rx = J == 3 ? cx : px;
+                real rq[4] = {J == 3 ? cq[0] : pq[0], J == 3 ? cq[1] : pq[1], J == 3 ? cq[2] : pq[2],
+                              J == 3 ? cq[3] : pq[3]};
+                const V3 Pcx = mk(partner(cx.x), partner(cx.y), partner(cx.z));          // partner's cart (J = 3)
+                const V3 Ppx = mk(partner(px.x), partner(px.y), partner(px.z));          // partner's pole
+                real Pcq[4], Ppq[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) { Pcq[k] = partner(cq[k]); Ppq[k] = partner(pq[k]); }
+                // A: island 0 -> own cart, island 1 -> partner's pole
+                real aq[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) aq[k] = second ? Ppq[k] : cq[k];
+                A = box_of<a0, a1>(second, selv(second, Ppx, cx), aq, P);
+                // B: island 0 -> partner's cart2 (J = 3) / pole2 (J = 4), island 1 -> own cart2 / pole2
+                const V3 pbx = J == 3 ? Pcx : Ppx;
+                real bq[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) bq[k] = second ? rq[k] : (J == 3 ? Pcq[k] : Ppq[k]);
+                Bx = box_of<b0, b1>(second, selv(second, rx, pbx), bq, P);
             }
-            Bx = box_pick<b0, b1>(second, S, P);
         });
         Contact C;
         C.m = 0;
@@ -2422,39 +2478,47 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
 #endif
     CP_STAMP(t1);
     CP_ACC(narrow, t0, t1);
-    // 3. unconstrained velocity update (both lanes, whole env)
+    // 3. unconstrained velocity update of the lane's own bodies (island 0's lane: cart, pole)
     const real kl = P.lin_damping, ka = P.ang_damping;
-#pragma unroll
-    for (int d = 0; d < CP_NUM_DYN; ++d) {
-        const int g = d + 1;
-        const real im = P.inv_mass[g];
-        const Axes ax = quat_axes(S.b[d].q[0], S.b[d].q[1], S.b[d].q[2], S.b[d].q[3]);
-        V3 v = S.b[d].v, w = S.b[d].w;
-        V3 F = (d == 0) ? S.f0 : ((d == 2) ? S.f2 : mk(real(0.0), real(0.0), real(0.0)));
+    const bool second_l = L.isl != 0;
+    auto vel_update = [&](Body& B, auto gsel, V3 F, int bit) {
+        constexpr int G0 = decltype(gsel)::value, G1 = G0 + 2;  // cart 1 / 3, pole 2 / 4
+        const real im = sel_arg(second_l, P.inv_mass[G0], P.inv_mass[G1]);
+        const real I0 = sel_arg(second_l, P.inertia[G0][0], P.inertia[G1][0]);
+        const real I1 = sel_arg(second_l, P.inertia[G0][1], P.inertia[G1][1]);
+        const real I2 = sel_arg(second_l, P.inertia[G0][2], P.inertia[G1][2]);
+        const real iI0 = sel_arg(second_l, P.inv_inertia[G0][0], P.inv_inertia[G1][0]);
+        const real iI1 = sel_arg(second_l, P.inv_inertia[G0][1], P.inv_inertia[G1][1]);
+        const real iI2 = sel_arg(second_l, P.inv_inertia[G0][2], P.inv_inertia[G1][2]);
+        const Axes ax = quat_axes(B.q[0], B.q[1], B.q[2], B.q[3]);
+        V3 v = B.v, w = B.w;
         real vlen = sqrt_(dot(v, v));
         real dv = fma_(kl, vlen, kl);
         V3 acc = mk(fma_(-v.x, dv, fma_(F.x, im, real(P.gravity[0]))), fma_(-v.y, dv, fma_(F.y, im, real(P.gravity[1]))),
                     fma_(-v.z, dv, fma_(F.z, im, real(P.gravity[2]))));
         V3 wl = rot_t(ax, w);
-        V3 Iwl = mk(P.inertia[g][0] * wl.x, P.inertia[g][1] * wl.y, P.inertia[g][2] * wl.z);
+        V3 Iwl = mk(I0 * wl.x, I1 * wl.y, I2 * wl.z);
         V3 gl = cross(wl, Iwl);
-        V3 al = mk(-(P.inv_inertia[g][0] * gl.x), -(P.inv_inertia[g][1] * gl.y), -(P.inv_inertia[g][2] * gl.z));
+        V3 al = mk(-(iI0 * gl.x), -(iI1 * gl.y), -(iI2 * gl.z));
         V3 aw = rot(ax, al);
         real wlen = sqrt_(dot(w, w));
         real dw = fma_(ka, wlen, ka);
         V3 accw = mk(fma_(-w.x, dw, aw.x), fma_(-w.y, dw, aw.y), fma_(-w.z, dw, aw.z));
         if constexpr (SLP) {  // CP_MODEL_SLEEPING: no gravity, forces or damping for a sleeping body
-            const bool sd = ((c.slp >> d) & 1u) != 0u;
-            S.b[d].v = selv(sd, v, madd(v, acc, dt));
-            S.b[d].w = selv(sd, w, madd(w, accw, dt));
+            const bool sd = ((c.slp >> bit) & 1u) != 0u;
+            B.v = selv(sd, v, madd(v, acc, dt));
+            B.w = selv(sd, w, madd(w, accw, dt));
         } else {
-            S.b[d].v = madd(v, acc, dt);
-            S.b[d].w = madd(w, accw, dt);
+            (void)bit;
+            B.v = madd(v, acc, dt);
+            B.w = madd(w, accw, dt);
         }
-    }
-    clamp_velocities(S, P);  // the unconstrained update goes through applyDeltaVeeMultiDof(output, dt)
-    S.f0 = mk(real(0.0), real(0.0), real(0.0));  // 6. external forces are consumed by the step
-    S.f2 = mk(real(0.0), real(0.0), real(0.0));
+    };
+    const int bit0 = second_l ? 2 : 0;
+    vel_update(O.c, std::integral_constant<int, 1>{}, O.f, bit0);
+    vel_update(O.p, std::integral_constant<int, 2>{}, mk(real(0.0), real(0.0), real(0.0)), bit0 + 1);
+    clamp_velocities(O, P);  // the unconstrained update goes through applyDeltaVeeMultiDof(output, dt)
+    O.f = mk(real(0.0), real(0.0), real(0.0));  // 6. external forces are consumed by the step
     // 4. solve setup.  No cross-island contact: each lane solves its own island
     //    (oracle: independent islands); otherwise the env is "merged" and its cross
     //    rows run on both lanes.  (DPP reads the partner lane's register: evaluate it
@@ -2474,7 +2538,7 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
     c.used = used;
     c.tot = used + (int)partner_u((uint32_t)used);
     const bool second = L.isl != 0;
-    island_view(S, P, L.isl, c);
+    island_view(O, P, L.isl, c);
     Isl& I = c.I;
     CP_STAMP(t2);
     CP_ACC(vel, t1, t2);
@@ -2487,10 +2551,10 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
     isl_warmstart<1, PM>(I, T, pool);
     isl_warmstart<2, PM>(I, T, pool);
     if (__ballot(c.merged) != 0ull && c.merged) {
-        cross_view(S, T, I, second);
-        pair_warmstart<5, PM>(S, T, second, P, pool0); pair_warmstart<6, PM>(S, T, second, P, pool0);
-        pair_warmstart<7, PM>(S, T, second, P, pool0); pair_warmstart<8, PM>(S, T, second, P, pool0);
-        cross_back(I, S, second);
+        cross_view(X, T, I, second);
+        pair_warmstart<5, PM>(X, T, second, P, pool0); pair_warmstart<6, PM>(X, T, second, P, pool0);
+        pair_warmstart<7, PM>(X, T, second, P, pool0); pair_warmstart<8, PM>(X, T, second, P, pool0);
+        cross_back(I, X, second);
     }
     c.active = c.tot > 0;  // same on both lanes of the env
 }
@@ -2499,23 +2563,16 @@ CP_DEV void substep_prep(Sim& S, const cp_physics& P, const Lane& L, real* pool,
 // env active), the warm-start cache refresh and the integration (DESIGN.md
 // §Physics model 5b-7).
 template <bool PM = false, bool SLP = false>
-CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx& c, real* pool, const Mem& G,
+CP_DEV void substep_finish(Own& O, const cp_physics& P, const Lane& L, const Ctx& c, real* pool, const Mem& G,
                            Stamps& ST, bool live) {
     const real dt = P.dt, inv_dt = P.inv_dt;
     const bool second = L.isl != 0;
     CP_STAMP(t3);
-    {
-        const Isl& I = c.I;  // whole-env velocities: island 0's from the even lane, island 1's from the odd
-        S.b[0].v = lane_of3<0>(I.d1.v);
-        S.b[0].w = lane_of3<0>(I.d1.w);
-        S.b[1].v = lane_of3<0>(I.d2.v);
-        S.b[1].w = lane_of3<0>(I.d2.w);
-        S.b[2].v = lane_of3<1>(I.d1.v);
-        S.b[2].w = lane_of3<1>(I.d1.w);
-        S.b[3].v = lane_of3<1>(I.d2.v);
-        S.b[3].w = lane_of3<1>(I.d2.w);
-    }
-    clamp_velocities(S, P);  // the solver's write-back goes through applyDeltaVeeMultiDof too
+    O.c.v = c.I.d1.v;  // the lane's own island's solved velocities
+    O.c.w = c.I.d1.w;
+    O.p.v = c.I.d2.v;
+    O.p.w = c.I.d2.w;
+    clamp_velocities(O, P);  // the solver's write-back goes through applyDeltaVeeMultiDof too
     // refresh the warm-start cache of the lane's island.  A pair with no point before or after
     // the substep holds 0 impulses and keeps them: it is not rewritten (the id word is a 0xFF-padded prefix,
     // the impulses past it 0, in every state the kernels and cp_init write; oracle: every slot
@@ -2540,15 +2597,14 @@ CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx
                 if (k < cnt) G.sp(pmf(j, 41 + k), pool_n(pool, F_LAM, base + k));
         }
     }
-    // 5. integrate positions and orientations (both lanes, whole env)
+    // 5. integrate positions and orientations of the lane's own bodies
     const real hdt = real(0.5) * dt;
     const real c3 = ((dt * dt) * dt) * (real)0.020833333333;
     const real maxang = P.max_angular_step;
-#pragma unroll
-    for (int d = 0; d < CP_NUM_DYN; ++d) {
-        V3 v = S.b[d].v, w = S.b[d].w;
-        const V3 x0 = S.b[d].x;
-        S.b[d].x = madd(x0, v, dt);
+    auto integrate = [&](Body& B, int bit) {
+        V3 v = B.v, w = B.w;
+        const V3 x0 = B.x;
+        const V3 x1 = madd(x0, v, dt);
         real ang = sqrt_(dot(w, w));
         if (ang * dt > maxang) ang = maxang * inv_dt;
         real half = hdt * ang;
@@ -2557,7 +2613,7 @@ CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx
         if (ang < real(0.001)) s = fma_(-c3, ang * ang, hdt);
         else s = sn / ang;
         real dx = w.x * s, dy = w.y * s, dz = w.z * s, dw = cs;
-        real qx = S.b[d].q[0], qy = S.b[d].q[1], qz = S.b[d].q[2], qw = S.b[d].q[3];
+        real qx = B.q[0], qy = B.q[1], qz = B.q[2], qw = B.q[3];
         real rw = fma_(dw, qw, -fma_(dx, qx, fma_(dy, qy, dz * qz)));
         real rx = fma_(dw, qx, fma_(dx, qw, fma_(dy, qz, -(dz * qy))));
         real ry = fma_(dw, qy, fma_(dy, qw, fma_(dz, qx, -(dx * qz))));
@@ -2565,23 +2621,28 @@ CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx
         real n2 = fma_(rx, rx, fma_(ry, ry, fma_(rz, rz, rw * rw)));
         real inv = real(1.0) / sqrt_(n2);
         if constexpr (SLP) {  // btMultiBodyDynamicsWorld::integrateTransforms: a sleeping body keeps its pose,
-            const bool sd = ((c.slp >> d) & 1u) != 0u;  // its velocities are cleared
+            const bool sd = ((c.slp >> bit) & 1u) != 0u;  // its velocities are cleared
             const V3 z = mk(real(0.0), real(0.0), real(0.0));
-            S.b[d].x = selv(sd, x0, S.b[d].x);
-            S.b[d].v = selv(sd, z, v);
-            S.b[d].w = selv(sd, z, w);
-            S.b[d].q[0] = sd ? qx : rx * inv;
-            S.b[d].q[1] = sd ? qy : ry * inv;
-            S.b[d].q[2] = sd ? qz : rz * inv;
-            S.b[d].q[3] = sd ? qw : rw * inv;
+            B.x = selv(sd, x0, x1);
+            B.v = selv(sd, z, v);
+            B.w = selv(sd, z, w);
+            B.q[0] = sd ? qx : rx * inv;
+            B.q[1] = sd ? qy : ry * inv;
+            B.q[2] = sd ? qz : rz * inv;
+            B.q[3] = sd ? qw : rw * inv;
         } else {
-            S.b[d].q[0] = rx * inv;
-            S.b[d].q[1] = ry * inv;
-            S.b[d].q[2] = rz * inv;
-            S.b[d].q[3] = rw * inv;
+            (void)bit;
+            B.x = x1;
+            B.q[0] = rx * inv;
+            B.q[1] = ry * inv;
+            B.q[2] = rz * inv;
+            B.q[3] = rw * inv;
         }
-    }
-    if constexpr (SLP) sleep_update(S, P);  // updateActivationState, after the integration
+    };
+    const int bit0 = second ? 2 : 0;
+    integrate(O.c, bit0);
+    integrate(O.p, bit0 + 1);
+    if constexpr (SLP) sleep_update(O, P);  // updateActivationState, after the integration
     CP_STAMP(t4);
 #ifndef CP_STAMP_C44
     CP_ACC(integ, t3, t4);
@@ -2599,27 +2660,26 @@ CP_DEV void substep_finish(Sim& S, const cp_physics& P, const Lane& L, const Ctx
 // PM: CP_MODEL_PERSISTENT (Bullet's persistent manifold, per-row normals in the pool).
 // SLP: CP_MODEL_SLEEPING (Bullet's deactivation: sleeping islands are neither integrated nor solved).
 template <bool FAST = false, bool C44 = false, bool ALLIN = C44, bool PM = false, bool SLP = false>
-CP_DEV void substep(Sim& S, const cp_physics& P, const Lane& L, real* pool, real* pool0, int& overflow,
+CP_DEV void substep(Own& O, const cp_physics& P, const Lane& L, real* pool, real* pool0, int& overflow,
                     const Mem& G, Stamps& ST, bool live = true) {
     Ctx c;
+    Sim X;  // scratch: the whole-env view of a merged env's cross rows (cross_view)
     c.slp = 0u;
-    if constexpr (SLP) c.slp = sleep_islands(S, P);
-    substep_prep<ALLIN, PM, SLP>(S, P, L, pool, pool0, overflow, G, ST, live, c);
+    if constexpr (SLP) c.slp = sleep_islands(O, P, L.isl != 0);
+    substep_prep<ALLIN, PM, SLP>(O, X, P, L, pool, pool0, overflow, G, ST, live, c);
     CP_STAMP(t2);
-    solve_range<FAST, C44, PM>(c, S, P, pool, pool0, L.isl != 0, 0, P.solver_iterations, ST);
+    solve_range<FAST, C44, PM>(c, X, P, pool, pool0, L.isl != 0, 0, P.solver_iterations, ST);
     CP_STAMP(t3);
     CP_ACC(solve, t2, t3);
-    substep_finish<PM, SLP>(S, P, L, c, pool, G, ST, live);
+    substep_finish<PM, SLP>(O, P, L, c, pool, G, ST, live);
 }
 
-// LINK_FRAME force at the COM on cart (C = 0) or cart2 (C = 1): world = R(q) f
-template <int C>
-CP_DEV void apply_force_link(Sim& S, real fx, real fy) {
-    const Body& B = S.b[C == 0 ? 0 : 2];
-    Axes A = quat_axes(B.q[0], B.q[1], B.q[2], B.q[3]);
+// LINK_FRAME force at the COM on the lane's own cart (cart on island 0's lane, cart2 on island 1's):
+// world = R(q) f, accumulated until the next substep consumes it
+CP_DEV void apply_force_link(Own& O, real fx, real fy) {
+    Axes A = quat_axes(O.c.q[0], O.c.q[1], O.c.q[2], O.c.q[3]);
     V3 fw = rot(A, mk(fx, fy, real(0.0)));
-    if constexpr (C == 0) S.f0 = add(S.f0, fw);
-    else S.f2 = add(S.f2, fw);
+    O.f = add(O.f, fw);
 }
 
 }  // namespace CP_NS
