@@ -139,23 +139,6 @@ def render_kernel_bytes(H, W, C, R):
     return 2 * H * W * 3 * C * R + 4 * R * 4 * 7 + 4
 
 
-SMALL2_PAIRS = {(1, 1), (1, 2), (1, 3), (1, 4), (1, 6), (2, 1), (2, 2), (2, 3)}   # cp_kernels.hip launch_render
-
-
-def render_kernel_name(H, W, C, R):
-    """The render kernel cp_step launches for this raster configuration (launch_render's choice:
-    the compile-time (C, R) pairs of cp_render_small2_kernel when its LDS fits 48 KB, unless
-    CP_RENDER_V1=1; else the round-3 one-block-per-env kernel, or the wave kernel for large frames)."""
-    npx, nf = H * W, C * R
-    def al(x):
-        return (x + 15) & ~15
-    head = al(al(al(al(R * 4 * 9 * 4) + R * 4 * 3 * 4) + C * R * 4 * 3 * 4) + C * R * 4 * 4 * 2)
-    small2 = al(al(head + R * 32 * 8) + max(npx * 4, 4 * 2 * (24 + 64 * 8 + 24) * 2)) + npx * (2 if nf <= 3 else 4)
-    if (C, R) in SMALL2_PAIRS and os.environ.get("CP_RENDER_V1") != "1" and small2 <= 48 * 1024:
-        return "cp_render_small2_kernel"
-    return "cp_render_small_kernel"
-
-
 def _pmc_files():
     import glob
     return list(reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))))
@@ -678,6 +661,9 @@ SECONDARY = (
     ("C3_bounds_same_step", 65536, 50, {"done_on_bounds": True}, False, 0),
     ("C3_f64", 65536, 200, {"precision": "f64"}, False, 0),
     ("C2_continuous_4096", 4096, 200, {}, True, 0),
+    # the model switch of DESIGN.md §3 (latency-shaped kernels) and C5 (BASELINE configs[4]) in the driver's run
+    ("C3_sleeping", 65536, 200, {"model_flags": abi.CP_MODEL_SLEEPING}, False, 0),
+    ("C5_raster", 65536, 100, {"raster": True}, False, 0),
 )
 
 
@@ -688,6 +674,7 @@ def secondary_lines(dev, R, W=20):
     for name, B, K, kw, continuous, rollout in SECONDARY:
         kw = dict(kw)
         autoreset = kw.pop("autoreset", "same_step")
+        raster = kw.pop("raster", False)
         next_step = autoreset == "next_step"
         w = W + (40 if kw.get("done_on_bounds") else 0)
         if rollout:   # warm-up = one full-window launch, so the timed launch (from the window boundary) has
@@ -695,6 +682,8 @@ def secondary_lines(dev, R, W=20):
         env = BatchedCartpole(B, dev.index, action_repeats=R, steps_per_repeat=1, max_episode_len=WINDOW,
                               initial_force=55.0, autoreset=autoreset, seed=SEED, **kw)
         actions = make_actions(continuous, B, 0, w + K, SEED, dev)
+        if raster:
+            env.enable_raster(True)
         env.reset()
         if rollout:   # warm-up through the kernel itself, its output buffers allocated up front (~2 GB)
             env.reserve_rollout(rollout)
@@ -708,13 +697,26 @@ def secondary_lines(dev, R, W=20):
         torch.cuda.synchronize()
         ep0 = episodes(env)
         p0 = pending(env) if next_step else 0
+        if raster:   # the render kernel's own time (HIP events around each launch): its HBM roofline
+            env.timing_begin(K)
+            env.timing_stride(STEP_EVENT_STRIDE, 1)
         el, _, _ = timed(env, actions, w, K, 1, dev, gather_at_end=False, rollout=rollout)
         sim, ran = simulated_steps(env, B, K, ep0, p0, next_step)
+        rend = {}
+        if raster:
+            tm = env.timing_end()
+            rc = env.raster_cfg
+            ms = tm["render_ms"] / max(1, tm["render_launches"])
+            gbs = B * render_kernel_bytes(rc.height, rc.width, rc.num_cameras, R) / (ms / 1e3) / 1e9
+            rend = {"render_avg_launch_ms": round(ms, 4), "render_achieved_GBps": round(gbs, 1),
+                    "render_hbm_frac": round(gbs / HBM_PEAK_GBS, 4)}
         out[name] = {"value": round(sim / el, 1), "unit": "env-steps/s", "ms_per_step": round(el / K * 1e3, 4),
                      "envs": B, "steps": K, "warmup": w, "resets_in_window": ran,
                      "kernel_shape": dict(zip(("step", "reset"), env.kernel_shape())),
                      **({"rollout_k": rollout} if rollout else {}), **kw,
-                     **({"autoreset": autoreset} if next_step else {})}
+                     **({"autoreset": autoreset} if next_step else {}),
+                     **({"raster": "50x50x3 fp16, 1 camera", "render_kernel": env.render_kernel_name(), **rend}
+                        if raster else {})}
         env.close()
         del actions
         torch.cuda.synchronize()
@@ -965,7 +967,7 @@ def main():
         per_launch_s = tm["render_ms"] / max(1, tm["render_launches"]) / 1e3  # one launch per step
         bytes_launch = B * render_kernel_bytes(rc.height, rc.width, rc.num_cameras, R)
         achieved = bytes_launch / per_launch_s / 1e9
-        kernel = render_kernel_name(rc.height, rc.width, rc.num_cameras, R)
+        kernel = env.render_kernel_name()   # the library's own choice (cp_render_kernel_name)
         traffic, traffic_src = pmc_traffic(kernel, B, R, kind)
     valu = None
     if not args.raster:

@@ -254,6 +254,12 @@ class BatchedCartpole:
         native.check(self.h, self.lib.cp_set_raster(self.h, C.byref(rc), _ptr(self.pixels)), "cp_set_raster")
         return self.pixels
 
+    def render_kernel_name(self):
+        """The render kernel the library launches for this raster configuration
+        (cp_render_kernel_name); None with the raster obs off."""
+        n = self.lib.cp_render_kernel_name(self.h)
+        return n.decode() if n else None
+
     def enable_lqr(self, gains, per_env=False, state8=True, done_pos=0.0, done_angle=0.0):
         """Closed-loop LQR policy (random_action_agent.py:60-135; see cp_set_lqr): every
         substep pushes cart p with action_force * action_p + u_p, u_p = -K_p . s_p from pole

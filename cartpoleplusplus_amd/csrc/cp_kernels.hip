@@ -439,12 +439,14 @@ void cp_destroy(cp_handle* h) {
     delete h;
 }
 
-// raster obs of the envs in list[0 .. *count) (a device count: the grid covers B)
-static int launch_render(cp_handle* h, const int32_t* list, const int32_t* count, hipStream_t st) {
-    hipEvent_t* ev = timing_slot(h, 2);
+// raster obs of the envs in list[0 .. *count) (a device count: the grid covers B).  launch = false only
+// names the kernel the handle would launch (cp_render_kernel_name): 0 small2, 1 small, 2 wave kernel.
+static int launch_render(cp_handle* h, const int32_t* list, const int32_t* count, hipStream_t st,
+                         bool launch = true, int* kind = nullptr) {
+    hipEvent_t* ev = launch ? timing_slot(h, 2) : nullptr;
     if (ev) CP_TRY(h, hipEventRecord(ev[0], st));
     const int C = h->raster.num_cameras, R = h->cfg.action_repeats, npx = h->raster.width * h->raster.height;
-    const uint8_t* cls = reinterpret_cast<const uint8_t*>(h->b.rtable + (size_t)C * npx);
+    const uint8_t* cls = launch ? reinterpret_cast<const uint8_t*>(h->b.rtable + (size_t)C * npx) : nullptr;
     const size_t small = (size_t)cp::render_small_lds(C, R, npx).total;
     // v2 of the small-frame kernel for the common (cameras, repeats) pairs, both compile-time
     auto small2 = [&](auto cc, auto rr) -> bool {
@@ -452,9 +454,10 @@ static int launch_render(cp_handle* h, const int32_t* list, const int32_t* count
         if (C != CC || R != RR || h->render_v1) return false;
         const size_t lds = (size_t)cp::render_small2_lds<CC * RR>(C, R, npx).total;
         if (lds > (size_t)cp::SMALL_LDS_MAX) return false;
-        hipLaunchKernelGGL((cp::cp_render_small2_kernel<CC, RR>), dim3((unsigned)h->cfg.num_envs),
-                           dim3(cp::RENDER_WAVES * cp::WAVE_R), lds, st, h->raster, h->cfg.phys, list, count,
-                           h->b.rposes, h->b.rtable, cls, h->pixels);
+        if (launch)
+            hipLaunchKernelGGL((cp::cp_render_small2_kernel<CC, RR>), dim3((unsigned)h->cfg.num_envs),
+                               dim3(cp::RENDER_WAVES * cp::WAVE_R), lds, st, h->raster, h->cfg.phys, list, count,
+                               h->b.rposes, h->b.rtable, cls, h->pixels);
         return true;
     };
     using I1 = std::integral_constant<int, 1>;
@@ -464,7 +467,10 @@ static int launch_render(cp_handle* h, const int32_t* list, const int32_t* count
     using I6 = std::integral_constant<int, 6>;
     if (small2(I1{}, I3{}) || small2(I1{}, I2{}) || small2(I1{}, I1{}) || small2(I1{}, I4{}) || small2(I1{}, I6{}) ||
         small2(I2{}, I1{}) || small2(I2{}, I2{}) || small2(I2{}, I3{})) {
-        // launched
+        if (kind) *kind = 0;  // launched
+    } else if (!launch) {
+        if (kind) *kind = small <= (size_t)cp::SMALL_LDS_MAX ? 1 : 2;
+        return 0;
     } else if (small <= (size_t)cp::SMALL_LDS_MAX) {  // one block per env, dense ray tests
         hipLaunchKernelGGL(cp::cp_render_small_kernel, dim3((unsigned)h->cfg.num_envs),
                            dim3(cp::RENDER_WAVES * cp::WAVE_R), small, st, h->raster, h->cfg.phys, R, list, count,
@@ -475,9 +481,18 @@ static int launch_render(cp_handle* h, const int32_t* list, const int32_t* count
         hipLaunchKernelGGL(cp::cp_render_kernel, dim3(grid), dim3(cp::RENDER_WAVES * cp::WAVE_R), lds, st, h->raster,
                            h->cfg.phys, R, list, count, h->b.rposes, h->b.rtable, cls, h->pixels);
     }
+    if (!launch) return 0;
     if (check(h, hipGetLastError(), "cp_render_kernel")) return -1;
     if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
     return 0;
+}
+
+const char* cp_render_kernel_name(cp_handle* h) {
+    if (!h || !h->pixels) return nullptr;
+    int kind = -1;
+    if (launch_render(h, nullptr, nullptr, nullptr, false, &kind) != 0) return nullptr;
+    static const char* const names[3] = {"cp_render_small2_kernel", "cp_render_small_kernel", "cp_render_kernel"};
+    return kind >= 0 && kind < 3 ? names[kind] : nullptr;
 }
 
 // the reset list's counter for this call: the one the previous call's reset launch zeroed

@@ -681,33 +681,10 @@ CP_DEV void isl_warmstart(Isl& I, const Step& T, real* pool) {
 #else
 #define CP_ROW_LOOP(k, n) for (int k = 0; k < (n); ++k)
 #endif
-#ifndef CP_EZ_PREFETCH
-#define CP_EZ_PREFETCH 0
-#endif
 template <int J, bool PM = false>
 CP_DEV void isl_normal_rows(Isl& I, const Step& T, real* pool, real tol, bool& bad) {
     const uint32_t pk = T.pk[J];
     const int cnt = pk_cnt(pk), base = pk_base(pk);
-#if CP_EZ_PREFETCH >= 4
-    if constexpr (!PM) {  // the counted loop software-pipelined: row k + 1's operands in flight during row k
-        struct Op { real rx, ry, rz, ie, tg, lam; };
-        auto ld = [&](int s) {
-            s = s < MAXP - 1 ? s : MAXP - 1;
-            return Op{pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s), pool_n(pool, F_IE, s),
-                      pool_n(pool, F_TG, s), pool_n(pool, F_LAM, s)};
-        };
-        Op cur = ld(base);
-        for (int k = 0; k < cnt; ++k) {
-            const Op nxt = ld(base + k + 1);
-            real lam = cur.lam;
-            bad |= isl_row<loc_a<J>(), loc_b<J>(), false>(I, mk(cur.rx, cur.ry, cur.rz), T.n[J], cur.ie, cur.tg, lam,
-                                                          real(0.0), tol);
-            pool_n(pool, F_LAM, base + k) = lam;
-            cur = nxt;
-        }
-        return;
-    }
-#endif
     CP_ROW_LOOP(k, cnt) {
         const int s = base + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
@@ -735,30 +712,6 @@ CP_DEV void isl_friction_rows(Isl& I, const Step& T, real mu, real* pool, real t
         asm volatile("" : "+v"(n.x), "+v"(n.y), "+v"(n.z));
         plane_space(n, t1, t2);
     }
-#if CP_EZ_PREFETCH >= 4
-    if constexpr (!PM) {  // software-pipelined like isl_normal_rows (the normal rows of this sweep are done)
-        struct Op { real rx, ry, rz, ln, ie1, ie2, l1, l2; };
-        auto ld = [&](int s, int fs) {
-            s = s < MAXP - 1 ? s : MAXP - 1;
-            fs = fs < MAXF - 1 ? fs : MAXF - 1;
-            return Op{pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s), pool_n(pool, F_LAM, s),
-                      pool_f(pool, FF_IE1, fs), pool_f(pool, FF_IE2, fs), pool_f(pool, FF_L1, fs), pool_f(pool, FF_L2, fs)};
-        };
-        Op cur = ld(base, fbase);
-        for (int k = 0; k < fcnt; ++k) {
-            const Op nxt = ld(base + k + 1, fbase + k + 1);
-            const V3 rb = mk(cur.rx, cur.ry, cur.rz);
-            const real bound = mu * cur.ln;
-            real l1 = cur.l1, l2 = cur.l2;
-            bad |= isl_row<loc_a<J>(), loc_b<J>(), true>(I, rb, t1, cur.ie1, real(0.0), l1, bound, tol);
-            bad |= isl_row<loc_a<J>(), loc_b<J>(), true>(I, rb, t2, cur.ie2, real(0.0), l2, bound, tol);
-            pool_f(pool, FF_L1, fbase + k) = l1;
-            pool_f(pool, FF_L2, fbase + k) = l2;
-            cur = nxt;
-        }
-        return;
-    }
-#endif
     CP_ROW_LOOP(k, fcnt) {
         const int s = base + k, fs = fbase + k;
         if constexpr (PM) plane_space(pool_normal(pool, s), t1, t2);  // the point's own normal
@@ -777,70 +730,11 @@ CP_DEV void isl_friction_rows(Isl& I, const Step& T, real mu, real* pool, real t
 #define CP_EZ_LOOP(k, n) _Pragma("unroll") for (int k = 0; k < 4; ++k) if (k < (n))
 // The rows of ground pair J (0 or 1) when every lane of the wave with rows on it has a +z
 // normal (wave-uniform choice in sweeps()): the same sweep with isl_row_ez.
-// CP_EZ_PREFETCH: software-pipelined LDS reads.  Each row's operands are read from the pool one row
-// ahead (inside the next row's own guard, so no lane reads a slot it does not own), so the ds_read
-// latency of row k + 1 overlaps row k's dependent VALU chain instead of stalling at its s_waitcnt.
-// No row writes a slot another row of the same loop reads (row k writes only its own lambda), so the
-// values -- and every result -- are those of the plain loop.
-#ifndef CP_EZ_PREFETCH
-#define CP_EZ_PREFETCH 0
-#endif
-// 1: the next row's operands inside the next row's guard; 2: unguarded, the slot clamped into the pool
-// (no branch, no copies); 3: 2 + the first row of the ground-pole loops read at the top of the sweep
-// (no earlier row of the sweep writes them) and the friction bounds taken from the ground-pole normal
-// rows' lambdas in registers (the values those rows store to the pool) instead of re-read.
-struct EzN { real rx, ry, ie, tg, lam; };
-struct EzF { real rx, ry, rz, ie1, ie2, l1, l2, ln; };  // ln: the point's normal impulse (levels 1, 2)
-CP_DEV int clamp_slot(int s, int n) { return s < n - 1 ? s : n - 1; }
-CP_DEV EzN ez_ld_n(real* pool, int s) {
-    return EzN{pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_IE, s), pool_n(pool, F_TG, s),
-               pool_n(pool, F_LAM, s)};
-}
-CP_DEV EzF ez_ld_f(real* pool, int s, int fs) {
-    return EzF{pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s), pool_f(pool, FF_IE1, fs),
-               pool_f(pool, FF_IE2, fs), pool_f(pool, FF_L1, fs), pool_f(pool, FF_L2, fs),
-               CP_EZ_PREFETCH >= 3 ? real(0.0) : pool_n(pool, F_LAM, s)};
-}
-// first normal row / friction point of ground pair J (level 3 preloads them at the top of the sweep)
 template <int J>
-CP_DEV EzN ez_first_n(const Step& T, real* pool) { return ez_ld_n(pool, clamp_slot(pk_base(T.pk[J]), MAXP)); }
-template <int J>
-CP_DEV EzF ez_first_f(const Step& T, real* pool) {
-    return ez_ld_f(pool, clamp_slot(pk_base(T.pk[J]), MAXP), clamp_slot(pk_fbase(T.pk[J]), MAXF));
-}
-
-template <int J>
-CP_DEV void isl_normal_rows_ez(Isl& I, const Step& T, real* pool, real tol, bool& bad, EzN first = EzN{},
-                               real* lam_out = nullptr) {
+CP_DEV void isl_normal_rows_ez(Isl& I, const Step& T, real* pool, real tol, bool& bad) {
     static_assert(loc_a<J>() == 0, "ground pairs only");
     const uint32_t pk = T.pk[J];
     const int cnt = pk_cnt(pk), base = pk_base(pk);
-#if CP_EZ_PREFETCH
-#if CP_EZ_PREFETCH >= 3
-    EzN cur = first;
-#elif CP_EZ_PREFETCH == 2
-    EzN cur = ez_ld_n(pool, clamp_slot(base, MAXP));
-#else
-    EzN cur{};
-    if (cnt > 0) cur = ez_ld_n(pool, base);
-#endif
-    (void)first;
-    CP_EZ_LOOP(k, cnt) {
-#if CP_EZ_PREFETCH >= 2
-        const EzN nxt = ez_ld_n(pool, clamp_slot(base + k + 1, MAXP));
-#else
-        EzN nxt = cur;
-        if (k + 1 < 4 && k + 1 < cnt) nxt = ez_ld_n(pool, base + k + 1);
-#endif
-        real lam = cur.lam;
-        bad |= isl_row_ez<loc_b<J>(), 0, false>(I, mk(cur.rx, cur.ry, real(0.0)), cur.ie, cur.tg, lam, real(0.0), tol);
-        pool_n(pool, F_LAM, base + k) = lam;
-        if (lam_out) lam_out[k] = lam;
-        cur = nxt;
-    }
-#else
-    (void)first;
-    (void)lam_out;
     CP_EZ_LOOP(k, cnt) {
         const int s = base + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
@@ -848,48 +742,14 @@ CP_DEV void isl_normal_rows_ez(Isl& I, const Step& T, real* pool, real tol, bool
         bad |= isl_row_ez<loc_b<J>(), 0, false>(I, rb, pool_n(pool, F_IE, s), pool_n(pool, F_TG, s), lam, real(0.0), tol);
         pool_n(pool, F_LAM, s) = lam;
     }
-#endif
 }
 template <int J>
-CP_DEV void isl_friction_rows_ez(Isl& I, const Step& T, real mu, real* pool, real tol, bool& bad, EzF first = EzF{},
-                                 const real* lam_in = nullptr) {
+CP_DEV void isl_friction_rows_ez(Isl& I, const Step& T, real mu, real* pool, real tol, bool& bad) {
     static_assert(loc_a<J>() == 0, "ground pairs only");
     const uint32_t pk = T.pk[J];
     const int fcnt = pk_fcnt(pk);
     if (fcnt == 0) return;
     const int base = pk_base(pk), fbase = pk_fbase(pk);
-#if CP_EZ_PREFETCH
-#if CP_EZ_PREFETCH >= 3
-    EzF cur = first;
-#else
-    EzF cur = ez_ld_f(pool, base, fbase);
-#endif
-    (void)first;
-    CP_EZ_LOOP(k, fcnt) {
-#if CP_EZ_PREFETCH >= 2
-        const EzF nxt = ez_ld_f(pool, clamp_slot(base + k + 1, MAXP), clamp_slot(fbase + k + 1, MAXF));
-#else
-        EzF nxt = cur;
-        if (k + 1 < 4 && k + 1 < fcnt) nxt = ez_ld_f(pool, base + k + 1, fbase + k + 1);
-#endif
-        // the point's normal impulse: this sweep's value of its normal row (k < fcnt <= cnt)
-#if CP_EZ_PREFETCH >= 3
-        const real ln = lam_in ? lam_in[k] : pool_n(pool, F_LAM, base + k);
-#else
-        const real ln = cur.ln;
-#endif
-        const V3 rb = mk(cur.rx, cur.ry, cur.rz);
-        const real bound = mu * ln;
-        real l1 = cur.l1, l2 = cur.l2;
-        bad |= isl_row_ez<loc_b<J>(), 1, true>(I, rb, cur.ie1, real(0.0), l1, bound, tol);
-        bad |= isl_row_ez<loc_b<J>(), 2, true>(I, rb, cur.ie2, real(0.0), l2, bound, tol);
-        pool_f(pool, FF_L1, fbase + k) = l1;
-        pool_f(pool, FF_L2, fbase + k) = l2;
-        cur = nxt;
-    }
-#else
-    (void)first;
-    (void)lam_in;
     CP_EZ_LOOP(k, fcnt) {
         const int s = base + k, fs = fbase + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
@@ -900,7 +760,6 @@ CP_DEV void isl_friction_rows_ez(Isl& I, const Step& T, real mu, real* pool, rea
         pool_f(pool, FF_L1, fs) = l1;
         pool_f(pool, FF_L2, fs) = l2;
     }
-#endif
 }
 
 // ---- merged solve (an env with a cross-island contact): both lanes run the
@@ -1016,25 +875,6 @@ CP_DEV void pair_normal_rows(Sim& S, const Step& T, bool second, const cp_physic
     const Hdr H = pair_hdr<PAIR>(T, second);
     const uint32_t pk = H.pk;
     const int cnt = pk_cnt(pk), base = pk_base(pk);
-#if CP_EZ_PREFETCH >= 4
-    if constexpr (!PM) {  // software-pipelined (isl_normal_rows): each row writes only its own lambda
-        struct Op { real rx, ry, rz, ie, tg, lam; };
-        auto ld = [&](int s) {
-            s = s < MAXP - 1 ? s : MAXP - 1;
-            return Op{pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s), pool_n(pool, F_IE, s),
-                      pool_n(pool, F_TG, s), pool_n(pool, F_LAM, s)};
-        };
-        Op cur = ld(base);
-        for (int k = 0; k < cnt; ++k) {
-            const Op nxt = ld(base + k + 1);
-            real lam = cur.lam;
-            bad |= solve_row<A, B, false>(S, T, P, mk(cur.rx, cur.ry, cur.rz), H.n, cur.ie, cur.tg, lam, real(0.0), tol);
-            pool_n(pool, F_LAM, base + k) = lam;
-            cur = nxt;
-        }
-        return;
-    }
-#endif
     for (int k = 0; k < cnt; ++k) {
         const int s = base + k;
         V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
@@ -1382,13 +1222,6 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0,
     // has its own normal, the generic rows)
 #ifdef CP_NO_EZ
     const bool ez0 = false, ez1 = false;
-#elif defined(CP_EZ_DYNAMIC)
-    // diagnostic: re-decided every sweep over the lanes still solving (once the tilted-cart lanes have
-    // converged, the capped lanes left run the +z rows)
-    const bool nz0 = pk_cnt(c.T.pk[0]) > 0 && !is_plus_z(c.T.n[0]);
-    const bool nz1 = pk_cnt(c.T.pk[1]) > 0 && !is_plus_z(c.T.n[1]);
-    bool ez0 = !PM && __ballot(nz0) == 0ull;
-    bool ez1 = !PM && __ballot(nz1) == 0ull;
 #else
     const bool ez0 = !PM && __ballot(pk_cnt(c.T.pk[0]) > 0 && !is_plus_z(c.T.n[0])) == 0ull;
     const bool ez1 = !PM && __ballot(pk_cnt(c.T.pk[1]) > 0 && !is_plus_z(c.T.n[1])) == 0ull;
@@ -1440,37 +1273,12 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0,
 #ifdef CP_STAMPS
         ST.sweeps += 1;
 #endif
-#if defined(CP_EZ_DYNAMIC) && !defined(CP_NO_EZ)
-        if (it > it0) {
-            ez0 = !PM && __ballot(c.active && nz0) == 0ull;
-            ez1 = !PM && __ballot(c.active && nz1) == 0ull;
-        }
-#endif
         bool bad = false, badc = false;
-#if CP_EZ_PREFETCH >= 3
-        // the ground-pole pair's first normal row and first friction point, read before any row of the
-        // sweep runs (rows of pair 0 write only their own lambdas; the friction point's bound comes from
-        // lam1 below), so their LDS latency overlaps the ground-cart rows
-        EzN n1{};
-        EzF f1{};
-        real lam1[4] = {real(0.0), real(0.0), real(0.0), real(0.0)};
-#endif
         if (c.active) {
-#if CP_EZ_PREFETCH >= 3
-            if (ez1) {
-                n1 = ez_first_n<1>(c.T, pool);
-                f1 = ez_first_f<1>(c.T, pool);
-            }
-            if (ez0) isl_normal_rows_ez<0>(c.I, c.T, pool, tol, bad, ez_first_n<0>(c.T, pool));
-            else isl_normal_rows<0, PM>(c.I, c.T, pool, tol, bad);
-            if (ez1) isl_normal_rows_ez<1>(c.I, c.T, pool, tol, bad, n1, lam1);
-            else isl_normal_rows<1, PM>(c.I, c.T, pool, tol, bad);
-#else
             if (ez0) isl_normal_rows_ez<0>(c.I, c.T, pool, tol, bad);
             else isl_normal_rows<0, PM>(c.I, c.T, pool, tol, bad);
             if (ez1) isl_normal_rows_ez<1>(c.I, c.T, pool, tol, bad);
             else isl_normal_rows<1, PM>(c.I, c.T, pool, tol, bad);
-#endif
             isl_normal_rows<2, PM>(c.I, c.T, pool, tol, bad);
         }
         const bool cross = c.active && c.merged;  // same on both lanes of an env
@@ -1483,15 +1291,9 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0,
             cross_back(c.I, S, second);
         }
         if (c.active) {
-#if CP_EZ_PREFETCH >= 3
-            if (ez0) isl_friction_rows_ez<0>(c.I, c.T, c.mu0, pool, tol, bad, ez_first_f<0>(c.T, pool));
-            else isl_friction_rows<0, false, PM>(c.I, c.T, c.mu0, pool, tol, bad);
-            if (ez1) isl_friction_rows_ez<1>(c.I, c.T, c.mu1, pool, tol, bad, f1, lam1);
-#else
             if (ez0) isl_friction_rows_ez<0>(c.I, c.T, c.mu0, pool, tol, bad);
             else isl_friction_rows<0, false, PM>(c.I, c.T, c.mu0, pool, tol, bad);
             if (ez1) isl_friction_rows_ez<1>(c.I, c.T, c.mu1, pool, tol, bad);
-#endif
             else if (PM) isl_friction_rows<1, false, PM>(c.I, c.T, c.mu1, pool, tol, bad);
             else isl_friction_rows<1, true>(c.I, c.T, c.mu1, pool, tol, bad, h1, h2);
             isl_friction_rows<2, false, PM>(c.I, c.T, c.mu2, pool, tol, bad);

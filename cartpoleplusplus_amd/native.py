@@ -22,7 +22,7 @@ EXPORTS = (
     "cp_event_record_bytes", "cp_encode_events", "cp_eventlog_open", "cp_eventlog_write", "cp_eventlog_close",
     "cp_set_lqr", "cp_get_stepped", "cp_replay_init", "cp_replay_add", "cp_replay_sample",
     "cp_state_bytes", "cp_set_kernel_shape", "cp_get_kernel_shape", "cp_rollout",
-    "cp_nonfinite_counts",
+    "cp_nonfinite_counts", "cp_render_kernel_name",
 )
 
 _lib = None
@@ -66,6 +66,7 @@ def load():
         "cp_default_raster_config": (None, [P(abi.cp_raster_config)]),
         "cp_set_raster": (I, [VP, P(abi.cp_raster_config), VP]),
         "cp_timing_render": (I, [VP, P(C.c_double), P(C.c_int32)]),
+        "cp_render_kernel_name": (C.c_char_p, [VP]),
         "cp_event_record_bytes": (I, [I, I, I]),
         "cp_encode_events": (I, [VP, I, VP, I, VP, VP, VP, VP, VP, VP, VP, VP, VP]),
         "cp_eventlog_open": (I, [C.c_char_p, I, P(VP)]),

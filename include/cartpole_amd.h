@@ -387,6 +387,12 @@ int cp_set_raster(cp_handle* h, const cp_raster_config* rc, uint16_t* pixels_out
  * of the last cp_timing_begin .. cp_timing_end window: summed ms and launch count. */
 int cp_timing_render(cp_handle* h, double* render_ms, int32_t* render_launches);
 
+/* The name of the render kernel cp_step / cp_reset launch for the handle's raster configuration
+ * (the library's own choice, for profiling: "cp_render_small2_kernel", "cp_render_small_kernel" or
+ * "cp_render_kernel"); NULL when the raster obs is off.  The environment variable CP_RENDER_V1=1 at
+ * cp_create is a diagnostic that forces the round-3 kernel (A/B measurements only). */
+const char* cp_render_kernel_name(cp_handle* h);
+
 /* ---- Event log (--event-log-out) ---------------------
  * Replaces event_log.EventLog (event_log.py:42-99) for B envs: episodes of events
  * in the protobuf wire format of event.proto:1-35, each episode framed by a

@@ -173,3 +173,24 @@ def test_render_v2_equals_v1_every_pixel(monkeypatch, R, C, W, H):
         out.append(torch.stack(frames).view(torch.int16))
         env.close()
     assert torch.equal(out[0], out[1])
+
+
+def test_render_kernel_name_is_the_launchers_choice(monkeypatch):
+    """cp_render_kernel_name reports launch_render's choice: the compile-time (C, R) small2 instances when
+    their LDS fits, the round-3 block kernel otherwise (or with the CP_RENDER_V1 diagnostic), the
+    wave kernel for large frames; None with the raster obs off."""
+    from cartpoleplusplus_amd.batched import BatchedCartpole
+    monkeypatch.delenv("CP_RENDER_V1", raising=False)
+    cases = [(1, 3, 50, 50, "cp_render_small2_kernel"), (2, 3, 50, 50, "cp_render_small2_kernel"),
+             (1, 5, 50, 50, "cp_render_small_kernel"), (1, 2, 160, 120, "cp_render_kernel")]
+    for C_, R, W, H, name in cases:
+        env = BatchedCartpole(8, 0, action_repeats=R)
+        assert env.render_kernel_name() is None
+        env.enable_raster(True, num_cameras=C_, width=W, height=H)
+        assert env.render_kernel_name() == name, (C_, R, W, H, env.render_kernel_name())
+        env.close()
+    monkeypatch.setenv("CP_RENDER_V1", "1")
+    env = BatchedCartpole(8, 0, action_repeats=3)
+    env.enable_raster(True)
+    assert env.render_kernel_name() == "cp_render_small_kernel"
+    env.close()
