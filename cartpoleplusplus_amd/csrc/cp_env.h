@@ -838,6 +838,7 @@ __global__ void __launch_bounds__(256) cp_nextstep_resolve_kernel(cp_config cfg,
 }
 
 // ---------------------------------------------------------------- host launchers
+#ifndef CP_KERNELS_ONLY  // tools/isa_one.sh: one kernel instantiated, no launchers
 static inline unsigned env_grid(int n, int block) { return (unsigned)((n + block - 1) / block); }
 
 void launch_init(const cp_config& cfg, const Bufs& b, hipStream_t st) {
@@ -963,4 +964,5 @@ void launch_step(bool lat, int kind, const cp_config& cfg, const Bufs& b, const 
     }
 }
 
+#endif  // CP_KERNELS_ONLY
 }  // namespace CP_NS

@@ -1368,51 +1368,71 @@ CP_DEV void fast_ground_rows(GRow* R, const Ctx& c, real* pool) {
     }
 }
 
+CP_DEV void fast_cart_pole_rows(CRow* C, const Ctx& c, real* pool) {
+    const uint32_t pk = c.T.pk[2];
+    const int cnt = pk_cnt(pk), base = pk_base(pk);
+    const V3 n = c.T.n[2];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (k < cnt) {
+            const int s = base + k;
+            const V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
+            CRow& R = C[k];
+            R.rbt = cross(rb, n);
+            R.ib = symv(c.I.d2.M, R.rbt);
+            const V3 ra = add(rb, sub(c.I.d2.x, c.I.d1.x));
+            R.rat = cross(ra, n);
+            R.ia = symv(c.I.d1.M, R.rat);
+            R.ie = pool_n(pool, F_IE, s);
+            R.tg = pool_n(pool, F_TG, s);
+            R.lam = pool_n(pool, F_LAM, s);
+        }
+    }
+}
+
+// The rows of the settle-loop structures alone (c4k_ok: local pair 0 in +z form, 0-4 cart-pole rows,
+// nothing else): the latency reset kernels' common case.  Built apart from FastIsl so that only these
+// ~100 values are live through sweeps_c44 / sweeps_c4k (with the whole FastIsl live, the register
+// allocator parked a third of them in AGPRs: 50 v_accvgpr_read per settle sweep of 279 instructions)
+struct FastC4 {
+    GRow g0[4];
+    CRow c2[4];
+};
+// the same for the pole lying on the ground (p1_ok, the step kernels' steady state): pair 0 (0 or 4 rows),
+// pair 1's normal rows and friction points, +z forms (sweeps_p1_fast)
+struct FastP1 {
+    GRow g0[4], g1[4];
+    FRow f1[4];
+};
+
+// local pair 1's friction points (the only island pair with friction rows under the URDF frictions)
+CP_DEV void fast_friction_rows(FRow* Fr, V3& t1, V3& t2, const Ctx& c, real* pool) {
+    const uint32_t pk = c.T.pk[1];
+    const int fcnt = pk_fcnt(pk), base = pk_base(pk), fbase = pk_fbase(pk);
+    plane_space(c.T.n[1], t1, t2);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (k < fcnt) {
+            const int s = base + k, fs = fbase + k;
+            const V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
+            FRow& R = Fr[k];
+            R.rbt1 = cross(rb, t1);
+            R.ib1 = symv(c.I.d2.M, R.rbt1);
+            R.rbt2 = cross(rb, t2);
+            R.ib2 = symv(c.I.d2.M, R.rbt2);
+            R.ie1 = pool_f(pool, FF_IE1, fs);
+            R.ie2 = pool_f(pool, FF_IE2, fs);
+            R.l1 = pool_f(pool, FF_L1, fs);
+            R.l2 = pool_f(pool, FF_L2, fs);
+        }
+    }
+}
+
 CP_DEV void fast_build(FastIsl& F, const Ctx& c, real* pool) {
     fast_ground_rows<0>(F.g0, c, pool);
     fast_ground_rows<1>(F.g1, c, pool);
-    {
-        const uint32_t pk = c.T.pk[2];
-        const int cnt = pk_cnt(pk), base = pk_base(pk);
-        const V3 n = c.T.n[2];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (k < cnt) {
-                const int s = base + k;
-                const V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
-                CRow& R = F.c2[k];
-                R.rbt = cross(rb, n);
-                R.ib = symv(c.I.d2.M, R.rbt);
-                const V3 ra = add(rb, sub(c.I.d2.x, c.I.d1.x));
-                R.rat = cross(ra, n);
-                R.ia = symv(c.I.d1.M, R.rat);
-                R.ie = pool_n(pool, F_IE, s);
-                R.tg = pool_n(pool, F_TG, s);
-                R.lam = pool_n(pool, F_LAM, s);
-            }
-        }
-    }
-    {
-        const uint32_t pk = c.T.pk[1];
-        const int fcnt = pk_fcnt(pk), base = pk_base(pk), fbase = pk_fbase(pk);
-        plane_space(c.T.n[1], F.t1, F.t2);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (k < fcnt) {
-                const int s = base + k, fs = fbase + k;
-                const V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
-                FRow& R = F.f1[k];
-                R.rbt1 = cross(rb, F.t1);
-                R.ib1 = symv(c.I.d2.M, R.rbt1);
-                R.rbt2 = cross(rb, F.t2);
-                R.ib2 = symv(c.I.d2.M, R.rbt2);
-                R.ie1 = pool_f(pool, FF_IE1, fs);
-                R.ie2 = pool_f(pool, FF_IE2, fs);
-                R.l1 = pool_f(pool, FF_L1, fs);
-                R.l2 = pool_f(pool, FF_L2, fs);
-            }
-        }
-    }
+    fast_cart_pole_rows(F.c2, c, pool);
+    fast_friction_rows(F.f1, F.t1, F.t2, c, pool);
 }
 
 // one ground row (A = static ground) on body b: isl_row<0, B, FRICTION> with r x t
@@ -1495,7 +1515,8 @@ CP_DEV bool c44_ok(const Ctx& c) {
 // sweeps_fast when every active lane of the wave has the settle structure: the same rows in
 // the same order (4 ground rows in +z form, then 4 cart-pole rows; no friction, no cross
 // rows), straight-line, without the per-row lane guards of the general loop.
-CP_DEV void sweeps_c44(Ctx& c, FastIsl& F, real tol, int it0, int it1, Stamps& ST) {
+template <class FI>
+CP_DEV void sweeps_c44(Ctx& c, FI& F, real tol, int it0, int it1, Stamps& ST) {
     const V3 n2 = c.T.n[2];
     for (int it = it0; it < it1; ++it) {
         if (__ballot(c.active) == 0ull) break;
@@ -1530,7 +1551,8 @@ CP_DEV bool c4k_ok(const Ctx& c) {
 
 // sweeps_c44 with the cart-pole rows guarded by the lane's own count (the same rows in the same order
 // as sweeps_fast runs them for this structure, without its other pairs' guards and checks)
-CP_DEV void sweeps_c4k(Ctx& c, FastIsl& F, real tol, int it0, int it1, Stamps& ST) {
+template <class FI>
+CP_DEV void sweeps_c4k(Ctx& c, FI& F, real tol, int it0, int it1, Stamps& ST) {
     const V3 n2 = c.T.n[2];
     const int cnt2 = pk_cnt(c.T.pk[2]);
     for (int it = it0; it < it1; ++it) {
@@ -1554,7 +1576,8 @@ CP_DEV void sweeps_c4k(Ctx& c, FastIsl& F, real tol, int it0, int it1, Stamps& S
 }
 
 // sweeps_p1_slow with the rows in fast form (the latency-shaped step kernel)
-CP_DEV void sweeps_p1_fast(Ctx& c, FastIsl& F, real tol, int it0, int it1, Stamps& ST) {
+template <class FI>
+CP_DEV void sweeps_p1_fast(Ctx& c, FI& F, real tol, int it0, int it1, Stamps& ST) {
     const bool cart = pk_cnt(c.T.pk[0]) != 0;
     for (int it = it0; it < it1; ++it) {
         if (__ballot(c.active) == 0ull) break;
@@ -1871,6 +1894,54 @@ CP_DEV void solve_range(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* p
 #ifndef CP_NO_FAST_ROWS
     if constexpr (FAST) {
         if (__ballot(!fast_ok(c)) == 0ull) {
+#if !defined(CP_NO_C44) && !defined(CP_NO_C4K) && !defined(CP_STAMP_C44) && !defined(CP_NO_LEAN_C4)
+            // every active lane of the wave in a settle-loop structure at the first sweep -> the lean rows
+            // (FastC4) and the guard-free loops (in the reset kernels sweeps_fast enters the same loop at it0;
+            // in the step kernels it is the poles standing on their carts)
+#ifdef CP_NO_LEAN_STEP  // diagnostic: the step kernels without the lean structure loops (round-5 A/B)
+            if constexpr (C44) {
+#else
+            {
+#endif
+                if (__ballot(c.active && !c4k_ok(c)) == 0ull) {
+                    const real tol = sqrt_(real(P.residual_threshold));  // oracle: SQRT((real)threshold)
+                    FastC4 F;
+                    fast_ground_rows<0>(F.g0, c, pool);
+                    fast_cart_pole_rows(F.c2, c, pool);
+                    if (__ballot(c.active && !c44_ok(c)) == 0ull) sweeps_c44(c, F, tol, it0, it1, ST);
+                    else sweeps_c4k(c, F, tol, it0, it1, ST);
+                    const int b0 = pk_base(c.T.pk[0]), cnt2 = pk_cnt(c.T.pk[2]), b2 = pk_base(c.T.pk[2]);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {  // fast_store (c4k_ok: 4 rows on pair 0, none on pair 1)
+                        pool_n(pool, F_LAM, b0 + k) = F.g0[k].lam;
+                        if (k < cnt2) pool_n(pool, F_LAM, b2 + k) = F.c2[k].lam;
+                    }
+                    return;
+                }
+            }
+#ifndef CP_NO_LEAN_STEP
+            // the step kernels: every active lane a pole lying or standing on the ground (p1_ok) at the first
+            // sweep -> the lean rows (FastP1), sweeps_p1_fast: the same rows in the same order as sweeps_fast
+            if constexpr (!C44) {
+                if (__ballot(c.active && !p1_ok(c)) == 0ull) {
+                    const real tol = sqrt_(real(P.residual_threshold));
+                    FastP1 F;
+                    V3 t1, t2;
+                    fast_ground_rows<0>(F.g0, c, pool);
+                    fast_ground_rows<1>(F.g1, c, pool);
+                    fast_friction_rows(F.f1, t1, t2, c, pool);
+                    sweeps_p1_fast(c, F, tol, it0, it1, ST);
+                    const int cnt0 = pk_cnt(c.T.pk[0]), b0 = pk_base(c.T.pk[0]), b1 = pk_base(c.T.pk[1]);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {  // fast_store (p1_ok: pair 1 has 4 rows, pair 2 none)
+                        if (k < cnt0) pool_n(pool, F_LAM, b0 + k) = F.g0[k].lam;
+                        pool_n(pool, F_LAM, b1 + k) = F.g1[k].lam;
+                    }
+                    return;
+                }
+            }
+#endif
+#endif
             FastIsl F;
             CP_STAMP(b0);
             fast_build(F, c, pool);
