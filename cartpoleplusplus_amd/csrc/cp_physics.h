@@ -1340,12 +1340,17 @@ struct FRow {
     V3 rbt1, ib1, rbt2, ib2;
     real ie1, ie2, l1, l2;
 };
-struct FastIsl {
-    GRow g0[4], g1[4];  // local pair 0 (ground, cart), 1 (ground, pole)
-    CRow c2[4];         // local pair 2 (cart, pole)
-    FRow f1[4];         // friction points of local pair 1
-    V3 t1, t2;          // their tangents (plane_space of pair 1's normal)
+// HC2 = false: no lane of the wave has cart-pole rows (the pole off its cart: 72 % of a C3 episode's
+// wave-sweeps), the 60 values of c2 are not built (the latency kernels' general loop then needs ~60 fewer
+// registers, which were AGPR moves inside it)
+template <bool HC2 = true>
+struct FastIslT {
+    GRow g0[4], g1[4];      // local pair 0 (ground, cart), 1 (ground, pole)
+    CRow c2[HC2 ? 4 : 1];   // local pair 2 (cart, pole); unused when !HC2
+    FRow f1[4];             // friction points of local pair 1
+    V3 t1, t2;              // their tangents (plane_space of pair 1's normal)
 };
+using FastIsl = FastIslT<true>;
 
 CP_DEV bool fast_ok(const Ctx& c) { return pk_fcnt(c.T.pk[0]) == 0 && pk_fcnt(c.T.pk[2]) == 0; }
 
@@ -1428,10 +1433,11 @@ CP_DEV void fast_friction_rows(FRow* Fr, V3& t1, V3& t2, const Ctx& c, real* poo
     }
 }
 
-CP_DEV void fast_build(FastIsl& F, const Ctx& c, real* pool) {
+template <bool HC2>
+CP_DEV void fast_build(FastIslT<HC2>& F, const Ctx& c, real* pool) {
     fast_ground_rows<0>(F.g0, c, pool);
     fast_ground_rows<1>(F.g1, c, pool);
-    fast_cart_pole_rows(F.c2, c, pool);
+    if constexpr (HC2) fast_cart_pole_rows(F.c2, c, pool);
     fast_friction_rows(F.f1, F.t1, F.t2, c, pool);
 }
 
@@ -1743,8 +1749,8 @@ CP_DEV void sweeps_p1_slow(Ctx& c, real* pool, real tol, int it0, int it1, Stamp
 }
 
 // sweeps() with the island rows in fast form (same row order, same stopping rule)
-template <bool C44>
-CP_DEV void sweeps_fast(Ctx& c, FastIsl& F, Sim& S, const cp_physics& P, real* pool, real* pool0, bool second,
+template <bool C44, bool HC2, bool HX = true>
+CP_DEV void sweeps_fast(Ctx& c, FastIslT<HC2>& F, Sim& S, const cp_physics& P, real* pool, real* pool0, bool second,
                         int it0, int it1, Stamps& ST) {
     const real tol = sqrt_(real(P.residual_threshold));  // oracle: SQRT((real)threshold)
     const int cnt0 = pk_cnt(c.T.pk[0]), cnt1 = pk_cnt(c.T.pk[1]), cnt2 = pk_cnt(c.T.pk[2]);
@@ -1763,7 +1769,7 @@ CP_DEV void sweeps_fast(Ctx& c, FastIsl& F, Sim& S, const cp_physics& P, real* p
         // every still-active lane of the wave in the settle structure: the guard-free loop
         // (the reset kernel's option: there every settle substep is in it; in the step kernel
         // the periodic test cost more than it saved, 0.450 -> 0.480 ms at B = 4,096)
-        if constexpr (C44) {
+        if constexpr (C44 && HC2) {
             if ((it - it0) % CP_C44_CHECK == 0 && __ballot(c.active && !c44_ok(c)) == 0ull) {
                 CP_STAMP(q0);
                 sweeps_c44(c, F, tol, it, it1, ST);
@@ -1818,10 +1824,11 @@ CP_DEV void sweeps_fast(Ctx& c, FastIsl& F, Sim& S, const cp_physics& P, real* p
             }
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if (k < cnt2) bad |= fast_crow(c.I, n2, F.c2[k], F.c2[k].lam, tol);
+                if constexpr (HC2)
+                    if (k < cnt2) bad |= fast_crow(c.I, n2, F.c2[k], F.c2[k].lam, tol);
         }
-        const bool cross = c.active && c.merged;  // same on both lanes of an env
-        if (__ballot(cross) != 0ull && cross) {
+        const bool cross = HX && c.active && c.merged;  // same on both lanes of an env
+        if (HX && __ballot(cross) != 0ull && cross) {
             cross_view(S, c.T, c.I, second);
             pair_normal_rows<5>(S, c.T, second, P, pool0, tol, badc);
             pair_normal_rows<6>(S, c.T, second, P, pool0, tol, badc);
@@ -1855,7 +1862,7 @@ CP_DEV void sweeps_fast(Ctx& c, FastIsl& F, Sim& S, const cp_physics& P, real* p
             }
         }
         const bool crossf = cross && c.xfric;  // see sweeps()
-        if (__ballot(crossf) != 0ull && crossf) {
+        if (HX && __ballot(crossf) != 0ull && crossf) {
             cross_view(S, c.T, c.I, second);
             pair_friction_rows<5>(S, c.T, second, P, pool0, tol, badc);
             pair_friction_rows<6>(S, c.T, second, P, pool0, tol, badc);
@@ -1870,15 +1877,89 @@ CP_DEV void sweeps_fast(Ctx& c, FastIsl& F, Sim& S, const cp_physics& P, real* p
 
 // the island rows' impulses back into the pool (substep_finish refreshes the
 // warm-start cache from it)
-CP_DEV void fast_store(const FastIsl& F, const Ctx& c, real* pool) {
+template <bool HC2>
+CP_DEV void fast_store(const FastIslT<HC2>& F, const Ctx& c, real* pool) {
     const int cnt0 = pk_cnt(c.T.pk[0]), cnt1 = pk_cnt(c.T.pk[1]), cnt2 = pk_cnt(c.T.pk[2]);
     const int b0 = pk_base(c.T.pk[0]), b1 = pk_base(c.T.pk[1]), b2 = pk_base(c.T.pk[2]);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         if (k < cnt0) pool_n(pool, F_LAM, b0 + k) = F.g0[k].lam;
         if (k < cnt1) pool_n(pool, F_LAM, b1 + k) = F.g1[k].lam;
-        if (k < cnt2) pool_n(pool, F_LAM, b2 + k) = F.c2[k].lam;
+        if constexpr (HC2)
+            if (k < cnt2) pool_n(pool, F_LAM, b2 + k) = F.c2[k].lam;
     }
+}
+
+// The lean structure loops: every active lane of the wave in one of the common row structures at the first
+// sweep -> only that structure's rows in fast form (FastC4, FastP1: ~100-120 values, no AGPR moves in the
+// latency kernels) and its guard-free loop, the same rows in the same order as the general loops.
+//   c4k_ok (FastC4, sweeps_c44 / sweeps_c4k): the cart on the ground and 0-4 rows of its pole standing on it:
+//     every island of a reset's settle substeps, ~99 % of the bump substeps', a step's first substeps;
+//   p1_ok (FastP1, sweeps_p1_fast, step kernels): the pole lying or standing on the ground (93-98 % of the
+//     islands from step 26 of an episode on).
+// PRIO (the throughput step kernels): the wave raises its issue priority after CP_PRIO_AFTER sweeps, as sweeps().
+// Returns false (nothing done) when the wave is not uniform.
+template <bool C44, bool PRIO>
+CP_DEV bool solve_lean(Ctx& c, const cp_physics& P, real* pool, int it0, int it1, Stamps& ST) {
+#if !defined(CP_NO_C44) && !defined(CP_NO_C4K) && !defined(CP_STAMP_C44) && !defined(CP_NO_LEAN_C4)
+    const real tol = sqrt_(real(P.residual_threshold));  // oracle: SQRT((real)threshold)
+    // the sweeps in two segments around the priority raise (the loops stop at the first sweep with no
+    // active lane, so the second segment continues exactly where the first left off)
+    const int itp = (PRIO && CP_PRIO_AFTER > 0 && it0 + CP_PRIO_AFTER < it1) ? it0 + CP_PRIO_AFTER : it1;
+    auto run = [&](auto loop) {
+        loop(it0, itp);
+        if constexpr (PRIO) {
+            if (itp < it1 && __ballot(c.active) != 0ull) {
+                __builtin_amdgcn_s_setprio(1);
+                loop(itp, it1);
+                __builtin_amdgcn_s_setprio(0);
+            }
+        }
+    };
+#ifdef CP_NO_LEAN_STEP  // diagnostic: the step kernels without the lean structure loops (round-5 A/B)
+    if constexpr (C44) {
+#else
+    {
+#endif
+        if (__ballot(c.active && !c4k_ok(c)) == 0ull) {
+            FastC4 F;
+            fast_ground_rows<0>(F.g0, c, pool);
+            fast_cart_pole_rows(F.c2, c, pool);
+            if (__ballot(c.active && !c44_ok(c)) == 0ull)
+                run([&](int a, int b) { sweeps_c44(c, F, tol, a, b, ST); });
+            else
+                run([&](int a, int b) { sweeps_c4k(c, F, tol, a, b, ST); });
+            const int b0 = pk_base(c.T.pk[0]), cnt2 = pk_cnt(c.T.pk[2]), b2 = pk_base(c.T.pk[2]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {  // fast_store (c4k_ok: 4 rows on pair 0, none on pair 1)
+                pool_n(pool, F_LAM, b0 + k) = F.g0[k].lam;
+                if (k < cnt2) pool_n(pool, F_LAM, b2 + k) = F.c2[k].lam;
+            }
+            return true;
+        }
+    }
+#ifndef CP_NO_LEAN_STEP
+    if constexpr (!C44) {
+        if (__ballot(c.active && !p1_ok(c)) == 0ull) {
+            FastP1 F;
+            V3 t1, t2;
+            fast_ground_rows<0>(F.g0, c, pool);
+            fast_ground_rows<1>(F.g1, c, pool);
+            fast_friction_rows(F.f1, t1, t2, c, pool);
+            run([&](int a, int b) { sweeps_p1_fast(c, F, tol, a, b, ST); });
+            const int cnt0 = pk_cnt(c.T.pk[0]), b0 = pk_base(c.T.pk[0]), b1 = pk_base(c.T.pk[1]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {  // fast_store (p1_ok: pair 1 has 4 rows, pair 2 none)
+                if (k < cnt0) pool_n(pool, F_LAM, b0 + k) = F.g0[k].lam;
+                pool_n(pool, F_LAM, b1 + k) = F.g1[k].lam;
+            }
+            return true;
+        }
+    }
+#endif
+#endif
+    (void)c; (void)P; (void)pool; (void)it0; (void)it1; (void)ST;
+    return false;
 }
 
 // PGS sweeps [it0, it1) of the lane's island.  FAST: fast-form island rows when no
@@ -1894,53 +1975,27 @@ CP_DEV void solve_range(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* p
 #ifndef CP_NO_FAST_ROWS
     if constexpr (FAST) {
         if (__ballot(!fast_ok(c)) == 0ull) {
-#if !defined(CP_NO_C44) && !defined(CP_NO_C4K) && !defined(CP_STAMP_C44) && !defined(CP_NO_LEAN_C4)
-            // every active lane of the wave in a settle-loop structure at the first sweep -> the lean rows
-            // (FastC4) and the guard-free loops (in the reset kernels sweeps_fast enters the same loop at it0;
-            // in the step kernels it is the poles standing on their carts)
-#ifdef CP_NO_LEAN_STEP  // diagnostic: the step kernels without the lean structure loops (round-5 A/B)
-            if constexpr (C44) {
-#else
-            {
-#endif
-                if (__ballot(c.active && !c4k_ok(c)) == 0ull) {
-                    const real tol = sqrt_(real(P.residual_threshold));  // oracle: SQRT((real)threshold)
-                    FastC4 F;
-                    fast_ground_rows<0>(F.g0, c, pool);
-                    fast_cart_pole_rows(F.c2, c, pool);
-                    if (__ballot(c.active && !c44_ok(c)) == 0ull) sweeps_c44(c, F, tol, it0, it1, ST);
-                    else sweeps_c4k(c, F, tol, it0, it1, ST);
-                    const int b0 = pk_base(c.T.pk[0]), cnt2 = pk_cnt(c.T.pk[2]), b2 = pk_base(c.T.pk[2]);
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {  // fast_store (c4k_ok: 4 rows on pair 0, none on pair 1)
-                        pool_n(pool, F_LAM, b0 + k) = F.g0[k].lam;
-                        if (k < cnt2) pool_n(pool, F_LAM, b2 + k) = F.c2[k].lam;
-                    }
-                    return;
-                }
-            }
-#ifndef CP_NO_LEAN_STEP
-            // the step kernels: every active lane a pole lying or standing on the ground (p1_ok) at the first
-            // sweep -> the lean rows (FastP1), sweeps_p1_fast: the same rows in the same order as sweeps_fast
+            if (solve_lean<C44, false>(c, P, pool, it0, it1, ST)) return;
+#ifndef CP_NO_HC2
+            // the step kernels: no merged env in the wave (61-96 % of a C3 episode's wave-sweeps from step 26 on)
+            // -> the general loop without the cross-row block, and without the cart-pole rows when no lane has
+            // any (the cross block's whole-env view and the 60 cart-pole row values were AGPR moves in it)
             if constexpr (!C44) {
-                if (__ballot(c.active && !p1_ok(c)) == 0ull) {
-                    const real tol = sqrt_(real(P.residual_threshold));
-                    FastP1 F;
-                    V3 t1, t2;
-                    fast_ground_rows<0>(F.g0, c, pool);
-                    fast_ground_rows<1>(F.g1, c, pool);
-                    fast_friction_rows(F.f1, t1, t2, c, pool);
-                    sweeps_p1_fast(c, F, tol, it0, it1, ST);
-                    const int cnt0 = pk_cnt(c.T.pk[0]), b0 = pk_base(c.T.pk[0]), b1 = pk_base(c.T.pk[1]);
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {  // fast_store (p1_ok: pair 1 has 4 rows, pair 2 none)
-                        if (k < cnt0) pool_n(pool, F_LAM, b0 + k) = F.g0[k].lam;
-                        pool_n(pool, F_LAM, b1 + k) = F.g1[k].lam;
+                if (__ballot(c.active && c.merged) == 0ull) {
+                    if (__ballot(c.active && pk_cnt(c.T.pk[2]) > 0) == 0ull) {
+                        FastIslT<false> F;
+                        fast_build(F, c, pool);
+                        sweeps_fast<C44, false, false>(c, F, S, P, pool, pool0, second, it0, it1, ST);
+                        fast_store(F, c, pool);
+                    } else {
+                        FastIsl F;
+                        fast_build(F, c, pool);
+                        sweeps_fast<C44, true, false>(c, F, S, P, pool, pool0, second, it0, it1, ST);
+                        fast_store(F, c, pool);
                     }
                     return;
                 }
             }
-#endif
 #endif
             FastIsl F;
             CP_STAMP(b0);
@@ -1958,6 +2013,14 @@ CP_DEV void solve_range(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* p
 #endif
             return;
         }
+    }
+#endif
+#ifdef CP_LEAN_TP
+    // opt-in diagnostic: the lean structure loops in the throughput step kernels as well (FAST = false: no room
+    // for the whole fast form at 2 waves per SIMD).  Measured slower (round 5: C3 step kernel 0.508 -> 0.528 ms,
+    // scratch 80 -> 120 B/lane; without an env sort only ~23 % of the wave-sweeps are in uniform waves)
+    if constexpr (!C44 && sizeof(real) == 4) {  // (fp64: the lean rows spill there, 240 -> 704 B/lane)
+        if (__ballot(!fast_ok(c)) == 0ull && solve_lean<false, true>(c, P, pool, it0, it1, ST)) return;
     }
 #endif
     sweeps<C44>(c, S, P, pool, pool0, second, it0, it1, ST);
