@@ -346,8 +346,12 @@ struct Contact {
 // ES: skip the edge axes' root where the separation tests cannot pass (below); the throughput-shaped kernels
 // (C3 step kernel -1.1 %; in the latency step kernel it measured +2 %, so those keep the full path)
 template <bool ALLIN = false, bool ES = false>
-CP_DEV void box_box(const Box& A, const Box& B, real margin, real edge_bias, Contact& C) {
+CP_DEV void box_box(const Box& A, const Box& B, real margin, real edge_bias, Contact& C, Stamps& ST) {
+    (void)ST;
     C.m = 0;
+#ifdef CP_STAMP_BB  // diagnostic: box_box's own split (slots sel: face axes, bb: edge axes, rows: contact)
+    CP_STAMP(bb0);
+#endif
     V3 d = sub(B.c, A.c);
     V3 Aax[3] = {A.ax.a0, A.ax.a1, A.ax.a2};
     V3 Bax[3] = {B.ax.a0, B.ax.a1, B.ax.a2};
@@ -383,6 +387,10 @@ CP_DEV void box_box(const Box& A, const Box& B, real margin, real edge_bias, Con
         sep = sep || (s > margin);
         if (s > best) { best = s; kind = 1; bj = j; }
     }
+#ifdef CP_STAMP_BB
+    CP_STAMP(bb1);
+    CP_ACC(sel, bb0, bb1);
+#endif
     if (sep) return;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -414,6 +422,10 @@ CP_DEV void box_box(const Box& A, const Box& B, real margin, real edge_bias, Con
             if (num > (best + edge_bias) * L) { best = num / L; kind = 2; bi = i; bj = j; bax = ax; }
         }
     }
+#ifdef CP_STAMP_BB
+    CP_STAMP(bb2);
+    CP_ACC(bb, bb1, bb2);
+#endif
     if (sep) return;
     if (kind != 2) {
         // face of A (kind 0) or face of B (kind 1) is the reference face
@@ -451,6 +463,10 @@ CP_DEV void box_box(const Box& A, const Box& B, real margin, real edge_bias, Con
             C.d[k] = o.n[k];
             C.ids |= (uint32_t)(o.id[k] + code) << (8 * k);
         }
+#ifdef CP_STAMP_BB
+        CP_STAMP(bb3);
+        CP_ACC(rows, bb2, bb3);
+#endif
         return;
     }
     // edge-edge
@@ -2293,7 +2309,7 @@ CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, rea
         // PM: Bullet's box-box detector reports overlapping boxes only (margin 0); the manifold keeps
         // the points within the pair's relative breaking threshold
         const real newmargin = PM ? real(0.0) : real(P.contact_margin);
-        if (plive && !face_separated(A, Bx, newmargin)) box_box<ALLIN, ES>(A, Bx, newmargin, P.edge_bias, C);
+        if (plive && !face_separated(A, Bx, newmargin)) box_box<ALLIN, ES>(A, Bx, newmargin, P.edge_bias, C, ST);
         PMan M;
         M.cnt = 0;
         if constexpr (PM) {
@@ -2309,7 +2325,7 @@ CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, rea
             }
         }
         CP_STAMP(n2);
-#ifndef CP_STAMP_C44
+#if !defined(CP_STAMP_C44) && !defined(CP_STAMP_BB)
         CP_ACC(sel, n0, n1);
         CP_ACC(bb, n1, n2);
 #endif
@@ -2387,7 +2403,7 @@ CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, rea
         used = base + m;
         fused = fbase + fm;
         CP_STAMP(n3);
-#ifndef CP_STAMP_C44
+#if !defined(CP_STAMP_C44) && !defined(CP_STAMP_BB)
         CP_ACC(rows, n2, n3);
 #endif
         // old point count = the leading non-0xFF bytes of the old id word (written as a prefix)
