@@ -438,6 +438,16 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
     bool want_reset = false;
     bool render_me = false;  // simulated this step: its frames go to the render kernel
     Stamps ST;
+    // the env index through an opaque register copy where the outputs are addressed after the substeps: the
+    // 64-bit per-lane addresses formed once at the top otherwise live through the substep loop (spilled: the
+    // step kernel's scratch frame, written at the top and read back at the end of every launch)
+    auto late_i = [&]() {
+        int x = i;
+#ifndef CP_NO_LATE_I  // diagnostic A/B: the addresses formed once at the top (round 5: scratch 80 B/lane)
+        asm volatile("" : "+v"(x));
+#endif
+        return x;
+    };
     CP_STAMP(k0);
     CP_RT(r0);
     if (inb) {
@@ -500,7 +510,7 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
                     if (readback) {  // 12-states of both poles: the whole env on both lanes (DPP), the lead writes
                         const Sim V = env_view(O);
                         if (lead) {
-                            float* rb = readback + (size_t)i * 2 * R * SR * 12;
+                            float* rb = readback + (size_t)late_i() * 2 * R * SR * 12;
                             readback_pole<1, 1>(V, rb + ((size_t)(0 * R + r) * SR + s) * 12);
                             if (rb_bug) readback_pole<3, 1>(V, rb + ((size_t)(1 * R + r) * SR + s) * 12);
                             else readback_pole<3, 3>(V, rb + ((size_t)(1 * R + r) * SR + s) * 12);
@@ -510,14 +520,16 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
                 if (lead) {
                     float row[14];
                     write_obs_row(O, row);
+                    float* orow = obs_out + ((size_t)late_i() * R + r) * 14;
 #pragma unroll
-                    for (int f = 0; f < 14; ++f) put_out(&obs[r * 14 + f], row[f]);
+                    for (int f = 0; f < 14; ++f) put_out(&orow[f], row[f]);
                 }
-                if (b.rposes) write_rposes_own(O, isl, b.rposes + ((size_t)i * R + r) * CP_NUM_DYN * 7);
+                if (b.rposes) write_rposes_own(O, isl, b.rposes + ((size_t)late_i() * R + r) * CP_NUM_DYN * 7);
             }
             render_me = lead && b.rposes != nullptr;
             ov += (int)partner_u((uint32_t)ov);
-            if (ov && lead) b.overflow[i] += ov;
+            const int il = late_i();
+            if (ov && lead) b.overflow[il] += ov;
             const int steps = ldi(G.st, CP_SF_STEPS, G.off) + 1;
             bool done = steps >= cfg.max_episode_len;
             if (cfg.done_on_bounds && bounds_exceeded(O, cfg)) done = true;
@@ -526,22 +538,24 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
             if constexpr (SLP) store_sleep(O, G, isl);
             const bool fin = env_finite(O);
             if (lead) {
-                if (!fin) b.nonfinite[i] += 1;
+                if (!fin) b.nonfinite[il] += 1;
                 sti(G.st, CP_SF_STEPS, G.off, steps);
-                put_out(&reward_out[i], 1.0f);  // bullet_cartpole.py:260
-                put_out(&done_out[i], (uint8_t)(done ? 1 : 0));
-                const float ret = b.ret_acc[i] + 1.0f;
+                put_out(&reward_out[il], 1.0f);  // bullet_cartpole.py:260
+                put_out(&done_out[il], (uint8_t)(done ? 1 : 0));
+                const float ret = b.ret_acc[il] + 1.0f;
                 if (done) {
-                    b.last_ret[i] = ret;
-                    b.last_len[i] = steps;
-                    b.ret_acc[i] = 0.0f;
-                    for (int f = 0; f < R * 14; ++f) term.st(f, toff, obs[f]);
+                    b.last_ret[il] = ret;
+                    b.last_len[il] = steps;
+                    b.ret_acc[il] = 0.0f;
+                    const float* obs_l = obs_out + (size_t)il * R * 14;
+                    const uint32_t toff_l = SoaF::eoff(il);
+                    for (int f = 0; f < R * 14; ++f) term.st(f, toff_l, obs_l[f]);
                     if (term_out)
-                        for (int f = 0; f < R * 14; ++f) term_out[(size_t)i * R * 14 + f] = obs[f];
+                        for (int f = 0; f < R * 14; ++f) term_out[(size_t)il * R * 14 + f] = obs_l[f];
                     sti(G.st, CP_SF_DONE, G.off, cfg.autoreset == CP_AUTORESET_NEXT_STEP ? 2 + b.npar : 1);
                     want_reset = cfg.autoreset != 0;
                 } else {
-                    b.ret_acc[i] = ret;
+                    b.ret_acc[il] = ret;
                 }
             }
         }

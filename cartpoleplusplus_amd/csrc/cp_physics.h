@@ -1240,7 +1240,9 @@ CP_DEV void sweeps_p1_slow(Ctx& c, real* pool, real tol, int it0, int it1, Stamp
 #ifndef CP_PRIO_MODE
 #define CP_PRIO_MODE 0    // 0: for the rest of that solve; 1, 2: diagnostics (sticky, accumulated)
 #endif
-template <bool C44 = false, bool PM = false>
+// HX = false: no env of the wave is merged (checked by the caller), so the cross-row blocks and the merge of
+// their results into the island view are compiled out of the sweep
+template <bool C44 = false, bool PM = false, bool HX = true>
 CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0, bool second, int it0, int it1,
                    Stamps& ST) {
     const real tol = sqrt_(real(P.residual_threshold));  // oracle: SQRT((real)threshold)
@@ -1313,8 +1315,8 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0,
             else isl_normal_rows<1, PM>(c.I, c.T, pool, tol, bad);
             isl_normal_rows<2, PM>(c.I, c.T, pool, tol, bad);
         }
-        const bool cross = c.active && c.merged;  // same on both lanes of an env
-        if (__ballot(cross) != 0ull && cross) {
+        const bool cross = HX && c.active && c.merged;  // same on both lanes of an env
+        if (HX && __ballot(cross) != 0ull && cross) {
             cross_view(S, c.T, c.I, second);
             pair_normal_rows<5, PM>(S, c.T, second, P, pool0, tol, badc);
             pair_normal_rows<6, PM>(S, c.T, second, P, pool0, tol, badc);
@@ -1333,7 +1335,7 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0,
         // the friction half only where a cross pair has friction rows: cross_view + cross_back alone
         // change no value (the whole-env view and back), and a wave with a merged env pays them per sweep
         const bool crossf = cross && c.xfric;
-        if (__ballot(crossf) != 0ull && crossf) {
+        if (HX && __ballot(crossf) != 0ull && crossf) {
             cross_view(S, c.T, c.I, second);
             pair_friction_rows<5, PM>(S, c.T, second, P, pool0, tol, badc);
             pair_friction_rows<6, PM>(S, c.T, second, P, pool0, tol, badc);
@@ -2053,6 +2055,17 @@ CP_DEV void solve_range(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* p
     // scratch 80 -> 120 B/lane; without an env sort only ~23 % of the wave-sweeps are in uniform waves)
     if constexpr (!C44 && sizeof(real) == 4) {  // (fp64: the lean rows spill there, 240 -> 704 B/lane)
         if (__ballot(!fast_ok(c)) == 0ull && solve_lean<false, true>(c, P, pool, it0, it1, ST)) return;
+    }
+#endif
+#ifdef CP_HX_TP
+    // opt-in diagnostic: the throughput kernels' sweep without the cross-row blocks when no env of the wave is
+    // merged (61-96 % of a C3 episode's wave-sweeps from step 26).  Measured slower (round 5: C3 kernel
+    // 0.503 -> 0.511 ms, driver window -2.5 %): the second copy of the sweep raises the scratch frame 80 -> 112 B
+    if constexpr (!C44 && !PM) {
+        if (__ballot(c.active && c.merged) == 0ull) {
+            sweeps<C44, PM, false>(c, S, P, pool, pool0, second, it0, it1, ST);
+            return;
+        }
     }
 #endif
     sweeps<C44>(c, S, P, pool, pool0, second, it0, it1, ST);
