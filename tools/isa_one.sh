@@ -13,15 +13,15 @@ cat > $T/one.hip <<SRC
 #include "$R/include/cartpole_amd.h"
 #include "$R/cartpoleplusplus_amd/csrc/cp_common.h"
 #define CP_KERNELS_ONLY
-#define CP_NS cp
-#define CP_REAL float
+#define CP_NS ${NS:-cp}
+#define CP_REAL ${REAL:-float}
 #include "$R/cartpoleplusplus_amd/csrc/cp_math.h"
 #include "$R/cartpoleplusplus_amd/csrc/cp_physics.h"
 #include "$R/cartpoleplusplus_amd/csrc/cp_env.h"
 __global__ void one_entry(cp_config cfg, cpc::Bufs b, float* o) { (void)cfg; (void)b; (void)o; }
-void one_launch(cp_config cfg, cpc::Bufs b, void* v, float* o, uint8_t* d, cp::Lqr lq) {
+void one_launch(cp_config cfg, cpc::Bufs b, void* v, float* o, uint8_t* d, cpc::Lqr lq) {
     (void)v; (void)d; (void)lq;
-    hipLaunchKernelGGL((cp::$K), dim3(1), dim3(64), 0, 0, cfg, b, $ARGS);
+    hipLaunchKernelGGL((${NS:-cp}::$K), dim3(1), dim3(64), 0, 0, cfg, b, $ARGS);
 }
 SRC
 /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -ffp-contract=off -fno-slp-vectorize \
