@@ -984,6 +984,11 @@ CP_DEV void pair_dispatch(int j, F&& f) {
         if (j == 0) f(std::integral_constant<int, 0>{});
         else f(std::integral_constant<int, 1>{});
     } else {
+#ifdef CP_NO_GROUND_PEEL  // diagnostic: every pair through this dispatch, the ground pairs included
+        if (j == 0) f(std::integral_constant<int, 0>{});
+        else if (j == 1) f(std::integral_constant<int, 1>{});
+        else
+#endif
         if (j == 2) f(std::integral_constant<int, 2>{});
         else if (j == 3) f(std::integral_constant<int, 3>{});
         else f(std::integral_constant<int, 4>{});
