@@ -39,6 +39,13 @@ constexpr bool kAllinStep = CP_ALLIN_STEP != 0;  // the all-inside face-contact 
 #define CP_STEP_C44 0
 #endif
 constexpr bool kC44Step = CP_STEP_C44 != 0;
+// the throughput-shaped step / reset kernels rebuild the lane's SoA offsets (Mem) per substep and for the epilogue
+// from an opaque env index instead of keeping the ones formed at the top live (round 5; CP_NO_LATE_G: A/B)
+#ifdef CP_NO_LATE_G
+constexpr int kLateG = 0;
+#else
+constexpr int kLateG = 1;
+#endif
 
 using Bufs = cpc::Bufs;
 using Lqr = cpc::Lqr;
@@ -359,6 +366,15 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     const int isl = t & 1;
     const bool lead = isl == 0;
     const int i = b.list[t >> 1];
+    // the env index through an opaque copy where the substeps and the epilogue address the state: the
+    // lane's SoA offsets are rebuilt there instead of living through the 130 substeps (cp_step_kernel)
+    auto late_i = [&]() {
+        int x = i;
+#ifndef CP_NO_LATE_I
+        asm volatile("" : "+v"(x));
+#endif
+        return x;
+    };
     real* pool = lds_pool + threadIdx.x;
     real* pool0 = lds_pool + (threadIdx.x & ~1u);
     const Mem G = Mem::make(b.state, b.scratch, B, i, isl, b.pman);
@@ -384,7 +400,8 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     int ov = 0;
     const int nsub = cfg.settle_steps + cfg.initial_force_steps;
     for (int s = 0; s < nsub; ++s) {
-        substep<LAT && !kF64, true, true, PM, SLP>(O, cfg.phys, L, pool, pool0, ov, G, ST);
+        const Mem Gs = (LAT || kLateG == 0) ? G : Mem::make(b.state, b.scratch, B, late_i(), isl, b.pman);
+        substep<LAT && !kF64, true, true, PM, SLP>(O, cfg.phys, L, pool, pool0, ov, Gs, ST);
         const int k = s - cfg.settle_steps;
         if (k >= 0) {  // bump the lane's own cart (cart, then cart2 in the reference's draw order)
             real fx, fy;
@@ -398,25 +415,27 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     CP_RT(r1);
     flush_stamps(ST, b.stamps + 16, k1 - k0, r0, r1);  // the reset kernel's counters: slots 16-26
 #endif
-    store_own(O, G, isl);  // each lane stores its own island
-    if constexpr (SLP) store_sleep(O, G, isl);
+    const Mem Ge = (LAT || kLateG == 0) ? G : Mem::make(b.state, b.scratch, B, late_i(), isl, b.pman);
+    const int il = late_i();
+    store_own(O, Ge, isl);  // each lane stores its own island
+    if constexpr (SLP) store_sleep(O, Ge, isl);
     const bool fin = env_finite(O);
     const int R = cfg.action_repeats;
     if (b.rposes)  // every repeat slot shows the reset pose (bullet_cartpole.py:342-345)
-        for (int r = 0; r < R; ++r) write_rposes_own(O, isl, b.rposes + ((size_t)i * R + r) * CP_NUM_DYN * 7);
+        for (int r = 0; r < R; ++r) write_rposes_own(O, isl, b.rposes + ((size_t)il * R + r) * CP_NUM_DYN * 7);
     if (!lead) return;
-    b.overflow[i] += ov;
-    if (!fin) b.nonfinite[i] += 1;
+    b.overflow[il] += ov;
+    if (!fin) b.nonfinite[il] += 1;
     float row[14];
     write_obs_row(O, row);
-    float* o = obs_out + (size_t)i * R * 14;
+    float* o = obs_out + (size_t)il * R * 14;
     for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int f = 0; f < 14; ++f) o[r * 14 + f] = row[f];
-    sti(G.st, CP_SF_STEPS, G.off, 0);
-    if (!b.keep_done) sti(G.st, CP_SF_DONE, G.off, 0);  // NEXT_STEP in flight: the fixup kernel clears it
-    sti(G.st, CP_SF_EPISODE, G.off, episode + 1);
-    b.ret_acc[i] = 0.0f;
+    sti(Ge.st, CP_SF_STEPS, Ge.off, 0);
+    if (!b.keep_done) sti(Ge.st, CP_SF_DONE, Ge.off, 0);  // NEXT_STEP in flight: the fixup kernel clears it
+    sti(Ge.st, CP_SF_EPISODE, Ge.off, episode + 1);
+    b.ret_acc[il] = 0.0f;
 }
 
 // LAT: the latency shape of cp_reset_kernel<true> (1 wave per SIMD, 512 registers, fast-form
@@ -498,8 +517,12 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
             }
             for (int r = 0; r < R; ++r) {
                 for (int s = 0; s < SR; ++s) {
+                    // the throughput shape: the lane's SoA offsets rebuilt per substep from the opaque index (not live
+                    // through the loop; scratch 48 -> 24 B/lane); the 0-scratch latency kernels keep G (a lone wave
+                    // pays the rebuild: latency reset list +2.6 %)
+                    const Mem Gs = (LAT || kLateG == 0) ? G : Mem::make(b.state, b.scratch, B, late_i(), isl, b.pman);
                     substep<LAT && !kF64, kC44Step && !LAT && !kF64 && !PM, kAllinStep, PM, SLP>(O, cfg.phys, L, pool,
-                                                                                                   pool0, ov, G, ST);
+                                                                                                   pool0, ov, Gs, ST);
                     if constexpr (LQR) {  // disturbance + control (:897-901), control from the pre-step state
                         apply_force_link(O, fa + u[0], fb + u[1]);
                         float* s8 = lq.state8 ? lq.state8 + (((size_t)i * R + r) * SR + s) * 16 : nullptr;
@@ -530,16 +553,17 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
             ov += (int)partner_u((uint32_t)ov);
             const int il = late_i();
             if (ov && lead) b.overflow[il] += ov;
-            const int steps = ldi(G.st, CP_SF_STEPS, G.off) + 1;
+            const Mem Ge = (LAT || kLateG == 0) ? G : Mem::make(b.state, b.scratch, B, il, isl, b.pman);
+            const int steps = ldi(Ge.st, CP_SF_STEPS, Ge.off) + 1;
             bool done = steps >= cfg.max_episode_len;
             if (cfg.done_on_bounds && bounds_exceeded(O, cfg)) done = true;
             if (LQR && lqr_done) done = true;
-            store_own(O, G, isl);  // each lane stores its own island
-            if constexpr (SLP) store_sleep(O, G, isl);
+            store_own(O, Ge, isl);  // each lane stores its own island
+            if constexpr (SLP) store_sleep(O, Ge, isl);
             const bool fin = env_finite(O);
             if (lead) {
                 if (!fin) b.nonfinite[il] += 1;
-                sti(G.st, CP_SF_STEPS, G.off, steps);
+                sti(Ge.st, CP_SF_STEPS, Ge.off, steps);
                 put_out(&reward_out[il], 1.0f);  // bullet_cartpole.py:260
                 put_out(&done_out[il], (uint8_t)(done ? 1 : 0));
                 const float ret = b.ret_acc[il] + 1.0f;
@@ -552,7 +576,7 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
                     for (int f = 0; f < R * 14; ++f) term.st(f, toff_l, obs_l[f]);
                     if (term_out)
                         for (int f = 0; f < R * 14; ++f) term_out[(size_t)il * R * 14 + f] = obs_l[f];
-                    sti(G.st, CP_SF_DONE, G.off, cfg.autoreset == CP_AUTORESET_NEXT_STEP ? 2 + b.npar : 1);
+                    sti(Ge.st, CP_SF_DONE, Ge.off, cfg.autoreset == CP_AUTORESET_NEXT_STEP ? 2 + b.npar : 1);
                     want_reset = cfg.autoreset != 0;
                 } else {
                     b.ret_acc[il] = ret;
