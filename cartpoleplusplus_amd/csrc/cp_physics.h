@@ -2062,6 +2062,13 @@ CP_DEV void solve_range(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* p
         if (__ballot(!fast_ok(c)) == 0ull && solve_lean<false, true>(c, P, pool, it0, it1, ST)) return;
     }
 #endif
+#ifndef CP_NO_LEAN_TR
+    // the throughput-shaped (burst) reset kernel: its settle and bump substeps are one structure in (nearly) every
+    // wave, so the lean settle rows (FastC4, ~100 values) in registers instead of the LDS-row settle loop
+    if constexpr (C44 && !FAST && !PM && sizeof(real) == 4) {
+        if (__ballot(!fast_ok(c)) == 0ull && solve_lean<true, false>(c, P, pool, it0, it1, ST)) return;
+    }
+#endif
 #ifdef CP_HX_TP
     // opt-in diagnostic: the throughput kernels' sweep without the cross-row blocks when no env of the wave is
     // merged (61-96 % of a C3 episode's wave-sweeps from step 26).  Measured slower (round 5: C3 kernel
