@@ -2054,6 +2054,12 @@ CP_DEV void solve_range(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* p
         }
     }
 #endif
+#ifdef CP_LEAN_F64
+    // diagnostic: the lean structure loops in the fp64 step kernels (1 wave per SIMD, 512 registers)
+    if constexpr (!C44 && !PM && sizeof(real) == 8) {
+        if (__ballot(!fast_ok(c)) == 0ull && solve_lean<false, false>(c, P, pool, it0, it1, ST)) return;
+    }
+#endif
 #ifdef CP_LEAN_TP
     // opt-in diagnostic: the lean structure loops in the throughput step kernels as well (FAST = false: no room
     // for the whole fast form at 2 waves per SIMD).  Measured slower (round 5: C3 step kernel 0.508 -> 0.528 ms,
@@ -2065,7 +2071,7 @@ CP_DEV void solve_range(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* p
 #ifndef CP_NO_LEAN_TR
     // the throughput-shaped (burst) reset kernel: its settle and bump substeps are one structure in (nearly) every
     // wave, so the lean settle rows (FastC4, ~100 values) in registers instead of the LDS-row settle loop
-    if constexpr (C44 && !FAST && !PM && sizeof(real) == 4) {
+    if constexpr (C44 && !FAST && !PM) {  // (fp64: the latency-shaped reset kernel, 512 registers)
         if (__ballot(!fast_ok(c)) == 0ull && solve_lean<true, false>(c, P, pool, it0, it1, ST)) return;
     }
 #endif
