@@ -400,7 +400,7 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     int ov = 0;
     const int nsub = cfg.settle_steps + cfg.initial_force_steps;
     for (int s = 0; s < nsub; ++s) {
-        const Mem Gs = (LAT || kLateG == 0) ? G : Mem::make(b.state, b.scratch, B, late_i(), isl, b.pman);
+        const Mem Gs = ((LAT && !kF64) || kLateG == 0) ? G : Mem::make(b.state, b.scratch, B, late_i(), isl, b.pman);
         substep<LAT && !kF64, true, true, PM, SLP>(O, cfg.phys, L, pool, pool0, ov, Gs, ST);
         const int k = s - cfg.settle_steps;
         if (k >= 0) {  // bump the lane's own cart (cart, then cart2 in the reference's draw order)
@@ -415,7 +415,7 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     CP_RT(r1);
     flush_stamps(ST, b.stamps + 16, k1 - k0, r0, r1);  // the reset kernel's counters: slots 16-26
 #endif
-    const Mem Ge = (LAT || kLateG == 0) ? G : Mem::make(b.state, b.scratch, B, late_i(), isl, b.pman);
+    const Mem Ge = ((LAT && !kF64) || kLateG == 0) ? G : Mem::make(b.state, b.scratch, B, late_i(), isl, b.pman);
     const int il = late_i();
     store_own(O, Ge, isl);  // each lane stores its own island
     if constexpr (SLP) store_sleep(O, Ge, isl);
@@ -520,7 +520,7 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
                     // the throughput shape: the lane's SoA offsets rebuilt per substep from the opaque index (not live
                     // through the loop; scratch 48 -> 24 B/lane); the 0-scratch latency kernels keep G (a lone wave
                     // pays the rebuild: latency reset list +2.6 %)
-                    const Mem Gs = (LAT || kLateG == 0) ? G : Mem::make(b.state, b.scratch, B, late_i(), isl, b.pman);
+                    const Mem Gs = ((LAT && !kF64) || kLateG == 0) ? G : Mem::make(b.state, b.scratch, B, late_i(), isl, b.pman);
                     substep<LAT && !kF64, kC44Step && !LAT && !kF64 && !PM, kAllinStep, PM, SLP>(O, cfg.phys, L, pool,
                                                                                                    pool0, ov, Gs, ST);
                     if constexpr (LQR) {  // disturbance + control (:897-901), control from the pre-step state
@@ -553,7 +553,7 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
             ov += (int)partner_u((uint32_t)ov);
             const int il = late_i();
             if (ov && lead) b.overflow[il] += ov;
-            const Mem Ge = (LAT || kLateG == 0) ? G : Mem::make(b.state, b.scratch, B, il, isl, b.pman);
+            const Mem Ge = ((LAT && !kF64) || kLateG == 0) ? G : Mem::make(b.state, b.scratch, B, il, isl, b.pman);
             const int steps = ldi(Ge.st, CP_SF_STEPS, Ge.off) + 1;
             bool done = steps >= cfg.max_episode_len;
             if (cfg.done_on_bounds && bounds_exceeded(O, cfg)) done = true;
