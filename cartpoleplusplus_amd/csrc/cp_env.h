@@ -144,6 +144,9 @@ CP_DEV void load_own(Own& O, const Mem& G, int isl) {
     load_body(O.c, G.st, CP_SF_BODY(0, 0), ob);
     load_body(O.p, G.st, CP_SF_BODY(1, 0), ob);
     O.f = mk(G.st.ld(CP_SF_PENDING(0, 0), of), G.st.ld(CP_SF_PENDING(0, 1), of), G.st.ld(CP_SF_PENDING(0, 2), of));
+    O.wsm = 0u;  // the island's warm-start id words' point counts (pair_body)
+#pragma unroll
+    for (int j = 0; j < CP_ISLAND_PAIRS; ++j) O.wsm |= ws_count(to_bits(G.lw(CP_SF_WS_ID(0, j)))) << (3 * j);
 }
 CP_DEV void store_own(const Own& O, const Mem& G, int isl) {
     const uint32_t ob = isl_off(G, isl, 2 * CP_BODY_FIELDS), of = isl_off(G, isl, 3);
@@ -397,6 +400,7 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) G.sl(CP_SF_WS_LAM(0, j, k), real(0.0));
     }
+    O.wsm = 0u;
     int ov = 0;
     const int nsub = cfg.settle_steps + cfg.initial_force_steps;
     for (int s = 0; s < nsub; ++s) {
@@ -778,6 +782,7 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
                         for (int q = 0; q < 4; ++q) G.sl(CP_SF_WS_LAM(0, j, q), real(0.0));
                         if constexpr (PM) G.sp(pmf(j, 0), bits_to<real>(0u));
                     }
+                    O.wsm = 0u;
                     stc(RC_SUB, 0);
                     stc(RC_STEPS, steps);
                     stc(RC_FLAGS, (int)(flags | RF_RESETTING));

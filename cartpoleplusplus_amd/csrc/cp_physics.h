@@ -84,9 +84,20 @@ struct Sim {
 struct Own {
     Body c, p;        // the island's cart and pole
     V3 f;             // pending world force on the island's cart (pybullet force accumulator)
+    uint32_t wsm;     // 3 bits per local pair: the point count of the pair's warm-start id word (ws_count)
     uint32_t sa[2];   // CP_MODEL_SLEEPING (SLP kernels only): activation words of c, p (CP_ACT_* | CP_ACT_AWAKE)
     real st[2];       //   and their sleep timers
 };
+
+// The point count of a warm-start id word: its leading non-0xFF bytes when the word is a prefix (ids, then
+// 0xFF padding: every word the kernels and cp_init write), 7 for any other word (a state set from outside),
+// which makes the pair's cache rewritten like a changed one.
+CP_DEV uint32_t ws_count(uint32_t id) {
+    const uint32_t b0 = id & 0xFFu, b1 = (id >> 8) & 0xFFu, b2 = (id >> 16) & 0xFFu, b3 = id >> 24;
+    const uint32_t n = b0 == 0xFFu ? 0u : b1 == 0xFFu ? 1u : b2 == 0xFFu ? 2u : b3 == 0xFFu ? 3u : 4u;
+    const uint32_t pad = n >= 4u ? 0u : 0xFFFFFFFFu << (8u * n);  // the bytes past the prefix
+    return (id & pad) == pad ? n : 7u;
+}
 
 // Per-env global memory touched once per substep (cold data kept out of VGPRs):
 // the warm-start cache lives in the state SoA (SoaT: buffer-resource access, cp_common.h).
@@ -2270,14 +2281,17 @@ CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, rea
             plive = live && !(((c.slp >> (bb - 1)) & 1u) || (a > 0 && ((c.slp >> (a - 1)) & 1u)));
         }
         CP_STAMP(n0);
-        // warm-start cache of the pair, loaded first: its latency overlaps the narrowphase
+        // warm-start cache of the pair (CP_NO_WSM: loaded first for every pair, its latency overlapping the
+        // narrowphase; else loaded below for the pairs past the broadphase only, the old point count from O.wsm)
         uint32_t oid = 0xFFFFFFFFu;
         real ol0 = real(0.0), ol1 = real(0.0), ol2 = real(0.0), ol3 = real(0.0);
+#ifdef CP_NO_WSM
         if constexpr (!PM) {
             oid = to_bits(G.lw(CP_SF_WS_ID(0, j)));
             ol0 = G.ll(CP_SF_WS_LAM(0, j, 0)); ol1 = G.ll(CP_SF_WS_LAM(0, j, 1));
             ol2 = G.ll(CP_SF_WS_LAM(0, j, 2)); ol3 = G.ll(CP_SF_WS_LAM(0, j, 3));
         }
+#endif
         // the island flag through a volatile empty asm per pair: the box selections below are
         // otherwise loop-invariant per branch, and hoisting all of them out of the pair loop
         // keeps every body's axes live across the narrowphase (spills)
@@ -2340,7 +2354,19 @@ CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, rea
         // PM: Bullet's box-box detector reports overlapping boxes only (margin 0); the manifold keeps
         // the points within the pair's relative breaking threshold
         const real newmargin = PM ? real(0.0) : real(P.contact_margin);
-        if (plive && !face_separated(A, Bx, newmargin)) box_box<ALLIN, ES>(A, Bx, newmargin, P.edge_bias, C, ST);
+        const bool near = plive && !face_separated(A, Bx, newmargin);
+#ifndef CP_NO_WSM
+        // a pair the broadphase separates makes no point: its cache is not read (m = 0, the id word's old count
+        // from O.wsm decides the rewrite below); the others load it here, its latency overlapping box_box
+        if constexpr (!PM) {
+            if (near) {
+                oid = to_bits(G.lw(CP_SF_WS_ID(0, j)));
+                ol0 = G.ll(CP_SF_WS_LAM(0, j, 0)); ol1 = G.ll(CP_SF_WS_LAM(0, j, 1));
+                ol2 = G.ll(CP_SF_WS_LAM(0, j, 2)); ol3 = G.ll(CP_SF_WS_LAM(0, j, 3));
+            }
+        }
+#endif
+        if (near) box_box<ALLIN, ES>(A, Bx, newmargin, P.edge_bias, C, ST);
         PMan M;
         M.cnt = 0;
         if constexpr (PM) {
@@ -2438,8 +2464,17 @@ CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, rea
         CP_ACC(rows, n2, n3);
 #endif
         // old point count = the leading non-0xFF bytes of the old id word (written as a prefix)
+#ifdef CP_NO_WSM
         const int om = (oid & 0xFFu) == 0xFFu ? 0 : ((oid >> 8) & 0xFFu) == 0xFFu ? 1
                      : ((oid >> 16) & 0xFFu) == 0xFFu ? 2 : ((oid >> 24) & 0xFFu) == 0xFFu ? 3 : 4;
+        const bool idw = nid != oid;
+#else
+        const int om = (int)((O.wsm >> (3 * j)) & 7u);
+        // the id word changes when the new prefix differs from the old word: loaded when near; a separated pair's
+        // new word is all 0xFF, which differs from the old exactly when that held a point or was not a prefix
+        const bool idw = near ? nid != oid : om > 0;
+        if (!PM && plive) O.wsm = (O.wsm & ~(7u << (3 * j))) | ((uint32_t)m << (3 * j));
+#endif
         const uint32_t pk = (uint32_t)m | ((uint32_t)base << 3) | ((uint32_t)fm << 8) | ((uint32_t)fbase << 11) |
                             ((uint32_t)(plive ? (m > om ? m : om) : 0) << 16);
 #ifdef CP_HDR_SCRATCH
@@ -2457,7 +2492,7 @@ CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, rea
             T.pk[q] = h ? pk : T.pk[q];
         }
 #endif
-        if (!PM && plive && nid != oid) G.sw(CP_SF_WS_ID(0, j), bits_to<real>(nid));  // unchanged: no write
+        if (!PM && plive && idw) G.sw(CP_SF_WS_ID(0, j), bits_to<real>(nid));  // unchanged: no write
     };
 #ifdef CP_NO_GROUND_PEEL
 #pragma unroll 1
