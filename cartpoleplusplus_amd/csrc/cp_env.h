@@ -471,6 +471,15 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
 #endif
         return x;
     };
+    // the lane's island (lane parity) recomputed from the lane id where the late offsets need it (a kept copy
+    // and the island offsets derived from it were spilled)
+    auto late_isl = [&]() {
+#if defined(CP_NO_LATE_I) || defined(CP_NO_LATE_ISL)
+        return isl;
+#else
+        return (int)(__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) & 1u);
+#endif
+    };
     CP_STAMP(k0);
     CP_RT(r0);
     if (inb) {
@@ -524,7 +533,7 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
                     // the throughput shape: the lane's SoA offsets rebuilt per substep from the opaque index (not live
                     // through the loop; scratch 48 -> 24 B/lane); the 0-scratch latency kernels keep G (a lone wave
                     // pays the rebuild: latency reset list +2.6 %)
-                    const Mem Gs = ((LAT && !kF64) || kLateG == 0) ? G : Mem::make(b.state, b.scratch, B, late_i(), isl, b.pman);
+                    const Mem Gs = ((LAT && !kF64) || kLateG == 0) ? G : Mem::make(b.state, b.scratch, B, late_i(), late_isl(), b.pman);
                     substep<LAT && !kF64, kC44Step && !LAT && !kF64 && !PM, kAllinStep, PM, SLP>(O, cfg.phys, L, pool,
                                                                                                    pool0, ov, Gs, ST);
                     if constexpr (LQR) {  // disturbance + control (:897-901), control from the pre-step state
@@ -557,13 +566,14 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
             ov += (int)partner_u((uint32_t)ov);
             const int il = late_i();
             if (ov && lead) b.overflow[il] += ov;
-            const Mem Ge = ((LAT && !kF64) || kLateG == 0) ? G : Mem::make(b.state, b.scratch, B, il, isl, b.pman);
+            const int isle = ((LAT && !kF64) || kLateG == 0) ? isl : late_isl();
+            const Mem Ge = ((LAT && !kF64) || kLateG == 0) ? G : Mem::make(b.state, b.scratch, B, il, isle, b.pman);
             const int steps = ldi(Ge.st, CP_SF_STEPS, Ge.off) + 1;
             bool done = steps >= cfg.max_episode_len;
             if (cfg.done_on_bounds && bounds_exceeded(O, cfg)) done = true;
             if (LQR && lqr_done) done = true;
-            store_own(O, Ge, isl);  // each lane stores its own island
-            if constexpr (SLP) store_sleep(O, Ge, isl);
+            store_own(O, Ge, isle);  // each lane stores its own island
+            if constexpr (SLP) store_sleep(O, Ge, isle);
             const bool fin = env_finite(O);
             if (lead) {
                 if (!fin) b.nonfinite[il] += 1;
