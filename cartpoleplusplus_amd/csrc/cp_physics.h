@@ -969,7 +969,7 @@ __host__ __device__ constexpr int island_pair_c(int isl, int j) {
 // Box of a body with the half extents of dynamic body G0 (island 0 lanes) or G1 (island 1 lanes): the
 // axes are rebuilt from the quaternion here rather than kept live through the narrowphase (same
 // arithmetic as the per-body quat_axes / world_inv_inertia).
-template <int G0, int G1>
+template <int G0, int G1, bool AX = true>
 CP_DEV Box box_of(bool second, const V3& x, const real q[4], const cp_physics& P) {
     static_assert(G0 >= 1 && G1 >= 1, "dynamic bodies only");
     Box b;
@@ -977,7 +977,8 @@ CP_DEV Box box_of(bool second, const V3& x, const real q[4], const cp_physics& P
     b.h1 = second ? real(P.half_extents[G1][1]) : real(P.half_extents[G0][1]);
     b.h2 = second ? real(P.half_extents[G1][2]) : real(P.half_extents[G0][2]);
     b.c = x;
-    b.ax = quat_axes(q[0], q[1], q[2], q[3]);
+    if constexpr (AX) b.ax = quat_axes(q[0], q[1], q[2], q[3]);
+    else b.ax = quat_axes(real(0.0), real(0.0), real(0.0), real(1.0));  // placeholder (pair_body: late B axes)
     return b;
 }
 template <int G0, int G1>
@@ -1390,6 +1391,12 @@ struct FRow {
     V3 rbt1, ib1, rbt2, ib2;
     real ie1, ie2, l1, l2;
 };
+// pair_body: B's box axes built after the broadphase, for the lanes it passes (CP_NO_LATE_BAX: A/B)
+#ifdef CP_NO_LATE_BAX
+constexpr bool kEarlyBax = true;
+#else
+constexpr bool kEarlyBax = false;
+#endif
 // HC2 = false: no lane of the wave has cart-pole rows (the pole off its cart: 72 % of a C3 episode's
 // wave-sweeps), the 60 values of c2 are not built (the latency kernels' general loop then needs ~60 fewer
 // registers, which were AGPR moves inside it)
@@ -2299,6 +2306,7 @@ CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, rea
         asm volatile("" : "+v"(sec));
         const bool second = sec != 0u;
         Box A, Bx;
+        real bqv[4];  // B's quaternion: its axes are built after the broadphase, for the pairs it passes only
         pair_dispatch<GROUND>(j, [&](auto jt) {
             constexpr int J = decltype(jt)::value;
             constexpr int a0 = pair_a(island_pair_c(0, J)), a1 = pair_a(island_pair_c(1, J));
@@ -2317,11 +2325,15 @@ CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, rea
                 A.h0 = P.half_extents[0][0];
                 A.h1 = P.half_extents[0][1];
                 A.h2 = P.half_extents[0][2];
-                if constexpr (J == 0) Bx = box_of<b0, b1>(second, cx, cq, P);
-                else Bx = box_of<b0, b1>(second, px, pq, P);
+                if constexpr (J == 0) Bx = box_of<b0, b1, kEarlyBax || PM>(second, cx, cq, P);
+                else Bx = box_of<b0, b1, kEarlyBax || PM>(second, px, pq, P);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) bqv[k] = J == 0 ? cq[k] : pq[k];
             } else if constexpr (J == 2) {     // (own cart, own pole)
                 A = box_of<a0, a1>(second, cx, cq, P);
-                Bx = box_of<b0, b1>(second, px, pq, P);
+                Bx = box_of<b0, b1, kEarlyBax || PM>(second, px, pq, P);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) bqv[k] = pq[k];
             } else {
                 // cross pairs: island 0 stores (cart, cart2) and (cart, pole2), island 1 (pole, cart2) and
                 // (pole, pole2): A is island 0's own cart or the partner's pole, B the partner's or the own
@@ -2344,7 +2356,9 @@ CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, rea
                 real bq[4];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) bq[k] = second ? rq[k] : (J == 3 ? Pcq[k] : Ppq[k]);
-                Bx = box_of<b0, b1>(second, selv(second, rx, pbx), bq, P);
+                Bx = box_of<b0, b1, kEarlyBax || PM>(second, selv(second, rx, pbx), bq, P);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) bqv[k] = bq[k];
             }
         });
         Contact C;
@@ -2354,7 +2368,14 @@ CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, rea
         // PM: Bullet's box-box detector reports overlapping boxes only (margin 0); the manifold keeps
         // the points within the pair's relative breaking threshold
         const real newmargin = PM ? real(0.0) : real(P.contact_margin);
-        const bool near = plive && !face_separated(A, Bx, newmargin);
+        const bool near = plive && !face_separated(A, Bx, newmargin);  // (B's centre and extents only)
+#ifndef CP_NO_LATE_BAX
+        // (PM: the persistent manifold's refresh reads B's axes on every live lane: built early there)
+        // B's axes for the pairs the broadphase passes (box_box, the row setup's inertias); the other lanes keep
+        // the identity box_of<.., .., false> gave them, which nothing of theirs reads
+        if constexpr (!PM)
+            if (near) Bx.ax = quat_axes(bqv[0], bqv[1], bqv[2], bqv[3]);
+#endif
 #ifndef CP_NO_WSM
         // a pair the broadphase separates makes no point: its cache is not read (m = 0, the id word's old count
         // from O.wsm decides the rewrite below); the others load it here, its latency overlapping box_box

@@ -20,7 +20,7 @@ SWITCHES = ["", "CP_STAMPS", "CP_STAMPS CP_STAMP_C44", "CP_P1", "CP_P1 CP_P1_CHE
             "CP_DIAG_NO_CROSS", "CP_UNROLL_ROWS=1", "CP_HDR_SCRATCH", "CP_NO_GROUND_PEEL", "CP_NO_EZ", "CP_NO_C4K",
             "CP_NO_C44", "CP_NO_FAST_ROWS", "CP_NO_NONFINITE", "CP_NT_OUT", "CP_SOA_AUX=2", "CP_ALLIN_STEP=0",
             "CP_C44_CHECK=1", "CP_WAVES_PER_EU=1", "CP_RV_NO_DENSE", "CP_RV_NO_OUTPUT", "CP_RV_NO_STORE",
-            "CP_RV_SPT=3", "CP_RV_STOP=0", "CP_RV_STOP=1", "CP_NO_LEAN_C4", "CP_NO_LEAN_STEP", "CP_LEAN_TP", "CP_NO_HC2", "CP_NO_EDGE_SKIP", "CP_STAMPS CP_STAMP_BB", "CP_HX_TP", "CP_NO_LATE_I", "CP_NO_LATE_G", "CP_NO_LEAN_TR", "CP_LEAN_F64", "CP_NO_WSM", "CP_NO_LATE_ISL"]
+            "CP_RV_SPT=3", "CP_RV_STOP=0", "CP_RV_STOP=1", "CP_NO_LEAN_C4", "CP_NO_LEAN_STEP", "CP_LEAN_TP", "CP_NO_HC2", "CP_NO_EDGE_SKIP", "CP_STAMPS CP_STAMP_BB", "CP_HX_TP", "CP_NO_LATE_I", "CP_NO_LATE_G", "CP_NO_LEAN_TR", "CP_LEAN_F64", "CP_NO_WSM", "CP_NO_LATE_ISL", "CP_NO_LATE_BAX"]
 
 
 def _check(defs, tu):
