@@ -141,7 +141,7 @@ struct Bufs {
     int32_t* nonfinite;  // [B] steps / resets that ended with a non-finite body state
     int32_t* list;     // [B] reset list
     int32_t* count;    // reset list length (one of the handle's two counters, by step parity)
-    int32_t* count_next;  // the other counter: zeroed by the reset kernel for the next call
+    int32_t* count_next;  // the other counter: zeroed by the step and reset kernels for the next call
     void* scratch;     // [CP_SCR_FIELDS][2B] real: manifold headers (CP_HDR_SCRATCH builds), cp_rollout state
     uint64_t* stamps;  // [waves][8] diagnostic phase cycles (CP_STAMPS builds only)
     float* rposes;     // [B][R][4][7] repeat-end poses for the raster obs (NULL: raster off)

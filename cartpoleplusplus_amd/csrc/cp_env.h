@@ -452,6 +452,9 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
     __shared__ real lds_pool[(PM ? POOL_FLOATS_PM : POOL_FLOATS) * WAVE];
     const int B = cfg.num_envs;
     const int t = blockIdx.x * WAVE + threadIdx.x;
+    // the next call's reset-list counter (the reset kernel zeroes it too): cp_step launches no reset
+    // kernel on calls where no episode can end (cp_kernels.hip may_finish)
+    if (t == 0 && b.count_next) *b.count_next = 0;
     const int i = t >> 1, isl = t & 1;
     const bool lead = isl == 0;  // lane 0 of the pair writes the env's outputs
     const bool inb = i < B;

@@ -152,8 +152,8 @@ struct cp_handle {
     cp_raster_config raster;
     uint16_t* pixels;  // raster obs output (NULL: raster off)
     bool render_v1;    // CP_RENDER_V1=1 at cp_create: the round-3 small-frame render kernel (A/B diagnostic)
-    int32_t* count2;   // [3] reset-list counters: [0] [1] alternating by call (SAME_STEP: each reset launch
-                       // zeroes the other one; NEXT_STEP: one per reset list), [2] NEXT_STEP's cp_reset list
+    int32_t* count2;   // [3] reset-list counters: [0] [1] alternating by call (SAME_STEP: each step kernel
+                       // and reset launch zeroes the other one; NEXT_STEP: one per reset list), [2] NEXT_STEP's cp_reset list
     int par;           // counter the next call appends to
     // CP_AUTORESET_NEXT_STEP: the two reset lists (by call parity), the side stream each one's reset
     // kernel runs on, the events that fork it after the step kernel and join it back, the reset obs
@@ -168,6 +168,13 @@ struct cp_handle {
     int step_lat;      // 1: latency-shaped step kernel (every wave gets a SIMD of its own)
     int reset_req;     // cp_set_kernel_shape request (CP_SHAPE_AUTO: choose_reset_shape decides)
     int step_req;
+    // SAME_STEP autoreset without early termination: the number of cp_step calls since every env's
+    // step counter was 0 (cp_create, cp_reset of all envs), -1 when unknown (a masked reset,
+    // cp_set_state, a call captured into a graph).  Fixed-length episodes then end only on calls n
+    // with (n + 1) % max_episode_len == 0, and the other calls launch no reset kernel
+    // (may_finish; their list is empty).  CP_RESET_EVERY_CALL=1 turns the skip off (diagnostic).
+    int64_t phase;
+    bool reset_every_call;
     std::string err;
 };
 
@@ -331,6 +338,11 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     }
     h->npar = 0;
     h->ninflight = -1;
+    h->phase = 0;  // every env's step counter is 0 (and done is 1: they do not step until reset)
+    {
+        const char* rc = std::getenv("CP_RESET_EVERY_CALL");
+        h->reset_every_call = rc && rc[0] == '1';
+    }
     h->reset_req = h->step_req = CP_SHAPE_AUTO;
     choose_reset_shape(h);
     cp_default_raster_config(&h->raster);
@@ -495,7 +507,7 @@ const char* cp_render_kernel_name(cp_handle* h) {
     return kind >= 0 && kind < 3 ? names[kind] : nullptr;
 }
 
-// the reset list's counter for this call: the one the previous call's reset launch zeroed
+// the reset list's counter for this call: the one the previous call's step kernel (and reset launch) zeroed
 static void use_counter(cp_handle* h) {
     h->b.count = h->count2 + h->par;
     h->b.count_next = h->count2 + (h->par ^ 1);
@@ -532,6 +544,22 @@ static int launch_reset_list(cp_handle* h, const cpc::Bufs& b, float* obs_out, h
     if (check(h, hipGetLastError(), "cp_reset_kernel")) return -1;
     if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
     return 0;
+}
+
+// false when no env can finish in this cp_step call (see cp_handle::phase): every env that steps
+// enters it with a step counter of phase % max_episode_len, so it reaches the limit only when
+// (phase + 1) % max_episode_len == 0, and nothing else ends an episode.  The step kernel zeroes the next call's counter itself, so a skipped reset launch
+// leaves the counters as a launched one would.
+static bool may_finish(cp_handle* h, hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+        h->phase = -1;  // a graph replays this call any number of times: launch, and stop tracking
+        return true;
+    }
+    const bool lqr_done = h->lqr.gains && (h->lqr.done_pos > 0.0f || h->lqr.done_angle > 0.0f);
+    if (h->reset_every_call || h->phase < 0 || h->cfg.done_on_bounds || lqr_done) return true;
+    if (h->cfg.max_episode_len <= 0) return false;
+    return (h->phase + 1) % h->cfg.max_episode_len == 0;
 }
 
 static int launch_reset_from_list(cp_handle* h, float* obs_out, hipStream_t st, bool render) {
@@ -610,6 +638,7 @@ int cp_reset(cp_handle* h, const uint8_t* env_mask, float* obs_out, void* stream
         return launch_reset_list(h, b, obs_out, st);
     }
     use_counter(h);
+    h->phase = env_mask ? -1 : 0;
     CP_TRY(h, hipMemsetAsync(h->b.count, 0, sizeof(int32_t), st));
     hipLaunchKernelGGL(cp::cp_mask_to_list_kernel, dim3(grid_for(B, 256)), dim3(256), 0, st, B, env_mask, h->b.list,
                        h->b.count);
@@ -626,7 +655,8 @@ int cp_step(cp_handle* h, const void* actions, int action_kind, float* obs_out, 
     CP_TRY(h, hipSetDevice(h->device));
     if (h->cfg.autoreset == CP_AUTORESET_NEXT_STEP)
         return step_next_step(h, actions, action_kind, obs_out, reward_out, done_out, terminal_obs_out, st);
-    if (h->cfg.autoreset) use_counter(h);  // zeroed by the previous call's reset launch
+    if (h->cfg.autoreset) use_counter(h);  // zeroed by the previous call's step kernel (and reset launch)
+    const bool reset = h->cfg.autoreset && may_finish(h, st);
     if (h->pixels) CP_TRY(h, hipMemsetAsync(h->b.rcount, 0, sizeof(int32_t), st));
     hipEvent_t* ev = timing_slot(h, 0);
     if (ev) CP_TRY(h, hipEventRecord(ev[0], st));
@@ -640,7 +670,8 @@ int cp_step(cp_handle* h, const void* actions, int action_kind, float* obs_out, 
     if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
     // autoreset envs were simulated this step, so they are in the render list; the reset
     // kernel rewrites their poses first, and the one render launch draws the new episode
-    if (h->cfg.autoreset && launch_reset_from_list(h, obs_out, st, false)) return -1;
+    if (reset && launch_reset_from_list(h, obs_out, st, false)) return -1;
+    if (h->phase >= 0) ++h->phase;
     if (h->pixels) return launch_render(h, h->b.rlist, h->b.rcount, st);
     return 0;
 }
@@ -668,6 +699,7 @@ int cp_rollout(cp_handle* h, int steps, const void* actions, int action_kind, fl
                            terminal_obs_out, h->lqr, st);
     CP_TRY(h, hipGetLastError());
     if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
+    if (h->phase >= 0) h->phase += steps;  // the kernel resets finishing envs inline
     return 0;
 }
 
@@ -746,6 +778,7 @@ int cp_set_state(cp_handle* h, const void* state_in, void* stream) {
     size_t n = (size_t)CP_STATE_FIELDS * h->cfg.num_envs;
     CP_TRY(h, hipMemcpyAsync(h->b.state, state_in, n * (h->f64 ? sizeof(double) : sizeof(float)), hipMemcpyDeviceToDevice,
                              (hipStream_t)stream));
+    h->phase = -1;  // step counters of any value
     // the persistent manifolds are not part of the state SoA: no cached contact survives a teleport
     // (as in the reset kernel), so the next step rebuilds them from the new poses
     if (h->b.pman)
