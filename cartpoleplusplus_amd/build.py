@@ -26,7 +26,8 @@ STAMPS_LIB = os.path.join(HERE, "libcartpole_hip_stamps.so")
 ARCH = os.environ.get("CP_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-fPIC",
+FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-ffp-contract=off"] + \
+        ([] if os.environ.get("CP_SLP") == "1" else ["-fno-slp-vectorize"]) + ["-fPIC",
          "-Wno-unused-result",
          # LLVM's iterative ILP scheduler for gfx9: step kernel 0.634 -> 0.624 ms (r11);
          # scheduling never reorders a rounding, so the results stay bit-identical
