@@ -175,6 +175,7 @@ struct cp_handle {
     // (may_finish; their list is empty).  CP_RESET_EVERY_CALL=1 turns the skip off (diagnostic).
     int64_t phase;
     bool reset_every_call;
+    bool captured;     // some call on this handle was captured into a graph: phase tracking off until cp_destroy
     std::string err;
 };
 
@@ -313,6 +314,13 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     if ((cfg->phys.model_flags & CP_MODEL_PERSISTENT) && (cfg->phys.model_flags & CP_MODEL_SLEEPING))
         return fail(nullptr, "cp_create: CP_MODEL_PERSISTENT and CP_MODEL_SLEEPING together are oracle-only");
     if (!(cfg->phys.residual_threshold >= 0.0f)) return fail(nullptr, "cp_create: negative residual_threshold");
+    // NaN would silently turn the clamp off (the documented off switch is <= 0) or keep bodies awake
+    if (!std::isfinite(cfg->phys.max_coord_velocity))
+        return fail(nullptr, "cp_create: phys.max_coord_velocity must be finite (<= 0 turns the clamp off)");
+    if ((cfg->phys.model_flags & CP_MODEL_SLEEPING) &&
+        (!std::isfinite(cfg->phys.sleep_epsilon) || cfg->phys.sleep_epsilon < 0.0f ||
+         !std::isfinite(cfg->phys.sleep_timeout) || cfg->phys.sleep_timeout < 0.0f))
+        return fail(nullptr, "cp_create: CP_MODEL_SLEEPING needs a finite, non-negative sleep_epsilon and sleep_timeout");
     if (cfg->autoreset != CP_AUTORESET_OFF && cfg->autoreset != CP_AUTORESET_SAME_STEP &&
         cfg->autoreset != CP_AUTORESET_NEXT_STEP)
         return fail(nullptr, "cp_create: autoreset must be CP_AUTORESET_OFF, _SAME_STEP or _NEXT_STEP");
@@ -339,6 +347,7 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     h->npar = 0;
     h->ninflight = -1;
     h->phase = 0;  // every env's step counter is 0 (and done is 1: they do not step until reset)
+    h->captured = false;
     {
         const char* rc = std::getenv("CP_RESET_EVERY_CALL");
         h->reset_every_call = rc && rc[0] == '1';
@@ -546,19 +555,27 @@ static int launch_reset_list(cp_handle* h, const cpc::Bufs& b, float* obs_out, h
     return 0;
 }
 
+// A graph replays a captured call any number of times without the host seeing it, so once any entry
+// point that moves the step counters (cp_step, cp_reset, cp_rollout) has been captured on this handle,
+// the phase is unknown for good: every later cp_step launches its reset kernel.
+static bool note_capture(cp_handle* h, hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+        h->captured = true;
+        h->phase = -1;
+        return true;
+    }
+    return false;
+}
+
 // false when no env can finish in this cp_step call (see cp_handle::phase): every env that steps
 // enters it with a step counter of phase % max_episode_len, so it reaches the limit only when
 // (phase + 1) % max_episode_len == 0, and nothing else ends an episode.  The step kernel zeroes the next call's counter itself, so a skipped reset launch
 // leaves the counters as a launched one would.
 static bool may_finish(cp_handle* h, hipStream_t st) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
-        h->phase = -1;  // a graph replays this call any number of times: launch, and stop tracking
-        return true;
-    }
     const bool lqr_done = h->lqr.gains && (h->lqr.done_pos > 0.0f || h->lqr.done_angle > 0.0f);
-    if (h->reset_every_call || h->phase < 0 || h->cfg.done_on_bounds || lqr_done) return true;
-    if (h->cfg.max_episode_len <= 0) return false;
+    if (h->reset_every_call || h->captured || h->phase < 0 || h->cfg.done_on_bounds || lqr_done) return true;
+    if (h->cfg.max_episode_len <= 0) return true;  // every step ends the episode (done = steps >= limit)
     return (h->phase + 1) % h->cfg.max_episode_len == 0;
 }
 
@@ -639,6 +656,7 @@ int cp_reset(cp_handle* h, const uint8_t* env_mask, float* obs_out, void* stream
     }
     use_counter(h);
     h->phase = env_mask ? -1 : 0;
+    note_capture(h, st);
     CP_TRY(h, hipMemsetAsync(h->b.count, 0, sizeof(int32_t), st));
     hipLaunchKernelGGL(cp::cp_mask_to_list_kernel, dim3(grid_for(B, 256)), dim3(256), 0, st, B, env_mask, h->b.list,
                        h->b.count);
@@ -656,6 +674,7 @@ int cp_step(cp_handle* h, const void* actions, int action_kind, float* obs_out, 
     if (h->cfg.autoreset == CP_AUTORESET_NEXT_STEP)
         return step_next_step(h, actions, action_kind, obs_out, reward_out, done_out, terminal_obs_out, st);
     if (h->cfg.autoreset) use_counter(h);  // zeroed by the previous call's step kernel (and reset launch)
+    const bool capturing = note_capture(h, st);
     const bool reset = h->cfg.autoreset && may_finish(h, st);
     if (h->pixels) CP_TRY(h, hipMemsetAsync(h->b.rcount, 0, sizeof(int32_t), st));
     hipEvent_t* ev = timing_slot(h, 0);
@@ -672,7 +691,10 @@ int cp_step(cp_handle* h, const void* actions, int action_kind, float* obs_out, 
     // kernel rewrites their poses first, and the one render launch draws the new episode
     if (reset && launch_reset_from_list(h, obs_out, st, false)) return -1;
     if (h->phase >= 0) ++h->phase;
-    if (h->pixels) return launch_render(h, h->b.rlist, h->b.rcount, st);
+    if (h->pixels && launch_render(h, h->b.rlist, h->b.rcount, st)) return -1;
+    // a graph replays this call with the same counter every time: leave it empty for the next replay
+    // (eagerly the next call's step kernel zeroes it, as the other counter)
+    if (capturing && h->cfg.autoreset) CP_TRY(h, hipMemsetAsync(h->b.count, 0, sizeof(int32_t), st));
     return 0;
 }
 
@@ -699,6 +721,7 @@ int cp_rollout(cp_handle* h, int steps, const void* actions, int action_kind, fl
                            terminal_obs_out, h->lqr, st);
     CP_TRY(h, hipGetLastError());
     if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
+    note_capture(h, st);
     if (h->phase >= 0) h->phase += steps;  // the kernel resets finishing envs inline
     return 0;
 }

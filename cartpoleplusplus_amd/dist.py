@@ -40,15 +40,37 @@ def return_histogram(returns, max_len=200):
     return torch.bincount(returns.to(torch.int64).clamp(0, max_len), minlength=max_len + 1)
 
 
-def _visible_filter():
-    """The device list a HIP process would see (HIP_VISIBLE_DEVICES, then ROCR_VISIBLE_DEVICES,
-    then CUDA_VISIBLE_DEVICES, as the ROCm runtime reads them): None = no filter."""
+def _visible_filters():
+    """The device filters a HIP process applies, in the order the ROCm runtime applies them:
+    ROCR_VISIBLE_DEVICES first (the ROCr runtime's list of agents), then HIP_VISIBLE_DEVICES and
+    CUDA_VISIBLE_DEVICES (HIP's alias for it), each an index list into what the one before left.
+    Returns [(var, [entries])] for every variable that is set."""
     import os
-    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+    out = []
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
         v = os.environ.get(var)
         if v is not None:
-            return var, [x for x in v.split(",") if x.strip() != ""]
-    return None, None
+            out.append((var, [x.strip() for x in v.split(",") if x.strip() != ""]))
+    return out
+
+
+def _apply_filter(count, entries):
+    """Devices left after one filter over `count` devices: integer indices count only when they
+    are in range (and once each); a UUID ("GPU-...") may only be counted, not checked."""
+    seen = set()
+    n = 0
+    for x in entries:
+        try:
+            k = int(x, 0)
+        except ValueError:
+            if x.upper().startswith("GPU-") and x not in seen:
+                seen.add(x)
+                n += 1
+            continue
+        if 0 <= k < count and k not in seen:
+            seen.add(k)
+            n += 1
+    return min(n, count)
 
 
 def visible_gpu_count(sysfs="/sys/class/kfd/kfd/topology/nodes", dev_dri="/dev/dri"):
@@ -60,7 +82,8 @@ def visible_gpu_count(sysfs="/sys/class/kfd/kfd/topology/nodes", dev_dri="/dev/d
          process (a container lists every GPU of the host in sysfs but maps only its own render
          nodes);
       2. amdsmi (the kernel driver's SMI interface, no HIP), when sysfs has no topology;
-    then capped by the length of HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES.
+    then filtered by ROCR_VISIBLE_DEVICES, HIP_VISIBLE_DEVICES and CUDA_VISIBLE_DEVICES in turn
+    (every one that is set; out-of-range indices dropped, _apply_filter).
     Never torch.cuda.device_count(): on ROCm it falls back to hipGetDeviceCount, which initialises
     the runtime, whenever amdsmi does not answer.  Returns (count, source)."""
     import os
@@ -96,8 +119,7 @@ def visible_gpu_count(sysfs="/sys/class/kfd/kfd/topology/nodes", dev_dri="/dev/d
             source = "amdsmi"
         except Exception:   # no driver interface at all: nothing visible
             count, source = 0, "none"
-    var, lst = _visible_filter()
-    if lst is not None:
-        count = min(count, len(lst))
+    for var, lst in _visible_filters():
+        count = _apply_filter(count, lst)
         source += f"+{var}"
     return count, source

@@ -242,8 +242,10 @@ int cp_reset(cp_handle* h, const uint8_t* env_mask, float* obs_out, void* stream
  * pole_readback_out may be NULL.  With CP_AUTORESET_SAME_STEP and no early termination
  * (no bounds, no LQR done thresholds) the handle counts the calls since every env's step
  * counter was 0 (cp_create, cp_reset with env_mask NULL, cp_rollout adds its steps) and
- * launches the reset kernel only on calls where episodes end; a masked cp_reset,
- * cp_set_state or a call under stream capture stops that until the next full reset
+ * launches the reset kernel only on calls where episodes end; a masked cp_reset or
+ * cp_set_state stops that until the next full reset, and a cp_step / cp_reset / cp_rollout
+ * under stream capture stops it for the handle's lifetime (graph replays move the step
+ * counters unseen); max_episode_len <= 0 launches it on every call
  * (CP_RESET_EVERY_CALL=1 in the environment at cp_create: a launch on every call). */
 int cp_step(cp_handle* h, const void* actions, int action_kind,
             float* obs_out, float* reward_out, uint8_t* done_out,

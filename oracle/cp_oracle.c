@@ -1440,6 +1440,13 @@ static void write_obs_row(const sim_t* S, float* dst /* 14 floats */) {
 }
 
 int orc_envs_create(const cp_config* cfg, orc_envs** out) {
+    /* the cp_create checks on the physics fields the oracle reads: NaN would silently
+       turn the clamp off or keep bodies awake */
+    if (!isfinite(cfg->phys.max_coord_velocity)) return -2;
+    if ((cfg->phys.model_flags & CP_MODEL_SLEEPING) &&
+        (!isfinite(cfg->phys.sleep_epsilon) || cfg->phys.sleep_epsilon < 0.0f ||
+         !isfinite(cfg->phys.sleep_timeout) || cfg->phys.sleep_timeout < 0.0f))
+        return -2;
     orc_envs* e = (orc_envs*)calloc(1, sizeof(orc_envs));
     if (!e) return -1;
     e->cfg = *cfg;

@@ -189,7 +189,11 @@ class Envs:
         self.cfg = cfg
         self.B, self.R, self.S = cfg.num_envs, cfg.action_repeats, cfg.steps_per_repeat
         self.h = C.c_void_p()
-        if self.lib.orc_envs_create(C.byref(cfg), C.byref(self.h)) != 0:
+        rc = self.lib.orc_envs_create(C.byref(cfg), C.byref(self.h))
+        if rc == -2:
+            raise ValueError("orc_envs_create: non-finite max_coord_velocity, or a non-finite / negative "
+                             "sleep_epsilon or sleep_timeout with CP_MODEL_SLEEPING (cp_create's checks)")
+        if rc != 0:
             raise MemoryError("orc_envs_create failed")
 
     def __del__(self):

@@ -160,6 +160,16 @@ def test_cp_create_rejects_inconsistent_derived_fields():
     cfg.reset_flags = 0x80                        # an unknown CP_RESET_* bit
     assert lib.cp_create(C.byref(cfg), 0, C.byref(h)) != 0
     assert b"reset_flags" in lib.cp_last_error(None)
+    cfg = native.default_config(num_envs=4)
+    cfg.phys.max_coord_velocity = float("nan")    # NaN would silently turn the clamp off
+    assert lib.cp_create(C.byref(cfg), 0, C.byref(h)) != 0
+    assert b"max_coord_velocity" in lib.cp_last_error(None)
+    for field, bad in (("sleep_epsilon", float("nan")), ("sleep_timeout", -1.0), ("sleep_timeout", float("inf"))):
+        cfg = native.default_config(num_envs=4)
+        cfg.phys.model_flags = abi.CP_MODEL_SLEEPING
+        setattr(cfg.phys, field, bad)
+        assert lib.cp_create(C.byref(cfg), 0, C.byref(h)) != 0
+        assert b"sleep_epsilon and sleep_timeout" in lib.cp_last_error(None), field
     cfg = native.default_config(num_envs=4, angle_threshold=1.45)
     if lib.cp_create(C.byref(cfg), 0, C.byref(h)) == 0:   # a GPU host: do not leak the handle
         lib.cp_destroy(h)

@@ -95,6 +95,15 @@ def test_visible_gpu_count_from_kfd_topology(tmp_path, monkeypatch):
     assert visible_gpu_count(sysfs, dri) == (8, "kfd-sysfs")
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1")
     assert visible_gpu_count(sysfs, dri) == (2, "kfd-sysfs+HIP_VISIBLE_DEVICES")
+    # ROCR first, then HIP indexes into what ROCR left: "0,1" over one device is one device
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "3")
+    assert visible_gpu_count(sysfs, dri) == (1, "kfd-sysfs+ROCR_VISIBLE_DEVICES+HIP_VISIBLE_DEVICES")
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES")
+    # out-of-range and repeated indices are no devices; UUIDs count once each
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,9,0,12")
+    assert visible_gpu_count(sysfs, dri)[0] == 1
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "GPU-aa,GPU-bb,7")
+    assert visible_gpu_count(sysfs, dri)[0] == 3
 
 
 def test_world_size_must_match_gpus():

@@ -155,3 +155,20 @@ def test_sleeping_zero_force_stability(oracle_mod):
     obs, _ = _run(oracle_mod, abi.CP_MODEL_SLEEPING, steps=200, B=16)
     q = obs[-1][..., 1, 3:7].astype(np.float64)
     assert (1.0 - 2.0 * (q[..., 0] ** 2 + q[..., 1] ** 2)).min() > math.cos(math.radians(2.0))
+
+
+def test_oracle_rejects_non_finite_model_parameters(oracle_mod):
+    """The oracle refuses what cp_create refuses: a NaN velocity clamp, and with the
+    sleeping model a non-finite or negative sleep threshold."""
+    cfg = oracle_mod.default_config(num_envs=2)
+    cfg.phys.max_coord_velocity = float("nan")
+    with pytest.raises(ValueError):
+        oracle_mod.Envs(cfg)
+    cfg = oracle_mod.default_config(num_envs=2)
+    cfg.phys.model_flags = abi.CP_MODEL_SLEEPING
+    cfg.phys.sleep_epsilon = -0.5
+    with pytest.raises(ValueError):
+        oracle_mod.Envs(cfg)
+    cfg.phys.sleep_epsilon = 0.05
+    cfg.phys.max_coord_velocity = 0.0          # <= 0: the documented off switch, accepted
+    oracle_mod.Envs(cfg)
