@@ -78,6 +78,11 @@ STEP_EVENT_STRIDE = 4
 VALU_PEAK_WINST_PER_S = 256 * 4 * 2.4e9 / 2
 
 
+def native_lib_path():
+    from cartpoleplusplus_amd import native
+    return native.LIB_PATH
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -144,34 +149,65 @@ def _pmc_files():
     return list(reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))))
 
 
-def _pmc_match(d, batch, repeats, kind):
-    return d.get("batch", batch) == batch and d.get("repeats", repeats) == repeats and \
-        d.get("action_kind", "discrete") == kind
+def lib_sha256(path=None):
+    """sha256 of the HIP library this process runs (CP_LIB_PATH or the in-tree build): a PMC summary
+    counts only for the binary it was collected on."""
+    import hashlib
+    from cartpoleplusplus_amd import native
+    with open(path or native.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
 
 
-def pmc_traffic(kernel, batch, repeats, kind):
+# the keys a PMC summary's "workload" must carry, equal to the timed run's, for its counters to be
+# attached to the bench line (tools/summarize_profile.py writes them from the profiled bench line)
+PMC_KEYS = ("batch", "repeats", "action_kind", "dtype", "step_shape", "lib_sha256")
+
+
+def _pmc_match(d, want):
+    """None when summary d was collected on the workload `want` (every PMC_KEYS entry present and
+    equal), else the reason it does not count.  A missing key is a mismatch, never a match."""
+    w = d.get("workload")
+    if not isinstance(w, dict):
+        return "no workload keys"
+    for k in PMC_KEYS:
+        if k not in w:
+            return f"no {k!r} key"
+        if w[k] != want.get(k):
+            return f"{k} {w[k]!r} != {want.get(k)!r}"
+    return None
+
+
+def _pmc_lookup(kernel, want, get, files=None):
+    """(value, source, None) from the newest summary of `kernel` that matches `want`, else
+    (None, None, reason)."""
+    reasons = []
+    for p in (_pmc_files() if files is None else files):
+        with open(p) as f:
+            d = json.load(f)
+        k = d.get("kernels", {}).get(kernel)
+        v = get(k) if k else None
+        if v is None:
+            continue
+        why = _pmc_match(d, want)
+        if why is None:
+            return v, os.path.relpath(p, ROOT), None
+        reasons.append(f"{os.path.basename(p)}: {why}")
+    if not reasons:
+        return None, None, f"no PMC summary holds {kernel}"
+    more = f" (+{len(reasons) - 3} more)" if len(reasons) > 3 else ""
+    return None, None, "no PMC summary matches the timed workload and library: " + "; ".join(reasons[:3]) + more
+
+
+def pmc_traffic(kernel, want, files=None):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
-    (profiles/<tag>_pmc.json, tools/profile.sh + tools/summarize_profile.py), if it was
-    collected on this workload; else None."""
-    for p in _pmc_files():
-        with open(p) as f:
-            d = json.load(f)
-        k = d.get("kernels", {}).get(kernel)
-        if k and "hbm_bytes_per_launch" in k and _pmc_match(d, batch, repeats, kind):
-            return k["hbm_bytes_per_launch"], os.path.relpath(p, ROOT)
-    return None, None
+    (profiles/<tag>_pmc.json, tools/profile.sh + tools/summarize_profile.py) collected on this
+    workload with this library -> (bytes, source, reason-if-None)."""
+    return _pmc_lookup(kernel, want, lambda k: k.get("hbm_bytes_per_launch"), files)
 
 
-def pmc_valu(kernel, batch, repeats, kind):
-    """VALU wave-instructions per launch of `kernel` (SQ_INSTS_VALU) from the newest
-    committed PMC summary of this workload, else None."""
-    for p in _pmc_files():
-        with open(p) as f:
-            d = json.load(f)
-        k = d.get("kernels", {}).get(kernel)
-        if k and "SQ_INSTS_VALU" in k.get("sq_per_launch", {}) and _pmc_match(d, batch, repeats, kind):
-            return k["sq_per_launch"]["SQ_INSTS_VALU"], os.path.relpath(p, ROOT)
-    return None, None
+def pmc_valu(kernel, want, files=None):
+    """VALU wave-instructions per launch of `kernel` (SQ_INSTS_VALU), same matching."""
+    return _pmc_lookup(kernel, want, lambda k: k.get("sq_per_launch", {}).get("SQ_INSTS_VALU"), files)
 
 
 # ------------------------------------------------------------------- workload
@@ -960,7 +996,11 @@ def main():
         per_launch_s = tm["step_ms"] / 1e3 / K
         kernel = kernel.replace("cp_step_kernel", "cp_rollout_kernel") + " (time per env-step of the launch)"
     achieved = bytes_launch / per_launch_s / 1e9
-    traffic, traffic_src = pmc_traffic(kernel, B, R, kind)
+    shape = env.kernel_shape()
+    lib_hash = lib_sha256()
+    want = {"batch": B, "repeats": R, "action_kind": kind, "dtype": args.dtype, "step_shape": shape[0],
+            "lib_sha256": lib_hash}
+    traffic, traffic_src, traffic_why = pmc_traffic(kernel, want)
     if args.raster:
         # C5: the render kernel writes 2.9 GB per step and is the dominant HBM consumer
         rc = env.raster_cfg
@@ -968,18 +1008,19 @@ def main():
         bytes_launch = B * render_kernel_bytes(rc.height, rc.width, rc.num_cameras, R)
         achieved = bytes_launch / per_launch_s / 1e9
         kernel = env.render_kernel_name()   # the library's own choice (cp_render_kernel_name)
-        traffic, traffic_src = pmc_traffic(kernel, B, R, kind)
+        traffic, traffic_src, traffic_why = pmc_traffic(kernel, want)
     valu = None
     if not args.raster:
-        vi, vsrc = pmc_valu(kernel, B, R, kind)
-        if vi is not None:
+        vi, vsrc, valu_why = pmc_valu(kernel, want)
+        if vi is None:
+            valu = {"null_reason": valu_why}
+        else:
             ach = vi / per_launch_s
             valu = {"bound": "valu-issue (secondary; the kernel is latency-bound, DESIGN.md §5)",
                     "wave_instructions_per_launch": vi, "achieved": round(ach / 1e12, 4),
                     "peak": round(VALU_PEAK_WINST_PER_S / 1e12, 4), "unit": "T wave-instr/s",
                     "frac": round(ach / VALU_PEAK_WINST_PER_S, 4), "source": vsrc + " SQ_INSTS_VALU"}
     name, wl = workload(args, world)
-    shape = env.kernel_shape()
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -1010,7 +1051,9 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                      "traffic_source": traffic_src and (traffic_src + " (2*FETCH_SIZE + WRITE_SIZE) KiB*1024 "
-                                                        "per launch, rocprofv3 --pmc, separate passes"),
+                                                        "per launch, rocprofv3 --pmc, separate passes; "
+                                                        "same workload and library sha256"),
+                     **({"traffic_null_reason": traffic_why} if traffic is None else {}),
                      "kernel": kernel,
                      "bytes_per_launch": bytes_launch,
                      "avg_launch_ms": round(per_launch_s * 1e3, 4),
@@ -1020,6 +1063,7 @@ def main():
                      **({"step_kernel_avg_ms": round(tm["step_ms"] / max(1, tm["step_launches"]), 4),
                          "render_launches": tm["render_launches"]} if args.raster else {})},
         "valu": valu,
+        "build": {"lib": os.path.relpath(native_lib_path(), ROOT), "lib_sha256": lib_hash},
         "episode_return_hist_nonzero": None if hist is None else int((hist > 0).sum().item()),
         "done_on_bounds": bool(args.done_on_bounds),
         "nonfinite_envs": int(nf.item()),

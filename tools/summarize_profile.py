@@ -63,8 +63,42 @@ def durations(path):
     return d
 
 
+def bench_line(path):
+    """The JSON line bench.py printed under the profiler (the pass's stdout), or None."""
+    if not os.path.exists(path):
+        return None
+    line = None
+    with open(path) as f:
+        for ln in f:
+            if ln.startswith("{"):
+                line = ln
+    return json.loads(line) if line else None
+
+
+def workload_keys(prof_dir):
+    """bench.py's PMC_KEYS for the profiled run, from the bench lines every pass printed: the
+    counters count only for this workload and this library (bench.py _pmc_match).  Passes that
+    disagree (a rebuilt library between passes) leave the summary without keys, so it never matches."""
+    keys = []
+    for sub in ("trace", "sq", "sq2", "fetch", "write"):
+        b = bench_line(os.path.join(prof_dir, sub + ".json"))
+        if b is None:
+            continue
+        c = b.get("config", {})
+        keys.append({"batch": c.get("envs_per_gpu"), "repeats": c.get("action_repeats"),
+                     "action_kind": c.get("action_kind"), "dtype": b.get("dtype"),
+                     "step_shape": c.get("kernel_shape", {}).get("step"),
+                     "lib_sha256": b.get("build", {}).get("lib_sha256")})
+    if not keys or any(k != keys[0] for k in keys) or any(v is None for v in keys[0].values()):
+        return None
+    return keys[0]
+
+
 def main(prof_dir, tag, out_dir):
     res = {"tag": tag, "source": os.path.relpath(prof_dir), "kernels": {}}
+    w = workload_keys(prof_dir)
+    if w is not None:
+        res["workload"] = w
     dur = durations(os.path.join(prof_dir, "trace", "run_kernel_trace.csv"))
     p1 = os.path.join(prof_dir, "sq", "run_counter_collection.csv")   # absent in traffic-only runs
     sq, n_sq = counters(p1) if os.path.exists(p1) else ({}, {})
