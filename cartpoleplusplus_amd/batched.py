@@ -17,6 +17,7 @@ library stream in between, overlapped with the other envs' steps).
 """
 import ctypes as C
 
+import numpy as np
 import torch
 
 from . import abi, native
@@ -279,10 +280,17 @@ class BatchedCartpole:
                                                  float(done_pos), float(done_angle)), "cp_set_lqr")
 
     def set_bump_forces(self, forces):
-        """Parity mode (bump_mode='host'): LINK-frame bump forces (B, 30, 2, 2)."""
-        f = _device_buffer(torch.as_tensor(forces, dtype=torch.float32), (self.B, self.cfg.initial_force_steps, 2, 2),
-                           torch.float32, self.device, "bump forces")
-        native.check(self.h, self.lib.cp_set_bump_forces(self.h, _ptr(f), self._stream()), "cp_set_bump_forces")
+        """Parity mode (bump_mode='host'): LINK-frame bump forces (B, 30, 2, 2).  float64 input goes
+        through cp_set_bump_forces64 (an fp64 handle keeps the reference's doubles, an fp32 handle
+        rounds them); anything else is taken as float32."""
+        shape = (self.B, self.cfg.initial_force_steps, 2, 2)
+        t = forces if isinstance(forces, torch.Tensor) else torch.as_tensor(np.asarray(forces))
+        if t.dtype == torch.float64:
+            f = _device_buffer(t, shape, torch.float64, self.device, "bump forces")
+            native.check(self.h, self.lib.cp_set_bump_forces64(self.h, _ptr(f), self._stream()), "cp_set_bump_forces64")
+        else:
+            f = _device_buffer(t.to(torch.float32), shape, torch.float32, self.device, "bump forces")
+            native.check(self.h, self.lib.cp_set_bump_forces(self.h, _ptr(f), self._stream()), "cp_set_bump_forces")
 
     def get_state(self):
         s = torch.empty((abi.CP_STATE_FIELDS, self.B), device=self.device, dtype=self.real)

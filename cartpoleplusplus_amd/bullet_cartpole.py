@@ -68,7 +68,9 @@ def draw_bump_forces(initial_force, random_theta, steps=30):
 class BulletCartpole(Env):
     """Single-env gym surface over the MI355X kernel (reference: bullet_cartpole.py:48)."""
 
-    def __init__(self, opts, discrete_actions, device=0):
+    def __init__(self, opts, discrete_actions, device=0, precision="f32"):
+        # precision (not a reference flag): "f64" steps the fp64 parity variant, fed the reset's float64
+        # pushes unrounded (cp_set_bump_forces64, as pybullet receives them, :354-359)
         self.gui = opts.gui
         self.delay = opts.delay if self.gui else 0.0
         self.max_episode_len = opts.max_episode_len
@@ -106,7 +108,8 @@ class BulletCartpole(Env):
         self._env = BatchedCartpole(
             1, device, action_repeats=self.repeats, steps_per_repeat=self.steps_per_repeat,
             max_episode_len=self.max_episode_len, action_force=self.action_force,
-            initial_force=self.initial_force, random_theta=self.random_theta, bump_mode="host")
+            initial_force=self.initial_force, random_theta=self.random_theta, bump_mode="host",
+            precision=precision)
         self._env.enable_readback(True, reference_bug=True)
         if self.use_raw_pixels:
             self._env.enable_raster(True, width=self.render_width, height=self.render_height,

@@ -133,7 +133,7 @@ struct Lqr {
 struct Bufs {
     void* state;       // [CP_STATE_FIELDS][B] real
     float* term_obs;   // [R*14][B]
-    float* bumps;      // [B][ifs][2][2]
+    void* bumps;       // [B][ifs][2][2] of the handle's real type (float, or double for fp64 handles)
     float* ret_acc;    // [B]
     float* last_ret;   // [B]
     int32_t* last_len; // [B]

@@ -299,10 +299,11 @@ CP_DEV bool bounds_exceeded(const Own& O, const cp_config& cfg) {
 }
 
 // Bump force k on cart C (LINK frame), bullet_cartpole.py:354-359
-CP_DEV void bump_force(const cp_config& cfg, const float* bumps, int i, int episode, int k, int c, real& fx,
+// (host mode: the forces in the handle's real type, so an fp64 handle gets the reference's doubles)
+CP_DEV void bump_force(const cp_config& cfg, const void* bumps, int i, int episode, int k, int c, real& fx,
                        real& fy) {
     if (cfg.bump_mode == CP_BUMP_HOST) {
-        const float* f = bumps + (((size_t)i * cfg.initial_force_steps + k) * 2 + c) * 2;
+        const real* f = static_cast<const real*>(bumps) + (((size_t)i * cfg.initial_force_steps + k) * 2 + c) * 2;
         fx = f[0];
         fy = f[1];
         return;

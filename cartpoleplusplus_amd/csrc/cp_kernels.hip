@@ -127,6 +127,14 @@ __global__ void __launch_bounds__(256) cp_copy_kernel(const float* src, float* d
     if (i < n) dst[i] = src[i];
 }
 
+// host bump forces into the handle's real type: widening is exact, narrowing rounds to nearest (as
+// numpy's astype(float32) does)
+template <typename S, typename D>
+__global__ void __launch_bounds__(256) cp_convert_kernel(const S* src, D* dst, size_t n) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = (D)src[i];
+}
+
 }  // namespace cp
 
 // ============================================================================ C-ABI
@@ -371,7 +379,7 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     const size_t rb = h->f64 ? sizeof(double) : sizeof(float);  // bytes of the handle's real type
     CP_ALLOC(h->b.state, (size_t)CP_STATE_FIELDS * B * rb);
     CP_ALLOC(h->b.term_obs, (size_t)R * 14 * B * sizeof(float));
-    CP_ALLOC(h->b.bumps, B * (size_t)(cfg->initial_force_steps > 0 ? cfg->initial_force_steps : 1) * 4 * sizeof(float));
+    CP_ALLOC(h->b.bumps, B * (size_t)(cfg->initial_force_steps > 0 ? cfg->initial_force_steps : 1) * 4 * rb);
     CP_ALLOC(h->b.ret_acc, B * sizeof(float));
     CP_ALLOC(h->b.last_ret, B * sizeof(float));
     CP_ALLOC(h->b.last_len, B * sizeof(int32_t));
@@ -413,7 +421,7 @@ int cp_create(const cp_config* cfg, int device, cp_handle** out) {
     if (e != hipSuccess) return fail_free(e, "hipMemset");
     e = hipMemset(h->b.term_obs, 0, (size_t)R * 14 * B * sizeof(float));
     if (e != hipSuccess) return fail_free(e, "hipMemset");
-    e = hipMemset(h->b.bumps, 0, B * (size_t)(cfg->initial_force_steps > 0 ? cfg->initial_force_steps : 1) * 4 * sizeof(float));
+    e = hipMemset(h->b.bumps, 0, B * (size_t)(cfg->initial_force_steps > 0 ? cfg->initial_force_steps : 1) * 4 * rb);
     if (e != hipSuccess) return fail_free(e, "hipMemset");
     if (h->f64) cp64::launch_init(h->cfg, h->b, 0);
     else cp::launch_init(h->cfg, h->b, 0);
@@ -748,13 +756,36 @@ int cp_set_lqr(cp_handle* h, const float* gains, int per_env, float* state8_out,
     return 0;
 }
 
-int cp_set_bump_forces(cp_handle* h, const float* forces, void* stream) {
-    if (!h || !forces) return fail(h, "cp_set_bump_forces: null argument");
+// the forces copied (same type) or converted into the handle's bump buffer (its real type)
+extern "C++" template <typename S>
+static int set_bumps(cp_handle* h, const S* forces, void* stream, const char* what) {
+    if (!h || !forces) return fail(h, std::string(what) + ": null argument");
     CP_TRY(h, hipSetDevice(h->device));
-    if (join_next_step(h, (hipStream_t)stream)) return -1;  // an in-flight reset reads the bumps
-    size_t n = (size_t)h->cfg.num_envs * h->cfg.initial_force_steps * 4;
-    CP_TRY(h, hipMemcpyAsync(h->b.bumps, forces, n * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    hipStream_t st = (hipStream_t)stream;
+    if (join_next_step(h, st)) return -1;  // an in-flight reset reads the bumps
+    const size_t n = (size_t)h->cfg.num_envs * h->cfg.initial_force_steps * 4;
+    if (n == 0) return 0;
+    const bool same = h->f64 == std::is_same<S, double>::value;
+    if (same) {
+        CP_TRY(h, hipMemcpyAsync(h->b.bumps, forces, n * sizeof(S), hipMemcpyDeviceToDevice, st));
+    } else if (h->f64) {
+        hipLaunchKernelGGL((cp::cp_convert_kernel<S, double>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                           forces, static_cast<double*>(h->b.bumps), n);
+        CP_TRY(h, hipGetLastError());
+    } else {
+        hipLaunchKernelGGL((cp::cp_convert_kernel<S, float>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                           forces, static_cast<float*>(h->b.bumps), n);
+        CP_TRY(h, hipGetLastError());
+    }
     return 0;
+}
+
+int cp_set_bump_forces(cp_handle* h, const float* forces, void* stream) {
+    return set_bumps(h, forces, stream, "cp_set_bump_forces");
+}
+
+int cp_set_bump_forces64(cp_handle* h, const double* forces, void* stream) {
+    return set_bumps(h, forces, stream, "cp_set_bump_forces64");
 }
 
 int64_t cp_state_bytes(const cp_handle* h) {

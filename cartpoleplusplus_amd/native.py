@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("CP_LIB_PATH") or os.path.join(HERE, "libcartpole_hip.
 # every entry point declared in include/cartpole_amd.h
 EXPORTS = (
     "cp_default_config", "cp_create", "cp_destroy", "cp_last_error", "cp_abi_version",
-    "cp_reset", "cp_step", "cp_set_readback", "cp_set_bump_forces", "cp_get_state",
+    "cp_reset", "cp_step", "cp_set_readback", "cp_set_bump_forces", "cp_set_bump_forces64", "cp_get_state",
     "cp_set_state", "cp_episode_returns", "cp_overflow_counts", "cp_timing_begin", "cp_timing_end",
     "cp_timing_stride",
     "cp_debug_stamps", "cp_default_raster_config", "cp_set_raster", "cp_timing_render",
@@ -54,6 +54,7 @@ def load():
         "cp_step": (I, [VP, VP, I, VP, VP, VP, VP, VP]),
         "cp_set_readback": (I, [VP, VP, I]),
         "cp_set_bump_forces": (I, [VP, VP, VP]),
+        "cp_set_bump_forces64": (I, [VP, VP, VP]),
         "cp_get_state": (I, [VP, VP, VP]),
         "cp_set_state": (I, [VP, VP, VP]),
         "cp_episode_returns": (I, [VP, VP, VP, VP]),

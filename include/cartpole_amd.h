@@ -279,6 +279,13 @@ int cp_set_readback(cp_handle* h, float* readback_out, int reference_bug);
  * Device pointer; copied into the handle (used by every later reset). */
 int cp_set_bump_forces(cp_handle* h, const float* forces, void* stream);
 
+/* The same in float64, as the reference draws them (bullet_cartpole.py:354-359: np.random
+ * doubles through cos/sin, handed to pybullet's applyExternalForce as doubles).  A
+ * CP_PRECISION_F64 handle keeps them exact; an fp32 handle rounds each to the nearest float
+ * (what cp_set_bump_forces of the rounded array gives).  cp_set_bump_forces on an fp64 handle
+ * widens its floats exactly.  Device pointer, [B][initial_force_steps][2 carts][2]. */
+int cp_set_bump_forces64(cp_handle* h, const double* forces, void* stream);
+
 /* Closed-loop LQR policy (random_action_agent.py:60-135, gains :812-829; SURVEY.md
  * §8f row f4).  With gains != NULL every substep applies, per cart p,
  *     force_p = action_force * action_p + u_p,   u_p = -K_p . s_p   (:92-95, :897-901)

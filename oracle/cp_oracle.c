@@ -1455,7 +1455,7 @@ int orc_envs_create(const cp_config* cfg, orc_envs** out) {
     int R = cfg->action_repeats;
     e->state = calloc((size_t)CP_STATE_FIELDS * B, sizeof(real));
     e->term_obs = (float*)calloc((size_t)R * 14 * B, sizeof(float));
-    e->bump_forces = (float*)calloc(B * (size_t)cfg->initial_force_steps * 4, sizeof(float));
+    e->bump_forces = (real*)calloc(B * (size_t)cfg->initial_force_steps * 4, sizeof(real));
     e->ret_acc = (float*)calloc(B, sizeof(float));
     e->last_ret = (float*)calloc(B, sizeof(float));
     e->last_len = (int32_t*)calloc(B, sizeof(int32_t));
@@ -1487,8 +1487,15 @@ void orc_envs_destroy(orc_envs* e) {
     free(e->held_obs);
     free(e);
 }
+/* cp_set_bump_forces / cp_set_bump_forces64: stored in the build's real type (widened exactly,
+   or rounded to nearest) */
 void orc_envs_set_bump_forces(orc_envs* e, const float* f) {
-    memcpy(e->bump_forces, f, (size_t)e->B * e->cfg.initial_force_steps * 4 * sizeof(float));
+    const size_t n = (size_t)e->B * e->cfg.initial_force_steps * 4;
+    for (size_t k = 0; k < n; ++k) ((real*)e->bump_forces)[k] = (real)f[k];
+}
+void orc_envs_set_bump_forces64(orc_envs* e, const double* f) {
+    const size_t n = (size_t)e->B * e->cfg.initial_force_steps * 4;
+    for (size_t k = 0; k < n; ++k) ((real*)e->bump_forces)[k] = (real)f[k];
 }
 void orc_envs_get_state(const orc_envs* e, void* out) {
     memcpy(out, e->state, (size_t)CP_STATE_FIELDS * e->B * sizeof(real));
@@ -1503,7 +1510,7 @@ void orc_envs_set_state(orc_envs* e, const void* in) {
 static void bump_force(const orc_envs* e, int i, int episode, int k, int c, real* fx, real* fy) {
     const cp_config* cfg = &e->cfg;
     if (cfg->bump_mode == CP_BUMP_HOST) {
-        const float* f = e->bump_forces + (((size_t)i * cfg->initial_force_steps + k) * 2 + c) * 2;
+        const real* f = (const real*)e->bump_forces + (((size_t)i * cfg->initial_force_steps + k) * 2 + c) * 2;
         *fx = f[0];
         *fy = f[1];
         return;

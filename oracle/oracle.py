@@ -79,6 +79,7 @@ def load(precision="f32"):
         "orc_envs_create": (C.c_int, [cfgp, P(VP)]),
         "orc_envs_destroy": (None, [VP]),
         "orc_envs_set_bump_forces": (None, [VP, VP]),
+        "orc_envs_set_bump_forces64": (None, [VP, VP]),
         "orc_envs_set_lqr": (None, [VP, VP, C.c_int, VP, C.c_float, C.c_float]),
         "orc_envs_get_state": (None, [VP, VP]),
         "orc_envs_set_state": (None, [VP, VP]),
@@ -202,6 +203,12 @@ class Envs:
             self.h = None
 
     def set_bump_forces(self, forces):
+        """float64 input: cp_set_bump_forces64 (kept exact by the f64 build); else float32."""
+        if np.asarray(forces).dtype == np.float64:
+            f = np.ascontiguousarray(forces, dtype=np.float64)
+            assert f.shape == (self.B, self.cfg.initial_force_steps, 2, 2)
+            self.lib.orc_envs_set_bump_forces64(self.h, _ptr(f))
+            return
         f = np.ascontiguousarray(forces, dtype=np.float32)
         assert f.shape == (self.B, self.cfg.initial_force_steps, 2, 2)
         self.lib.orc_envs_set_bump_forces(self.h, _ptr(f))

@@ -16,7 +16,7 @@ HEADER = os.path.join(ROOT, "include", "cartpole_amd.h")
 
 def _declared():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"\b(cp_[a-z_]+)\s*\(", src)) - {"cp_handle"})
+    return sorted(set(re.findall(r"\b(cp_[a-z0-9_]+)\s*\(", src)) - {"cp_handle"})
 
 
 def test_library_exports_every_declared_symbol():

@@ -104,3 +104,67 @@ def test_f64_state_dtype_is_enforced():
     with pytest.raises(ValueError):
         env.set_state(s.float())
     env.set_state(s)
+
+
+def test_f64_reference_double_pushes(oracle_mod):
+    """The reference's pushes are float64 (bullet_cartpole.py:354-359, drawn by draw_bump_forces from
+    np.random exactly as the reference draws them): an fp64 handle takes them unrounded through
+    cp_set_bump_forces64 and matches the fp64 oracle fed the same doubles, reset and step, bit for
+    bit.  Also the gym mirror's f64 mode."""
+    from cartpoleplusplus_amd.bullet_cartpole import draw_bump_forces
+    B = 48
+    gpu, orc = _pair(oracle_mod, num_envs=B, action_repeats=3, initial_force=55.0, bump_mode=abi.CP_BUMP_HOST,
+                     autoreset=1, max_episode_len=20)
+    state = np.random.get_state()
+    try:
+        np.random.seed(1234)
+        f = np.stack([draw_bump_forces(55.0, True, 30) for _ in range(B)])
+    finally:
+        np.random.set_state(state)
+    assert f.dtype == np.float64 and not np.array_equal(f, f.astype(np.float32).astype(np.float64))
+    gpu.set_bump_forces(torch.from_numpy(f).cuda())
+    orc.set_bump_forces(f)
+    _same(_np(gpu.reset()), orc.reset(), "reset obs")
+    _state(gpu, orc, "reset")
+    rng = np.random.default_rng(12)
+    for t in range(45):                                  # two autoreset bursts from the double pushes
+        a = rng.integers(0, 5, (B, 2)).astype(np.int8)
+        go, _, gd = gpu.step(torch.from_numpy(a).cuda())
+        oo, _, od = orc.step(a)
+        _same(_np(go), oo, f"obs step {t}")
+        _same(_np(gd), od, f"done step {t}")
+    _state(gpu, orc, "after 45 steps")
+    # the same doubles through the fp32-rounded entry point give another state
+    g32, _ = _pair(oracle_mod, num_envs=B, action_repeats=3, initial_force=55.0, bump_mode=abi.CP_BUMP_HOST,
+                   autoreset=1, max_episode_len=20)
+    g32.set_bump_forces(torch.from_numpy(f.astype(np.float32)).cuda())
+    g32.reset()
+    assert not np.array_equal(_np(g32.get_state()), _np(gpu.get_state()))
+    gpu.close()
+    g32.close()
+
+
+def test_f64_gym_mirror_takes_double_pushes(oracle_mod):
+    """BulletCartpole(precision='f64'): the reset draws the reference's float64 pushes and hands
+    them over unrounded; its obs equal the fp64 oracle fed the same doubles."""
+    import argparse
+    from cartpoleplusplus_amd.bullet_cartpole import BulletCartpole, add_opts, draw_bump_forces
+    parser = argparse.ArgumentParser()
+    add_opts(parser)
+    opts = parser.parse_args(["--initial-force", "55"])
+    state = np.random.get_state()
+    try:
+        np.random.seed(77)
+        env = BulletCartpole(opts, discrete_actions=True, precision="f64")
+        s0 = env.reset()
+        np.random.seed(77)
+        f = draw_bump_forces(55.0, True, 30)[None]
+    finally:
+        np.random.set_state(state)
+    cfg = native.default_config(num_envs=1, action_repeats=opts.action_repeats, initial_force=55.0,
+                                bump_mode=abi.CP_BUMP_HOST)
+    cfg.precision = abi.CP_PRECISION_F64
+    orc = oracle_mod.Envs(abi.cp_config.from_buffer_copy(cfg), precision="f64")
+    orc.set_bump_forces(f)
+    _same(s0, orc.reset()[0], "mirror reset obs")
+    env.close()

@@ -271,3 +271,27 @@ def test_coordinate_velocity_clamp(oracle_mod, prec):
     assert w0[2] == pytest.approx(150.0 - dt * 150.0 * k * (1.0 + 150.0), rel=1e-5)
     clamped = _spin(oracle_mod, prec, 100.0, (30.0, 0.0, 150.0), 400)
     assert np.isfinite(clamped).all() and np.abs(clamped).max() <= 100.0
+
+
+def test_f64_double_pushes_differ_from_rounded(oracle_mod):
+    """The fp64 oracle keeps the reference's float64 pushes (orc_envs_set_bump_forces64): the same
+    forces rounded to float32 first reset to another state, while the fp32
+    oracle gives one state for both (it rounds the doubles itself)."""
+    import numpy as np
+    from cartpoleplusplus_amd import abi
+    B = 8
+    rng = np.random.default_rng(5)
+    th = rng.random((B, 30, 2)) * 2 * np.pi
+    f = np.stack([55.0 * np.cos(th), 55.0 * np.sin(th)], -1)
+    assert f.dtype == np.float64
+    states = {}
+    for prec in ("f64", "f32"):
+        for kind, forces in (("double", f), ("rounded", f.astype(np.float32))):
+            cfg = oracle_mod.default_config(num_envs=B, action_repeats=3, initial_force=55.0,
+                                            bump_mode=abi.CP_BUMP_HOST)
+            env = oracle_mod.Envs(cfg, precision=prec)
+            env.set_bump_forces(forces)
+            env.reset()
+            states[prec, kind] = env.get_state()
+    assert not np.array_equal(states["f64", "double"], states["f64", "rounded"])
+    assert np.array_equal(states["f32", "double"].view(np.uint32), states["f32", "rounded"].view(np.uint32))
