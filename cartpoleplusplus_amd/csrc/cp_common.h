@@ -21,10 +21,10 @@
 #define CP_PM_PAIR_FIELDS 45
 #define CP_PM_FIELDS (CP_ISLAND_PAIRS * CP_PM_PAIR_FIELDS)
 
-// Scratch SoA (Bufs::scratch), one column per lane: rows [0, CP_SCR_HDR_FIELDS) hold the manifold
-// headers of CP_HDR_SCRATCH builds (4 per pair, written and read inside one substep); rows
+// Scratch SoA (Bufs::scratch), one column per lane: rows [0, CP_SCR_HDR_FIELDS) are reserved (the
+// manifold headers of a diagnostic build until round 5; the headers live in registers); rows
 // [CP_SCR_RC_BASE, CP_SCR_FIELDS) hold cp_rollout's per-lane state machine (RC_* in cp_env.h), kept
-// across substeps -- disjoint, so a header write never lands on the rollout's state.
+// across substeps.
 #define CP_SCR_HDR_FIELDS (4 * CP_ISLAND_PAIRS)
 #define CP_SCR_RC_BASE CP_SCR_HDR_FIELDS
 #define CP_SCR_RC_FIELDS 10
@@ -83,11 +83,8 @@ CP_DEV uint32_t to_bits(double x) { return (uint32_t)(uint64_t)__double_as_longl
 // each env keeps one offset register instead of a 64-bit address per field (the flat form
 // made the compiler hoist and spill ~100 of them).  Limits one SoA array to 4 GiB:
 // B * fields * sizeof(T) < 2^32 (checked at cp_create).
-// cache policy bits of the SoA buffer accesses (gfx950 CPol: 1 sc0, 2 nt, 16 sc1); 0 = default.
-// Diagnostic builds (-DCP_SOA_AUX=2) stream the state past L2 so that the spill frame stays resident.
-#ifndef CP_SOA_AUX
-#define CP_SOA_AUX 0
-#endif
+// The SoA buffer accesses use the default cache policy (aux 0): streaming the state past L2 (nt) was
+// measured slower.
 
 template <typename T>
 struct SoaT {
@@ -103,19 +100,19 @@ struct SoaT {
     CP_DEV static uint32_t eoff(int i) { return (uint32_t)i * (uint32_t)sizeof(T); }
     CP_DEV T ld(int f, uint32_t off) const {
         if constexpr (sizeof(T) == 4) {
-            return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, (int)((uint32_t)f * fstride), CP_SOA_AUX));
+            return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, (int)((uint32_t)f * fstride), 0));
         } else {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, (int)((uint32_t)f * fstride), CP_SOA_AUX);
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, (int)((uint32_t)f * fstride), 0);
             return __longlong_as_double((long long)(((uint64_t)(uint32_t)v[1] << 32) | (uint32_t)v[0]));
         }
     }
     CP_DEV void st(int f, uint32_t off, T x) const {
         if constexpr (sizeof(T) == 4) {
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, (int)off, (int)((uint32_t)f * fstride), CP_SOA_AUX);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, (int)off, (int)((uint32_t)f * fstride), 0);
         } else {
             const uint64_t u = (uint64_t)__double_as_longlong(x);
             __attribute__((ext_vector_type(2))) unsigned int v = {(unsigned int)u, (unsigned int)(u >> 32)};
-            __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, (int)((uint32_t)f * fstride), CP_SOA_AUX);
+            __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, (int)((uint32_t)f * fstride), 0);
         }
     }
 };
@@ -142,7 +139,7 @@ struct Bufs {
     int32_t* list;     // [B] reset list
     int32_t* count;    // reset list length (one of the handle's two counters, by step parity)
     int32_t* count_next;  // the other counter: zeroed by the step and reset kernels for the next call
-    void* scratch;     // [CP_SCR_FIELDS][2B] real: manifold headers (CP_HDR_SCRATCH builds), cp_rollout state
+    void* scratch;     // [CP_SCR_FIELDS][2B] real: reserved rows, cp_rollout state
     uint64_t* stamps;  // [waves][8] diagnostic phase cycles (CP_STAMPS builds only)
     float* rposes;     // [B][R][4][7] repeat-end poses for the raster obs (NULL: raster off)
     float4* rtable;    // [C][H*W] (d, t_ground) then [C][H*W] uint8 ground class (cp_raster_table_kernel)

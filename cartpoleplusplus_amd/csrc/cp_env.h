@@ -28,24 +28,10 @@ namespace CP_NS {
 // fp64: only the 1-wave-per-SIMD (512 VGPR) kernel shape, with the slow-form rows (the fast
 // form's precomputed rows do not fit twice the registers)
 constexpr bool kF64 = sizeof(real) == 8;
-#ifndef CP_ALLIN_STEP
-#define CP_ALLIN_STEP 1
-#endif
-constexpr bool kAllinStep = CP_ALLIN_STEP != 0;  // the all-inside face-contact exit in the step kernel (C3 kernel -0.6 %, C2 -2 %)
-// the reset kernels' guard-free settle / bump-structure sweep loops (sweeps_c44_slow, sweeps_c4k_slow) in
-// the throughput-shaped step kernel too: the first ~10 steps of an episode are poles standing on their
-// carts, every wave at the 50-sweep cap (tools/episode_phase.py)
-#ifndef CP_STEP_C44
-#define CP_STEP_C44 0
-#endif
-constexpr bool kC44Step = CP_STEP_C44 != 0;
-// the throughput-shaped step / reset kernels rebuild the lane's SoA offsets (Mem) per substep and for the epilogue
-// from an opaque env index instead of keeping the ones formed at the top live (round 5; CP_NO_LATE_G: A/B)
-#ifdef CP_NO_LATE_G
-constexpr int kLateG = 0;
-#else
-constexpr int kLateG = 1;
-#endif
+// The throughput-shaped step / reset kernels rebuild the lane's SoA offsets (Mem) per substep and for the
+// epilogue from an opaque env index instead of keeping the ones formed at the top live (round 5).  The
+// step kernels take the all-inside face-contact exit (C3 kernel -0.6 %, C2 -2 %); the reset kernels' settle
+// loops in the step kernel were measured slower and dropped.
 
 using Bufs = cpc::Bufs;
 using Lqr = cpc::Lqr;
@@ -105,14 +91,9 @@ CP_DEV void flush_stamps(const Stamps& ST, uint64_t* dst, uint64_t total, uint64
 }
 
 // per-step outputs (obs rows, reward, done): written once, read by the caller after the launch.
-// Diagnostic builds (-DCP_NT_OUT) store them non-temporally (past L2).
 template <typename T>
 CP_DEV void put_out(T* p, T v) {
-#ifdef CP_NT_OUT
-    __builtin_nontemporal_store(v, p);
-#else
     *p = v;
-#endif
 }
 
 // The lane's own island's fields of the state SoA: island p's bodies are dyn 2p, 2p + 1 (CP_SF_BODY(2p + k, c)),
@@ -194,10 +175,6 @@ CP_DEV void sti(const Soa& st, int f, uint32_t o, int32_t v) { st.st(f, o, bits_
 // true if every body value (pos, quat, v, w) of the lane's own bodies is finite: x * 0 is +-0 for a finite
 // x and NaN for an inf or NaN, so the fma chain stays a zero exactly when all 26 values are finite
 CP_DEV bool own_finite(const Own& O) {
-#ifdef CP_NO_NONFINITE  // diagnostic A/B build: the counter's cost (never counts)
-    (void)O;
-    return true;
-#endif
     real acc = real(0.0);
     auto body = [&](const Body& y) {
         acc = fma_(y.x.x, real(0.0), acc); acc = fma_(y.x.y, real(0.0), acc); acc = fma_(y.x.z, real(0.0), acc);
@@ -374,9 +351,7 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     // lane's SoA offsets are rebuilt there instead of living through the 130 substeps (cp_step_kernel)
     auto late_i = [&]() {
         int x = i;
-#ifndef CP_NO_LATE_I
         asm volatile("" : "+v"(x));
-#endif
         return x;
     };
     real* pool = lds_pool + threadIdx.x;
@@ -405,7 +380,7 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     int ov = 0;
     const int nsub = cfg.settle_steps + cfg.initial_force_steps;
     for (int s = 0; s < nsub; ++s) {
-        const Mem Gs = ((LAT && !kF64) || kLateG == 0) ? G : Mem::make(b.state, b.scratch, B, late_i(), isl, b.pman);
+        const Mem Gs = (LAT && !kF64) ? G : Mem::make(b.state, b.scratch, B, late_i(), isl, b.pman);
         substep<LAT && !kF64, true, true, PM, SLP>(O, cfg.phys, L, pool, pool0, ov, Gs, ST);
         const int k = s - cfg.settle_steps;
         if (k >= 0) {  // bump the lane's own cart (cart, then cart2 in the reference's draw order)
@@ -420,7 +395,7 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     CP_RT(r1);
     flush_stamps(ST, b.stamps + 16, k1 - k0, r0, r1);  // the reset kernel's counters: slots 16-26
 #endif
-    const Mem Ge = ((LAT && !kF64) || kLateG == 0) ? G : Mem::make(b.state, b.scratch, B, late_i(), isl, b.pman);
+    const Mem Ge = (LAT && !kF64) ? G : Mem::make(b.state, b.scratch, B, late_i(), isl, b.pman);
     const int il = late_i();
     store_own(O, Ge, isl);  // each lane stores its own island
     if constexpr (SLP) store_sleep(O, Ge, isl);
@@ -470,19 +445,13 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
     // step kernel's scratch frame, written at the top and read back at the end of every launch)
     auto late_i = [&]() {
         int x = i;
-#ifndef CP_NO_LATE_I  // diagnostic A/B: the addresses formed once at the top (round 5: scratch 80 B/lane)
         asm volatile("" : "+v"(x));
-#endif
         return x;
     };
     // the lane's island (lane parity) recomputed from the lane id where the late offsets need it (a kept copy
     // and the island offsets derived from it were spilled)
     auto late_isl = [&]() {
-#if defined(CP_NO_LATE_I) || defined(CP_NO_LATE_ISL)
-        return isl;
-#else
         return (int)(__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) & 1u);
-#endif
     };
     CP_STAMP(k0);
     CP_RT(r0);
@@ -537,8 +506,8 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
                     // the throughput shape: the lane's SoA offsets rebuilt per substep from the opaque index (not live
                     // through the loop; scratch 48 -> 24 B/lane); the 0-scratch latency kernels keep G (a lone wave
                     // pays the rebuild: latency reset list +2.6 %)
-                    const Mem Gs = ((LAT && !kF64) || kLateG == 0) ? G : Mem::make(b.state, b.scratch, B, late_i(), late_isl(), b.pman);
-                    substep<LAT && !kF64, kC44Step && !LAT && !kF64 && !PM, kAllinStep, PM, SLP>(O, cfg.phys, L, pool,
+                    const Mem Gs = (LAT && !kF64) ? G : Mem::make(b.state, b.scratch, B, late_i(), late_isl(), b.pman);
+                    substep<LAT && !kF64, false, true, PM, SLP>(O, cfg.phys, L, pool,
                                                                                                    pool0, ov, Gs, ST);
                     if constexpr (LQR) {  // disturbance + control (:897-901), control from the pre-step state
                         apply_force_link(O, fa + u[0], fb + u[1]);
@@ -570,8 +539,8 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
             ov += (int)partner_u((uint32_t)ov);
             const int il = late_i();
             if (ov && lead) b.overflow[il] += ov;
-            const int isle = ((LAT && !kF64) || kLateG == 0) ? isl : late_isl();
-            const Mem Ge = ((LAT && !kF64) || kLateG == 0) ? G : Mem::make(b.state, b.scratch, B, il, isle, b.pman);
+            const int isle = (LAT && !kF64) ? isl : late_isl();
+            const Mem Ge = (LAT && !kF64) ? G : Mem::make(b.state, b.scratch, B, il, isle, b.pman);
             const int steps = ldi(Ge.st, CP_SF_STEPS, Ge.off) + 1;
             bool done = steps >= cfg.max_episode_len;
             if (cfg.done_on_bounds && bounds_exceeded(O, cfg)) done = true;
@@ -732,7 +701,7 @@ cp_rollout_kernel(cp_config cfg, Bufs b, int K, const void* actions, float* obs_
                            ldi(G.st, CP_SF_DONE, G.off) != 0 ? RF_DONE : 0u, b.ret_acc[i]);
     while (__ballot(work) != 0ull) {
         if (!work) continue;
-        substep<LAT && !kF64, false, kAllinStep, PM, SLP>(O, cfg.phys, L, pool, pool0, ov, G, ST);
+        substep<LAT && !kF64, false, true, PM, SLP>(O, cfg.phys, L, pool, pool0, ov, G, ST);
         int k = ldc(RC_K), sub = ldc(RC_SUB);
         uint32_t flags = (uint32_t)ldc(RC_FLAGS);
         if (!(flags & RF_RESETTING)) {

@@ -360,9 +360,6 @@ template <bool ALLIN = false, bool ES = false>
 CP_DEV void box_box(const Box& A, const Box& B, real margin, real edge_bias, Contact& C, Stamps& ST) {
     (void)ST;
     C.m = 0;
-#ifdef CP_STAMP_BB  // diagnostic: box_box's own split (slots sel: face axes, bb: edge axes, rows: contact)
-    CP_STAMP(bb0);
-#endif
     V3 d = sub(B.c, A.c);
     V3 Aax[3] = {A.ax.a0, A.ax.a1, A.ax.a2};
     V3 Bax[3] = {B.ax.a0, B.ax.a1, B.ax.a2};
@@ -398,10 +395,6 @@ CP_DEV void box_box(const Box& A, const Box& B, real margin, real edge_bias, Con
         sep = sep || (s > margin);
         if (s > best) { best = s; kind = 1; bj = j; }
     }
-#ifdef CP_STAMP_BB
-    CP_STAMP(bb1);
-    CP_ACC(sel, bb0, bb1);
-#endif
     if (sep) return;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -414,7 +407,6 @@ CP_DEV void box_box(const Box& A, const Box& B, real margin, real edge_bias, Con
             real ra = fma_(Ah[i1], AC[i2][j], Ah[i2] * AC[i1][j]);
             real rb = fma_(Bh[j1], AC[i][j2], Bh[j2] * AC[i][j1]);
             real num = abs_(dot(d, ax)) - (ra + rb);   // separation * L
-#ifndef CP_NO_EDGE_SKIP
             if constexpr (ES) {
             // Both tests below compare num with (c * L) for c = margin and c = best + edge_bias, where
             // L = |a x b| <= 1 + 2^-11 (unit axes from normalised quaternions).  For num <= min(c, 0) (1 + 2^-10)
@@ -427,16 +419,11 @@ CP_DEV void box_box(const Box& A, const Box& B, real margin, real edge_bias, Con
             lo = lo < real(0.0) ? lo : real(0.0);
             if (num <= lo * real(1.0009765625)) continue;
             }
-#endif
             real L = sqrt_(L2);
             sep = sep || (num > margin * L);
             if (num > (best + edge_bias) * L) { best = num / L; kind = 2; bi = i; bj = j; bax = ax; }
         }
     }
-#ifdef CP_STAMP_BB
-    CP_STAMP(bb2);
-    CP_ACC(bb, bb1, bb2);
-#endif
     if (sep) return;
     if (kind != 2) {
         // face of A (kind 0) or face of B (kind 1) is the reference face
@@ -474,10 +461,6 @@ CP_DEV void box_box(const Box& A, const Box& B, real margin, real edge_bias, Con
             C.d[k] = o.n[k];
             C.ids |= (uint32_t)(o.id[k] + code) << (8 * k);
         }
-#ifdef CP_STAMP_BB
-        CP_STAMP(bb3);
-        CP_ACC(rows, bb2, bb3);
-#endif
         return;
     }
     // edge-edge
@@ -718,12 +701,8 @@ CP_DEV void isl_warmstart(Isl& I, const Step& T, real* pool) {
     }
 }
 
-// CP_UNROLL_ROWS (diagnostic): the generic row loops unrolled to the 4-point bound like the +z ones
-#if defined(CP_UNROLL_ROWS) && CP_UNROLL_ROWS
-#define CP_ROW_LOOP(k, n) _Pragma("unroll") for (int k = 0; k < 4; ++k) if (k < (n))
-#else
+// the generic row loops are counted loops (unrolled to the 4-point bound they were measured slower)
 #define CP_ROW_LOOP(k, n) for (int k = 0; k < (n); ++k)
-#endif
 template <int J, bool PM = false>
 CP_DEV void isl_normal_rows(Isl& I, const Step& T, real* pool, real tol, bool& bad) {
     const uint32_t pk = T.pk[J];
@@ -814,30 +793,12 @@ struct Hdr {
     V3 n;
     uint32_t pk;
 };
-// Opaque register copies for the cross-row code of merged envs (CP_CROSS_OPAQUE).  Its inputs that
-// stay fixed during a solve (both islands' positions, inverse inertias and manifold headers, read
-// from the partner lane by DPP) are loop-invariant in the sweep loop; hoisted out of it, the partner
-// copies and selects stay live across every sweep of every wave, merged env or not, and push the
-// island rows' values into scratch.  The empty asm makes them fresh values inside each cross block.
-#ifndef CP_CROSS_OPAQUE
-#define CP_CROSS_OPAQUE 0
-#endif
-CP_DEV void opq(real& x) {
-    if constexpr (CP_CROSS_OPAQUE != 0) asm volatile("" : "+v"(x));
-}
-CP_DEV void opq(uint32_t& x) {
-    if constexpr (CP_CROSS_OPAQUE != 0) asm volatile("" : "+v"(x));
-}
-CP_DEV V3 opq3(V3 v) { opq(v.x); opq(v.y); opq(v.z); return v; }
-CP_DEV Sym opqs(Sym m) { opq(m.m0); opq(m.m1); opq(m.m2); opq(m.m3); opq(m.m4); opq(m.m5); return m; }
-
 template <int PAIR>
 CP_DEV Hdr pair_hdr(const Step& T, bool second) {
     (void)second;
     constexpr int j = local_of(PAIR), isl = island_of(PAIR) != 0 ? 1 : 0;
-    const V3 tn = opq3(T.n[j]);
-    uint32_t tpk = T.pk[j];
-    opq(tpk);
+    const V3 tn = T.n[j];
+    const uint32_t tpk = T.pk[j];
     Hdr h;  // the owning island's lane's header, on both lanes
     h.n = lane_of3<isl>(tn);
     h.pk = lane_of_u<isl>(tpk);
@@ -996,20 +957,10 @@ CP_DEV void pair_dispatch(int j, F&& f) {
         if (j == 0) f(std::integral_constant<int, 0>{});
         else f(std::integral_constant<int, 1>{});
     } else {
-#ifdef CP_NO_GROUND_PEEL  // diagnostic: every pair through this dispatch, the ground pairs included
-        if (j == 0) f(std::integral_constant<int, 0>{});
-        else if (j == 1) f(std::integral_constant<int, 1>{});
-        else
-#endif
         if (j == 2) f(std::integral_constant<int, 2>{});
         else if (j == 3) f(std::integral_constant<int, 3>{});
         else f(std::integral_constant<int, 4>{});
     }
-}
-CP_DEV V3 sel5v(int g, V3 z, V3 a, V3 b, V3 c, V3 d) {
-    return mk(g == 1 ? a.x : g == 2 ? b.x : g == 3 ? c.x : g == 4 ? d.x : z.x,
-              g == 1 ? a.y : g == 2 ? b.y : g == 3 ? c.y : g == 4 ? d.y : z.y,
-              g == 1 ? a.z : g == 2 ? b.z : g == 3 ? c.z : g == 4 ? d.z : z.z);
 }
 
 // Broadphase: true when a face axis of A already separates the pair by more than
@@ -1192,10 +1143,10 @@ CP_DEV void cross_view(Sim& S, Step& T, const Isl& I, bool second) {
     (void)second;
     // island 0's bodies (cart, pole) from the pair's even lane, island 1's (cart2, pole2) from the odd
     // lane, one DPP move per value on both lanes (S is scratch: each lane holds only its own island)
-    S.b[0].x = lane_of3<0>(opq3(I.d1.x));
-    S.b[1].x = lane_of3<0>(opq3(I.d2.x));
-    S.b[2].x = lane_of3<1>(opq3(I.d1.x));
-    S.b[3].x = lane_of3<1>(opq3(I.d2.x));
+    S.b[0].x = lane_of3<0>(I.d1.x);
+    S.b[1].x = lane_of3<0>(I.d2.x);
+    S.b[2].x = lane_of3<1>(I.d1.x);
+    S.b[3].x = lane_of3<1>(I.d2.x);
     S.b[0].v = lane_of3<0>(I.d1.v);
     S.b[0].w = lane_of3<0>(I.d1.w);
     S.b[1].v = lane_of3<0>(I.d2.v);
@@ -1204,7 +1155,7 @@ CP_DEV void cross_view(Sim& S, Step& T, const Isl& I, bool second) {
     S.b[2].w = lane_of3<1>(I.d1.w);
     S.b[3].v = lane_of3<1>(I.d2.v);
     S.b[3].w = lane_of3<1>(I.d2.w);
-    const Sym oM1 = opqs(I.d1.M), oM2 = opqs(I.d2.M);           // fixed during the solve: see opq
+    const Sym oM1 = I.d1.M, oM2 = I.d2.M;
     T.M[0] = lane_of_sym<0>(oM1);
     T.M[1] = lane_of_sym<0>(oM2);
     T.M[2] = lane_of_sym<1>(oM1);
@@ -1238,25 +1189,13 @@ struct Ctx {
 CP_DEV bool c44_ok(const Ctx& c);
 // how often (in sweeps) the reset kernels' sweep loops re-test whether every active lane of the wave
 // has the settle structure (the lanes without it usually converge first)
-#ifndef CP_C44_CHECK
-#define CP_C44_CHECK 8
-#endif
+constexpr int kC44Check = 8;
 CP_DEV bool c4k_ok(const Ctx& c);
 CP_DEV void sweeps_c44_slow(Ctx& c, real* pool, real tol, int it0, int it1, Stamps& ST);
 CP_DEV void sweeps_c4k_slow(Ctx& c, real* pool, real tol, int it0, int it1, Stamps& ST);
 CP_DEV bool p1_ok(const Ctx& c);
-CP_DEV void sweeps_p1_slow(Ctx& c, real* pool, real tol, int it0, int it1, Stamps& ST);
-// how often (in sweeps) the step kernels' sweep loops test whether every active lane of the wave is a
-// pole standing on the ground (p1_ok)
-#ifndef CP_P1_CHECK
-#define CP_P1_CHECK 8
-#endif
-#ifndef CP_PRIO_AFTER
-#define CP_PRIO_AFTER 16  // sweeps into a solve after which the step kernels' wave raises its priority (0: off)
-#endif
-#ifndef CP_PRIO_MODE
-#define CP_PRIO_MODE 0    // 0: for the rest of that solve; 1, 2: diagnostics (sticky, accumulated)
-#endif
+// sweeps into a solve after which the throughput step kernels' wave raises its issue priority
+constexpr int kPrioAfter = 16;
 // HX = false: no env of the wave is merged (checked by the caller), so the cross-row blocks and the merge of
 // their results into the island view are compiled out of the sweep
 template <bool C44 = false, bool PM = false, bool HX = true>
@@ -1271,56 +1210,30 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0,
     // ground pairs whose rows all have a +z normal in this wave run isl_row_ez (wave-uniform):
     // the ground-pole pair in every measured wave, the ground-cart pair in ~3 of 4 (PM: every row
     // has its own normal, the generic rows)
-#ifdef CP_NO_EZ
-    const bool ez0 = false, ez1 = false;
-#else
     const bool ez0 = !PM && __ballot(pk_cnt(c.T.pk[0]) > 0 && !is_plus_z(c.T.n[0])) == 0ull;
     const bool ez1 = !PM && __ballot(pk_cnt(c.T.pk[1]) > 0 && !is_plus_z(c.T.n[1])) == 0ull;
-#endif
 #ifdef CP_STAMPS
     ST.flags |= (ez0 ? 0u : 2u) | (ez1 ? 0u : 4u);
 #endif
     for (int it = it0; it < it1; ++it) {
         if (__ballot(c.active) == 0ull) break;
-#if CP_PRIO_AFTER > 0
         // a wave deep into a long solve (a capped env: the launch's tail) takes its SIMD's issue
         // priority from its co-resident partner: C3 +1.2 % (threshold 8, 16 or 30 alike)
         if constexpr (!C44) {
-#ifdef CP_PRIO_MERGED  // diagnostic: a wave holding a merged env (the launch's tail) raises its priority at once
-            if (it == it0 && __ballot(c.merged) != 0ull) __builtin_amdgcn_s_setprio(1);
-#endif
-            if (it == it0 + CP_PRIO_AFTER) {
-#if CP_PRIO_MODE == 2  // diagnostic: +1 per long solve of the step (the wave's level, up to 3)
-                const uint32_t lvl = __builtin_amdgcn_s_getreg((1 << 11) | (0 << 6) | 2) & 3u;  // STATUS.PRIORITY
-                if (lvl == 0u) __builtin_amdgcn_s_setprio(1);
-                else if (lvl == 1u) __builtin_amdgcn_s_setprio(2);
-                else __builtin_amdgcn_s_setprio(3);
-#else
+            if (it == it0 + kPrioAfter) {
                 __builtin_amdgcn_s_setprio(1);
-#endif
             }
         }
-#endif
         if constexpr (C44 && !PM) {  // every still-active lane in the settle structure (the reset kernels)
-            if ((it - it0) % CP_C44_CHECK == 0 && __ballot(c.active && !c44_ok(c)) == 0ull) {
+            if ((it - it0) % kC44Check == 0 && __ballot(c.active && !c44_ok(c)) == 0ull) {
                 sweeps_c44_slow(c, pool, tol, it, it1, ST);
                 return;
             }
-#ifndef CP_NO_C4K
             if (it == it0 && __ballot(c.active && !c4k_ok(c)) == 0ull) {  // the bump phase's structures
                 sweeps_c4k_slow(c, pool, tol, it, it1, ST);
                 return;
             }
-#endif
         }
-#ifdef CP_P1  // opt-in: measured slower in the step kernels
-        if constexpr (!C44 && !PM) {  // the step kernels: every still-active lane a pole standing on the ground
-            if ((it - it0) % CP_P1_CHECK == 0 && __ballot(c.active && !p1_ok(c)) == 0ull) {
-                sweeps_p1_slow(c, pool, tol, it, it1, ST);
-                return;
-            }
-        }
-#endif
 #ifdef CP_STAMPS
         ST.sweeps += 1;
 #endif
@@ -1364,9 +1277,7 @@ CP_DEV void sweeps(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* pool0,
         const uint32_t pbad = partner_u(bad ? 1u : 0u);
         if (c.active && !bad && !badc && pbad == 0u) c.active = false;
     }
-#if CP_PRIO_AFTER > 0 && CP_PRIO_MODE == 0  // modes 1 (sticky) and 2 (accumulated): kept to the wave's end
     if constexpr (!C44) __builtin_amdgcn_s_setprio(0);
-#endif
 }
 
 // ---- fast-form island rows.  Bullet's sequential-impulse solver
@@ -1391,12 +1302,8 @@ struct FRow {
     V3 rbt1, ib1, rbt2, ib2;
     real ie1, ie2, l1, l2;
 };
-// pair_body: B's box axes built after the broadphase, for the lanes it passes (CP_NO_LATE_BAX: A/B)
-#ifdef CP_NO_LATE_BAX
-constexpr bool kEarlyBax = true;
-#else
+// pair_body: B's box axes built after the broadphase, for the lanes it passes (built early: measured slower)
 constexpr bool kEarlyBax = false;
-#endif
 // HC2 = false: no lane of the wave has cart-pole rows (the pole off its cart: 72 % of a C3 episode's
 // wave-sweeps), the 60 values of c2 are not built (the latency kernels' general loop then needs ~60 fewer
 // registers, which were AGPR moves inside it)
@@ -1586,9 +1493,6 @@ CP_DEV void sweeps_c44(Ctx& c, FI& F, real tol, int it0, int it1, Stamps& ST) {
 #ifdef CP_STAMPS
         ST.sweeps += 1;
 #endif
-#ifdef CP_STAMP_C44  // diagnostic: settle-loop sweeps in the integration slot
-        ST.integ += 1;
-#endif
         bool bad = false;
         if (c.active) {
 #pragma unroll
@@ -1638,7 +1542,7 @@ CP_DEV void sweeps_c4k(Ctx& c, FI& F, real tol, int it0, int it1, Stamps& ST) {
     }
 }
 
-// sweeps_p1_slow with the rows in fast form (the latency-shaped step kernel)
+// the p1_ok island's rows (pole on the ground) in fast form, guard-free (the lean step loops)
 template <class FI>
 CP_DEV void sweeps_p1_fast(Ctx& c, FI& F, real tol, int it0, int it1, Stamps& ST) {
     const bool cart = pk_cnt(c.T.pk[0]) != 0;
@@ -1756,54 +1660,6 @@ CP_DEV bool p1_ok(const Ctx& c) {
            (c0 == 0 || (c0 == 4 && is_plus_z(c.T.n[0])));
 }
 
-// sweeps() for islands with p1_ok, rows from the LDS pool: the same rows in the same order (pair 0's
-// normal rows, pair 1's normal rows, pair 1's friction points; +z forms), the pole's rows without
-// per-row guards, the cart's behind one guard
-CP_DEV void sweeps_p1_slow(Ctx& c, real* pool, real tol, int it0, int it1, Stamps& ST) {
-    const bool cart = pk_cnt(c.T.pk[0]) != 0;
-    const int b1 = pk_base(c.T.pk[1]), f1 = pk_fbase(c.T.pk[1]);
-    for (int it = it0; it < it1; ++it) {
-        if (__ballot(c.active) == 0ull) break;
-#ifdef CP_STAMPS
-        ST.sweeps += 1;
-#endif
-        bool bad = false;
-        if (c.active) {
-            if (cart) {
-#pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    const V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
-                    real lam = pool_n(pool, F_LAM, s);
-                    bad |= isl_row_ez<1, 0, false>(c.I, rb, pool_n(pool, F_IE, s), pool_n(pool, F_TG, s), lam,
-                                                   real(0.0), tol);
-                    pool_n(pool, F_LAM, s) = lam;
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int s = b1 + k;
-                const V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
-                real lam = pool_n(pool, F_LAM, s);
-                bad |= isl_row_ez<2, 0, false>(c.I, rb, pool_n(pool, F_IE, s), pool_n(pool, F_TG, s), lam, real(0.0),
-                                               tol);
-                pool_n(pool, F_LAM, s) = lam;
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int s = b1 + k, fs = f1 + k;
-                const V3 rb = mk(pool_n(pool, F_RBX, s), pool_n(pool, F_RBY, s), pool_n(pool, F_RBZ, s));
-                const real bound = c.mu1 * pool_n(pool, F_LAM, s);
-                real l1 = pool_f(pool, FF_L1, fs), l2 = pool_f(pool, FF_L2, fs);
-                bad |= isl_row_ez<2, 1, true>(c.I, rb, pool_f(pool, FF_IE1, fs), real(0.0), l1, bound, tol);
-                bad |= isl_row_ez<2, 2, true>(c.I, rb, pool_f(pool, FF_IE2, fs), real(0.0), l2, bound, tol);
-                pool_f(pool, FF_L1, fs) = l1;
-                pool_f(pool, FF_L2, fs) = l2;
-            }
-        }
-        const uint32_t pbad = partner_u(bad ? 1u : 0u);  // every lane that entered the loop is here
-        if (c.active && !bad && pbad == 0u) c.active = false;
-    }
-}
 
 // sweeps() with the island rows in fast form (same row order, same stopping rule)
 template <bool C44, bool HC2, bool HX = true>
@@ -1814,44 +1670,24 @@ CP_DEV void sweeps_fast(Ctx& c, FastIslT<HC2>& F, Sim& S, const cp_physics& P, r
     const int fc1 = pk_fcnt(c.T.pk[1]);
     const V3 n0 = c.T.n[0], n1 = c.T.n[1], n2 = c.T.n[2];
     // ground pairs whose rows all have a +z normal in this wave run fast_grow_ez (wave-uniform)
-#ifdef CP_NO_EZ
-    const bool ez0 = false, ez1 = false;
-#else
     const bool ez0 = __ballot(cnt0 > 0 && !is_plus_z(n0)) == 0ull;
     const bool ez1 = __ballot(cnt1 > 0 && !is_plus_z(n1)) == 0ull;
-#endif
     for (int it = it0; it < it1; ++it) {
         if (__ballot(c.active) == 0ull) break;
-#ifndef CP_NO_C44
         // every still-active lane of the wave in the settle structure: the guard-free loop
         // (the reset kernel's option: there every settle substep is in it; in the step kernel
         // the periodic test cost more than it saved, 0.450 -> 0.480 ms at B = 4,096)
         if constexpr (C44 && HC2) {
-            if ((it - it0) % CP_C44_CHECK == 0 && __ballot(c.active && !c44_ok(c)) == 0ull) {
+            if ((it - it0) % kC44Check == 0 && __ballot(c.active && !c44_ok(c)) == 0ull) {
                 CP_STAMP(q0);
                 sweeps_c44(c, F, tol, it, it1, ST);
-#ifdef CP_STAMP_C44  // diagnostic: the settle loop's own cycles in the row-setup slot
-                CP_STAMP(q1);
-                CP_ACC(rows, q0, q1);
-#endif
                 return;
             }
-#ifndef CP_NO_C4K
             if (it == it0 && __ballot(c.active && !c4k_ok(c)) == 0ull) {  // the bump phase's structures
                 sweeps_c4k(c, F, tol, it, it1, ST);
                 return;
             }
-#endif
         }
-#endif
-#ifdef CP_P1  // opt-in: measured slower in the step kernels
-        if constexpr (!C44) {  // the step kernels: every still-active lane a pole standing on the ground
-            if ((it - it0) % CP_P1_CHECK == 0 && __ballot(c.active && !p1_ok(c)) == 0ull) {
-                sweeps_p1_fast(c, F, tol, it, it1, ST);
-                return;
-            }
-        }
-#endif
 #ifdef CP_STAMPS
         ST.sweeps += 1;
 #endif
@@ -1954,15 +1790,14 @@ CP_DEV void fast_store(const FastIslT<HC2>& F, const Ctx& c, real* pool) {
 //     every island of a reset's settle substeps, ~99 % of the bump substeps', a step's first substeps;
 //   p1_ok (FastP1, sweeps_p1_fast, step kernels): the pole lying or standing on the ground (93-98 % of the
 //     islands from step 26 of an episode on).
-// PRIO (the throughput step kernels): the wave raises its issue priority after CP_PRIO_AFTER sweeps, as sweeps().
+// PRIO (the throughput step kernels): the wave raises its issue priority after kPrioAfter sweeps, as sweeps().
 // Returns false (nothing done) when the wave is not uniform.
 template <bool C44, bool PRIO>
 CP_DEV bool solve_lean(Ctx& c, const cp_physics& P, real* pool, int it0, int it1, Stamps& ST) {
-#if !defined(CP_NO_C44) && !defined(CP_NO_C4K) && !defined(CP_STAMP_C44) && !defined(CP_NO_LEAN_C4)
     const real tol = sqrt_(real(P.residual_threshold));  // oracle: SQRT((real)threshold)
     // the sweeps in two segments around the priority raise (the loops stop at the first sweep with no
     // active lane, so the second segment continues exactly where the first left off)
-    const int itp = (PRIO && CP_PRIO_AFTER > 0 && it0 + CP_PRIO_AFTER < it1) ? it0 + CP_PRIO_AFTER : it1;
+    const int itp = (PRIO && it0 + kPrioAfter < it1) ? it0 + kPrioAfter : it1;
     auto run = [&](auto loop) {
         loop(it0, itp);
         if constexpr (PRIO) {
@@ -1973,11 +1808,7 @@ CP_DEV bool solve_lean(Ctx& c, const cp_physics& P, real* pool, int it0, int it1
             }
         }
     };
-#ifdef CP_NO_LEAN_STEP  // diagnostic: the step kernels without the lean structure loops (round-5 A/B)
-    if constexpr (C44) {
-#else
     {
-#endif
         if (__ballot(c.active && !c4k_ok(c)) == 0ull) {
             FastC4 F;
             fast_ground_rows<0>(F.g0, c, pool);
@@ -1995,7 +1826,6 @@ CP_DEV bool solve_lean(Ctx& c, const cp_physics& P, real* pool, int it0, int it1
             return true;
         }
     }
-#ifndef CP_NO_LEAN_STEP
     if constexpr (!C44) {
         if (__ballot(c.active && !p1_ok(c)) == 0ull) {
             FastP1 F;
@@ -2013,8 +1843,6 @@ CP_DEV bool solve_lean(Ctx& c, const cp_physics& P, real* pool, int it0, int it1
             return true;
         }
     }
-#endif
-#endif
     (void)c; (void)P; (void)pool; (void)it0; (void)it1; (void)ST;
     return false;
 }
@@ -2029,11 +1857,9 @@ CP_DEV void solve_range(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* p
         sweeps<false, true>(c, S, P, pool, pool0, second, it0, it1, ST);
         return;
     }
-#ifndef CP_NO_FAST_ROWS
     if constexpr (FAST) {
         if (__ballot(!fast_ok(c)) == 0ull) {
             if (solve_lean<C44, false>(c, P, pool, it0, it1, ST)) return;
-#ifndef CP_NO_HC2
             // the step kernels: no merged env in the wave (61-96 % of a C3 episode's wave-sweeps from step 26 on)
             // -> the general loop without the cross-row block, and without the cart-pole rows when no lane has
             // any (the cross block's whole-env view and the 60 cart-pole row values were AGPR moves in it)
@@ -2053,7 +1879,6 @@ CP_DEV void solve_range(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* p
                     return;
                 }
             }
-#endif
             FastIsl F;
             CP_STAMP(b0);
             fast_build(F, c, pool);
@@ -2061,49 +1886,14 @@ CP_DEV void solve_range(Ctx& c, Sim& S, const cp_physics& P, real* pool, real* p
             sweeps_fast<C44>(c, F, S, P, pool, pool0, second, it0, it1, ST);
             CP_STAMP(b2);
             fast_store(F, c, pool);
-#ifdef CP_STAMP_C44  // diagnostic: fast_build in the box-selection slot, the rest of sweeps_fast outside the
-                     // settle loop in the box_box slot (fast_store is a few LDS writes)
-            CP_STAMP(b3);
-            CP_ACC(sel, b0, b1);
-            CP_ACC(bb, b1, b2);
-            (void)b3;
-#endif
             return;
         }
     }
-#endif
-#ifdef CP_LEAN_F64
-    // diagnostic: the lean structure loops in the fp64 step kernels (1 wave per SIMD, 512 registers)
-    if constexpr (!C44 && !PM && sizeof(real) == 8) {
-        if (__ballot(!fast_ok(c)) == 0ull && solve_lean<false, false>(c, P, pool, it0, it1, ST)) return;
-    }
-#endif
-#ifdef CP_LEAN_TP
-    // opt-in diagnostic: the lean structure loops in the throughput step kernels as well (FAST = false: no room
-    // for the whole fast form at 2 waves per SIMD).  Measured slower (round 5: C3 step kernel 0.508 -> 0.528 ms,
-    // scratch 80 -> 120 B/lane; without an env sort only ~23 % of the wave-sweeps are in uniform waves)
-    if constexpr (!C44 && sizeof(real) == 4) {  // (fp64: the lean rows spill there, 240 -> 704 B/lane)
-        if (__ballot(!fast_ok(c)) == 0ull && solve_lean<false, true>(c, P, pool, it0, it1, ST)) return;
-    }
-#endif
-#ifndef CP_NO_LEAN_TR
     // the throughput-shaped (burst) reset kernel: its settle and bump substeps are one structure in (nearly) every
     // wave, so the lean settle rows (FastC4, ~100 values) in registers instead of the LDS-row settle loop
     if constexpr (C44 && !FAST && !PM) {  // (fp64: the latency-shaped reset kernel, 512 registers)
         if (__ballot(!fast_ok(c)) == 0ull && solve_lean<true, false>(c, P, pool, it0, it1, ST)) return;
     }
-#endif
-#ifdef CP_HX_TP
-    // opt-in diagnostic: the throughput kernels' sweep without the cross-row blocks when no env of the wave is
-    // merged (61-96 % of a C3 episode's wave-sweeps from step 26).  Measured slower (round 5: C3 kernel
-    // 0.503 -> 0.511 ms, driver window -2.5 %): the second copy of the sweep raises the scratch frame 80 -> 112 B
-    if constexpr (!C44 && !PM) {
-        if (__ballot(c.active && c.merged) == 0ull) {
-            sweeps<C44, PM, false>(c, S, P, pool, pool0, second, it0, it1, ST);
-            return;
-        }
-    }
-#endif
     sweeps<C44>(c, S, P, pool, pool0, second, it0, it1, ST);
 }
 
@@ -2288,17 +2078,10 @@ CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, rea
             plive = live && !(((c.slp >> (bb - 1)) & 1u) || (a > 0 && ((c.slp >> (a - 1)) & 1u)));
         }
         CP_STAMP(n0);
-        // warm-start cache of the pair (CP_NO_WSM: loaded first for every pair, its latency overlapping the
-        // narrowphase; else loaded below for the pairs past the broadphase only, the old point count from O.wsm)
+        // warm-start cache of the pair: loaded below for the pairs past the broadphase only, the old point
+        // count from O.wsm (loading it first for every pair, to overlap the narrowphase, was measured slower)
         uint32_t oid = 0xFFFFFFFFu;
         real ol0 = real(0.0), ol1 = real(0.0), ol2 = real(0.0), ol3 = real(0.0);
-#ifdef CP_NO_WSM
-        if constexpr (!PM) {
-            oid = to_bits(G.lw(CP_SF_WS_ID(0, j)));
-            ol0 = G.ll(CP_SF_WS_LAM(0, j, 0)); ol1 = G.ll(CP_SF_WS_LAM(0, j, 1));
-            ol2 = G.ll(CP_SF_WS_LAM(0, j, 2)); ol3 = G.ll(CP_SF_WS_LAM(0, j, 3));
-        }
-#endif
         // the island flag through a volatile empty asm per pair: the box selections below are
         // otherwise loop-invariant per branch, and hoisting all of them out of the pair loop
         // keeps every body's axes live across the narrowphase (spills)
@@ -2369,14 +2152,11 @@ CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, rea
         // the points within the pair's relative breaking threshold
         const real newmargin = PM ? real(0.0) : real(P.contact_margin);
         const bool near = plive && !face_separated(A, Bx, newmargin);  // (B's centre and extents only)
-#ifndef CP_NO_LATE_BAX
         // (PM: the persistent manifold's refresh reads B's axes on every live lane: built early there)
         // B's axes for the pairs the broadphase passes (box_box, the row setup's inertias); the other lanes keep
         // the identity box_of<.., .., false> gave them, which nothing of theirs reads
         if constexpr (!PM)
             if (near) Bx.ax = quat_axes(bqv[0], bqv[1], bqv[2], bqv[3]);
-#endif
-#ifndef CP_NO_WSM
         // a pair the broadphase separates makes no point: its cache is not read (m = 0, the id word's old count
         // from O.wsm decides the rewrite below); the others load it here, its latency overlapping box_box
         if constexpr (!PM) {
@@ -2386,7 +2166,6 @@ CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, rea
                 ol2 = G.ll(CP_SF_WS_LAM(0, j, 2)); ol3 = G.ll(CP_SF_WS_LAM(0, j, 3));
             }
         }
-#endif
         if (near) box_box<ALLIN, ES>(A, Bx, newmargin, P.edge_bias, C, ST);
         PMan M;
         M.cnt = 0;
@@ -2403,10 +2182,8 @@ CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, rea
             }
         }
         CP_STAMP(n2);
-#if !defined(CP_STAMP_C44) && !defined(CP_STAMP_BB)
         CP_ACC(sel, n0, n1);
         CP_ACC(bb, n1, n2);
-#endif
         const int base = used, fbase = fused;
         int m = 0, fm = 0;
         uint32_t nid = 0xFFFFFFFFu;
@@ -2481,29 +2258,15 @@ CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, rea
         used = base + m;
         fused = fbase + fm;
         CP_STAMP(n3);
-#if !defined(CP_STAMP_C44) && !defined(CP_STAMP_BB)
         CP_ACC(rows, n2, n3);
-#endif
         // old point count = the leading non-0xFF bytes of the old id word (written as a prefix)
-#ifdef CP_NO_WSM
-        const int om = (oid & 0xFFu) == 0xFFu ? 0 : ((oid >> 8) & 0xFFu) == 0xFFu ? 1
-                     : ((oid >> 16) & 0xFFu) == 0xFFu ? 2 : ((oid >> 24) & 0xFFu) == 0xFFu ? 3 : 4;
-        const bool idw = nid != oid;
-#else
         const int om = (int)((O.wsm >> (3 * j)) & 7u);
         // the id word changes when the new prefix differs from the old word: loaded when near; a separated pair's
         // new word is all 0xFF, which differs from the old exactly when that held a point or was not a prefix
         const bool idw = near ? nid != oid : om > 0;
         if (!PM && plive) O.wsm = (O.wsm & ~(7u << (3 * j))) | ((uint32_t)m << (3 * j));
-#endif
         const uint32_t pk = (uint32_t)m | ((uint32_t)base << 3) | ((uint32_t)fm << 8) | ((uint32_t)fbase << 11) |
                             ((uint32_t)(plive ? (m > om ? m : om) : 0) << 16);
-#ifdef CP_HDR_SCRATCH
-        G.sx(4 * j + 0, C.n.x);
-        G.sx(4 * j + 1, C.n.y);
-        G.sx(4 * j + 2, C.n.z);
-        G.sx(4 * j + 3, bits_to<real>(pk));
-#else
         // the pair's manifold header into registers: a select per slot on the wave-uniform j
         // (a switch is merged back into one indexed store, which keeps T in private memory)
 #pragma unroll
@@ -2512,25 +2275,12 @@ CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, rea
             T.n[q] = selv(h, C.n, T.n[q]);
             T.pk[q] = h ? pk : T.pk[q];
         }
-#endif
         if (!PM && plive && idw) G.sw(CP_SF_WS_ID(0, j), bits_to<real>(nid));  // unchanged: no write
     };
-#ifdef CP_NO_GROUND_PEEL
-#pragma unroll 1
-    for (int j = 0; j < CP_ISLAND_PAIRS; ++j) pair_body(std::false_type{}, j);
-#else
 #pragma unroll 1
     for (int j = 0; j < 2; ++j) pair_body(std::true_type{}, j);
 #pragma unroll 1
     for (int j = 2; j < CP_ISLAND_PAIRS; ++j) pair_body(std::false_type{}, j);
-#endif
-#ifdef CP_HDR_SCRATCH
-#pragma unroll
-    for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
-        T.n[j] = mk(G.lx(4 * j + 0), G.lx(4 * j + 1), G.lx(4 * j + 2));
-        T.pk[j] = to_bits(G.lx(4 * j + 3));
-    }
-#endif
     CP_STAMP(t1);
     CP_ACC(narrow, t0, t1);
     // 3. unconstrained velocity update of the lane's own bodies (island 0's lane: cart, pole)
@@ -2584,9 +2334,6 @@ CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, rea
     const uint32_t own_xf = (pk_fcnt(T.pk[3]) + pk_fcnt(T.pk[4])) > 0 ? 1u : 0u;
     const uint32_t any_xf = own_xf | partner_u(own_xf);  // unconditionally, like any_cross
     c.xfric = (any_cross & any_xf) != 0u;
-#ifdef CP_DIAG_NO_CROSS  // diagnostic only (wrong physics for merged envs): what the cross-row code costs
-    c.merged = false;
-#endif
 #ifdef CP_STAMPS
     ST.flags |= __ballot(c.merged) != 0ull ? 1u : 0u;
 #endif
@@ -2699,9 +2446,7 @@ CP_DEV void substep_finish(Own& O, const cp_physics& P, const Lane& L, const Ctx
     integrate(O.p, bit0 + 1);
     if constexpr (SLP) sleep_update(O, P);  // updateActivationState, after the integration
     CP_STAMP(t4);
-#ifndef CP_STAMP_C44
     CP_ACC(integ, t3, t4);
-#endif
 #ifdef CP_STAMPS
     ST.substeps += 1;
 #endif

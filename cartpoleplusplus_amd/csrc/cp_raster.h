@@ -381,8 +381,6 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_kernel(
 }
 
 // ---- small frames (the reference's 50 x 50): one block per env, dense ray tests ----
-// (diagnostic builds: -DCP_RV_NO_DENSE / -DCP_RV_NO_OUTPUT / -DCP_RV_NO_STORE drop a
-// phase to time the others; tools/variant_raster.sh)
 // Per frame an LDS code buffer holds, per pixel, what it shows: the static ground
 // class (face 0..5, or 30 = background) to start with, then body b's face f as
 // b * 6 + f once a box is nearer, with its depth in a depth buffer.  Every box is
@@ -506,7 +504,6 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small_kernel(
     __syncthreads();
 
     // dense ray tests: frame by frame, body by body
-#ifndef CP_RV_NO_DENSE
     for (int f = 0; f < F; ++f) {
         const int cam = f / R, r = f % R;
         uint8_t* cf = scode + f * npx;
@@ -542,13 +539,9 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small_kernel(
             __syncthreads();  // the next body compares against this one's hits
         }
     }
-#endif
 
     // colours, strips of 64 pixels per wave
     uint16_t* out = pixels + (size_t)env * npx * per_px;
-#ifdef CP_RV_NO_OUTPUT
-    if (npx > 0) return;
-#endif
     for (int p0 = wave * WAVE_R; p0 < npx; p0 += RENDER_WAVES * WAVE_R) {
         const int p = p0 + lane;
         const bool valid = p < npx;
@@ -565,7 +558,6 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small_kernel(
             }
         }
         wave_sync();
-#ifndef CP_RV_NO_STORE
         const int nh = ((npx - p0) < WAVE_R ? (npx - p0) : WAVE_R) * per_px;
         const int tot = sh + nh;
         uint4* d4 = reinterpret_cast<uint4*>(dst - sh);
@@ -578,7 +570,6 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small_kernel(
                 for (int e = (h0 > sh ? h0 : sh); e < (h0 + 8 < tot ? h0 + 8 : tot); ++e) dst[e - sh] = stage[e];
             }
         }
-#endif
         wave_sync();
     }
 }
@@ -603,10 +594,7 @@ template <int NF> using CodeWord = typename CodeWordT<(NF <= 3)>::T;
 // strip edge by less than that; 16-byte multiples)
 template <int NF>
 __host__ __device__ constexpr int small2_stage_halves() { return 24 + WAVE_R * 8 + 24; }
-#ifndef CP_RV_SPT
-#define CP_RV_SPT 2
-#endif
-constexpr int SMALL2_SPT = CP_RV_SPT;  // strips per trip of the colour pass (independent chains between syncs)
+constexpr int SMALL2_SPT = 2;  // strips per trip of the colour pass (independent chains between syncs)
 template <int NF>
 __host__ __device__ inline Small2Lds render_small2_lds(int C, int R, int npx) {
     static_assert(NF <= 6, "five-bit code fields: at most 6 frames in a word");
@@ -634,9 +622,6 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
     extern __shared__ __align__(16) unsigned char render_lds_raw[];
     if ((int)blockIdx.x >= *count) return;  // block-uniform
     const int env = list[blockIdx.x];
-#if defined(CP_RV_STOP) && CP_RV_STOP == 0  // diagnostic: the launch alone
-    if (env >= 0) return;
-#endif
     const int tid = threadIdx.x, wave = tid / WAVE_R, lane = tid % WAVE_R;
     constexpr int C = CC;
     const int W = rc.width, H = rc.height, npx = W * H;
@@ -740,12 +725,8 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
         slut[it] = make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2]);
     }
     __syncthreads();
-#if defined(CP_RV_STOP) && CP_RV_STOP == 1  // diagnostic: the launch + the scene setup
-    if (env >= 0) return;
-#endif
 
     // dense ray tests: frame by frame, body by body (cp_render_small_kernel's, pixel-major codes)
-#ifndef CP_RV_NO_DENSE
 #pragma unroll 1
     for (int f = 0; f < NF; ++f) {
         const int cam = f / R, r = f % R;
@@ -783,7 +764,6 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
             __syncthreads();  // the next body compares against this one's hits
         }
     }
-#endif
 
     // colours, in strips of 64 output chunks: chunk q is the 16 bytes at out + 16 q - (out mod 16), so
     // every strip is 16-byte aligned and each lane stores one whole chunk; the pixels overlapping the
@@ -797,9 +777,6 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
     constexpr int M = 24;                                                // stage margin (>= PP, 16-byte multiple)
     static_assert(PP <= M, "small2_stage_halves: the margins must hold a pixel's values");
     uint4* d4 = reinterpret_cast<uint4*>(out - sh);
-#ifdef CP_RV_NO_OUTPUT
-    if (Q > 0) return;
-#endif
     constexpr int SH = small2_stage_halves<NF>();
     // two strips per trip (stage u = 0, 1): two independent load / LUT / stage chains between syncs;
     // wave w takes strips w, w + 4, w + 8, ... (in units of 64 chunks)
@@ -857,11 +834,7 @@ __global__ void __launch_bounds__(RENDER_WAVES * WAVE_R) cp_render_small2_kernel
         for (int u = 0; u < SMALL2_SPT; ++u) {
             const int q = s0 + u * RENDER_WAVES * WAVE_R + lane;
             const int e0 = q * 8 - sh;                                  // the chunk's first value
-#ifdef CP_RV_NO_STORE
-            if (q < 0) {
-#else
             if (q < Q) {
-#endif
                 const uint16_t* src = stage + u * SH + M + lane * 8;
                 if (e0 >= 0 && e0 + 8 <= N) {
                     store_stream(&d4[q], *reinterpret_cast<const uint4*>(src));
