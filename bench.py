@@ -236,6 +236,8 @@ def workload(args, world):
         s += f", as {args.streams} shard handles of {B // args.streams:,} envs on {args.streams} HIP streams"
     if getattr(args, "shape", "auto") != "auto":
         s += f", kernel shape {args.shape}"
+    if getattr(args, "reset_shape", None) not in (None, "auto"):
+        s += f", reset kernel shape {args.reset_shape}"
     if getattr(args, "persistent", False):
         s += ", CP_MODEL_PERSISTENT contact model (Bullet's persistent manifold; model-fidelity variant)"
     if getattr(args, "sleeping", False):
@@ -522,6 +524,9 @@ def gym_mirror_rate(steps=400):
     np_state = np.random.get_state()   # the mirror draws its bumps from np.random, as the reference does
     np.random.seed(0)
     try:
+        env.reset()
+        for _ in range(20):   # warm-up: the step graph's capture and the first launches stay out of the window
+            env.step(rng.integers(0, 5, 2))
         t0 = time.perf_counter()
         env.reset()
         t_reset = time.perf_counter() - t0
@@ -534,13 +539,15 @@ def gym_mirror_rate(steps=400):
                 resets += 1
         dt = time.perf_counter() - t0
         use_graph = env.use_graph
+        shape = "/".join(env._env.kernel_shape())
     finally:
         env.close()
         np.random.set_state(np_state)
     return {"value": round(n / dt, 1), "unit": "env-steps/s", "ms_per_step": round(dt / n * 1e3, 4),
             "reset_ms": round(t_reset * 1e3, 2), "step_as_hipgraph": use_graph,
+            "kernel_shape": shape,
             "sample": f"C1 config on the GPU: B=1, R=2, F_init 55, discrete random actions, {n} steps incl. "
-                      f"{resets} resets ({dt:.2f} s)"}
+                      f"{resets} resets ({dt:.2f} s), after 20 warm-up steps (the step graph's capture)"}
 
 
 def _pose_diffs(g, o):
@@ -848,8 +855,10 @@ def main():
     ap.add_argument("--streams", type=int, default=1, metavar="S",
                     help="run the GPU's batch as S shard handles on S HIP streams (the C4 shard rule inside one "
                          "GPU; each env computes what it computes in one handle)")
-    ap.add_argument("--shape", choices=("auto", "throughput", "latency"), default="auto",
+    ap.add_argument("--shape", choices=("auto", "throughput", "latency", "wide"), default="auto",
                     help="kernel shapes (cp_set_kernel_shape) of the step and autoreset kernels")
+    ap.add_argument("--reset-shape", choices=("auto", "throughput", "latency", "wide"), default=None,
+                    help="the autoreset kernel's shape when it differs from --shape")
     ap.add_argument("--sleeping", action="store_true",
                     help="the CP_MODEL_SLEEPING model (Bullet's deactivation: resting islands sleep after 2 s; "
                          "latency-shaped kernels; a model-fidelity variant, not the headline)")
@@ -908,8 +917,8 @@ def main():
         env = StreamShards(args.streams, B, local, spec["env_id_offset"], **env_kw)
     else:
         env = BatchedCartpole(B, local, env_id_offset=spec["env_id_offset"], **env_kw)
-    if args.shape != "auto":
-        env.set_kernel_shape(args.shape, args.shape)
+    if args.shape != "auto" or args.reset_shape not in (None, "auto"):
+        env.set_kernel_shape(args.shape, args.reset_shape or args.shape)
     if args.raster:
         env.enable_raster(True, num_cameras=args.cameras)
     ss_steps = 0 if args.no_steady_state else WINDOW
@@ -1076,6 +1085,7 @@ def main():
     headline = not (args.rollout or args.continuous or args.dtype != "f32" or args.done_on_bounds or args.persistent
                     or args.sleeping
                     or args.streams > 1 or args.raster or next_step or args.shape != "auto"
+                    or args.reset_shape not in (None, "auto")
                     or args.solver_iterations is not None or args.batch != 65536 or args.repeats != 3)
     if rank == 0 and world == 1 and headline and not (args.no_secondary or args.no_cpu_baseline):
         log("secondary configurations ...")

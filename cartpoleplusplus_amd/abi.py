@@ -106,7 +106,8 @@ CP_MODEL_GPU_FLAGS = 0xC
 CP_SHAPE_AUTO = -1
 CP_SHAPE_THROUGHPUT = 0
 CP_SHAPE_LATENCY = 1
-SHAPES = {"auto": CP_SHAPE_AUTO, "throughput": CP_SHAPE_THROUGHPUT, "latency": CP_SHAPE_LATENCY}
+CP_SHAPE_WIDE = 2
+SHAPES = {"auto": CP_SHAPE_AUTO, "throughput": CP_SHAPE_THROUGHPUT, "latency": CP_SHAPE_LATENCY, "wide": CP_SHAPE_WIDE}
 
 
 class cp_config(C.Structure):

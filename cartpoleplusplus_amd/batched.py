@@ -218,8 +218,8 @@ class BatchedCartpole:
         return obs[:K], rew[:K], done[:K], (term_obs[:K] if want_term else None)
 
     def set_kernel_shape(self, step="auto", reset="auto"):
-        """Override the step / autoreset kernel shapes ("auto", "throughput" or "latency";
-        cp_set_kernel_shape).  Both shapes compute the same numbers."""
+        """Override the step / autoreset kernel shapes ("auto", "throughput", "latency" or "wide";
+        cp_set_kernel_shape).  Every shape computes the same numbers."""
         native.check(self.h, self.lib.cp_set_kernel_shape(self.h, abi.SHAPES[step], abi.SHAPES[reset]),
                      "cp_set_kernel_shape")
 
@@ -227,7 +227,7 @@ class BatchedCartpole:
         """-> (step shape, reset shape) in use: "throughput" or "latency"."""
         st, rs = C.c_int(), C.c_int()
         native.check(self.h, self.lib.cp_get_kernel_shape(self.h, C.byref(st), C.byref(rs)), "cp_get_kernel_shape")
-        names = {abi.CP_SHAPE_THROUGHPUT: "throughput", abi.CP_SHAPE_LATENCY: "latency"}
+        names = {abi.CP_SHAPE_THROUGHPUT: "throughput", abi.CP_SHAPE_LATENCY: "latency", abi.CP_SHAPE_WIDE: "wide"}
         return names[st.value], names[rs.value]
 
     def enable_readback(self, on=True, reference_bug=True):

@@ -159,13 +159,13 @@ struct Bufs {
 #define CP_DECLARE_LAUNCHES(NS)                                                                                  \
     namespace NS {                                                                                               \
     void launch_init(const cp_config& cfg, const cpc::Bufs& b, hipStream_t st);                                  \
-    void launch_reset(bool lat, const cp_config& cfg, const cpc::Bufs& b, float* obs_out, hipStream_t st);      \
+    void launch_reset(int shape, const cp_config& cfg, const cpc::Bufs& b, float* obs_out, hipStream_t st);     \
     void launch_nextstep_fixup(const cp_config& cfg, const cpc::Bufs& b, const int32_t* list, const int32_t* count, \
                                int q, const float* nobs, float* obs_out, float* reward_out, uint8_t* done_out,    \
                                hipStream_t st);                                                                    \
     void launch_nextstep_resolve(const cp_config& cfg, const cpc::Bufs& b, const uint8_t* mask, const float* nobs, \
                                  float* obs_out, hipStream_t st);                                                  \
-    void launch_step(bool lat, int kind, const cp_config& cfg, const cpc::Bufs& b, const void* actions,          \
+    void launch_step(int shape, int kind, const cp_config& cfg, const cpc::Bufs& b, const void* actions,         \
                      float* obs_out, float* reward_out, uint8_t* done_out, float* term_out, float* readback,    \
                      int rb_bug, const cpc::Lqr& lq, hipStream_t st);                                            \
     void launch_rollout(bool lat, int kind, const cp_config& cfg, const cpc::Bufs& b, int steps,                 \

@@ -334,19 +334,24 @@ __global__ void __launch_bounds__(256) cp_init_kernel(cp_config cfg, Bufs b) {
 // (fixed-length episodes end together).  LAT = true: one wave per SIMD with 512 registers and
 // fast-form rows, for the short lists of desynchronised episodes (bounds termination), where
 // the 130 serial substeps of one wave are the whole latency of the step.
-template <bool LAT, bool PM = false, bool SLP = false>
+// WIDE (latency shape only): 16 lanes per env, 8 replicas of the env's lane pair that divide the narrowphase
+// (narrow_wide, cp_physics.h); lane 0 of the 16 is the lead, lanes 0-1 store the state.
+template <bool LAT, bool PM = false, bool SLP = false, bool WIDE = false>
 __global__ void __launch_bounds__(WAVE)
 __attribute__((amdgpu_waves_per_eu(LAT ? 1 : CP_WAVES_PER_EU, LAT ? 1 : CP_WAVES_PER_EU)))
 cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
+    static_assert(!WIDE || (LAT && !PM && !SLP), "WIDE: latency shape, default contact model");
+    constexpr int LW = WIDE ? 16 : 2;  // lanes per env
     __shared__ real lds_pool[(PM ? POOL_FLOATS_PM : POOL_FLOATS) * WAVE];
     const int B = cfg.num_envs;
     const int t = blockIdx.x * WAVE + threadIdx.x;
     if (t == 0 && b.count_next) *b.count_next = 0;  // the next cp_step's list starts empty
     const int n = *b.count;
-    if ((t >> 1) >= n) return;  // lane pairs past the compacted list
+    if ((t / LW) >= n) return;  // envs past the compacted list
     const int isl = t & 1;
-    const bool lead = isl == 0;
-    const int i = b.list[t >> 1];
+    const bool lead = (t & (LW - 1)) == 0;
+    const bool owner = (t & (LW - 1)) < 2;  // the lane pair that stores the env's state (WIDE: replica 0)
+    const int i = b.list[t / LW];
     // the env index through an opaque copy where the substeps and the epilogue address the state: the
     // lane's SoA offsets are rebuilt there instead of living through the 130 substeps (cp_step_kernel)
     auto late_i = [&]() {
@@ -354,10 +359,12 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
         asm volatile("" : "+v"(x));
         return x;
     };
-    real* pool = lds_pool + threadIdx.x;
-    real* pool0 = lds_pool + (threadIdx.x & ~1u);
+    // WIDE: the replicas of an island share its pool column (the replica-0 lane's)
+    real* pool0 = lds_pool + (threadIdx.x & ~(LW - 1u));
+    real* pool = WIDE ? pool0 + isl : lds_pool + threadIdx.x;
     const Mem G = Mem::make(b.state, b.scratch, B, i, isl, b.pman);
-    const Lane L = Lane::make(isl, cfg.phys);
+    Lane L = Lane::make(isl, cfg.phys);
+    L.pj = (int)((t & (LW - 1)) >> 1);
     Stamps ST;
     CP_STAMP(k0);
     CP_RT(r0);
@@ -381,7 +388,7 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     const int nsub = cfg.settle_steps + cfg.initial_force_steps;
     for (int s = 0; s < nsub; ++s) {
         const Mem Gs = (LAT && !kF64) ? G : Mem::make(b.state, b.scratch, B, late_i(), isl, b.pman);
-        substep<LAT && !kF64, true, true, PM, SLP>(O, cfg.phys, L, pool, pool0, ov, Gs, ST);
+        substep<LAT && !kF64, true, true, PM, SLP, WIDE>(O, cfg.phys, L, pool, pool0, ov, Gs, ST);
         const int k = s - cfg.settle_steps;
         if (k >= 0) {  // bump the lane's own cart (cart, then cart2 in the reference's draw order)
             real fx, fy;
@@ -397,11 +404,11 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
 #endif
     const Mem Ge = (LAT && !kF64) ? G : Mem::make(b.state, b.scratch, B, late_i(), isl, b.pman);
     const int il = late_i();
-    store_own(O, Ge, isl);  // each lane stores its own island
+    if (owner) store_own(O, Ge, isl);  // each lane stores its own island
     if constexpr (SLP) store_sleep(O, Ge, isl);
     const bool fin = env_finite(O);
     const int R = cfg.action_repeats;
-    if (b.rposes)  // every repeat slot shows the reset pose (bullet_cartpole.py:342-345)
+    if (b.rposes && owner)  // every repeat slot shows the reset pose (bullet_cartpole.py:342-345)
         for (int r = 0; r < R; ++r) write_rposes_own(O, isl, b.rposes + ((size_t)il * R + r) * CP_NUM_DYN * 7);
     if (!lead) return;
     b.overflow[il] += ov;
@@ -419,24 +426,29 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
 }
 
 // LAT: the latency shape of cp_reset_kernel<true> (1 wave per SIMD, 512 registers, fast-form
-// rows) for batches whose waves all get a SIMD of their own (<= 32,768 envs)
-template <int KIND, bool LQR, bool LAT, bool PM = false, bool SLP = false>
+// rows) for batches whose waves all get a SIMD of their own (<= 32,768 envs).  WIDE: the latency shape on
+// 16 lanes per env (cp_reset_kernel), for batches that leave most SIMDs idle.
+template <int KIND, bool LQR, bool LAT, bool PM = false, bool SLP = false, bool WIDE = false>
 __global__ void __launch_bounds__(WAVE)
 __attribute__((amdgpu_waves_per_eu(LAT ? 1 : CP_WAVES_PER_EU, LAT ? 1 : CP_WAVES_PER_EU)))
 cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float* reward_out, uint8_t* done_out,
                float* term_out, float* readback, int rb_bug, Lqr lq) {
+    static_assert(!WIDE || (LAT && !PM && !SLP), "WIDE: latency shape, default contact model");
+    constexpr int LW = WIDE ? 16 : 2;  // lanes per env
     __shared__ real lds_pool[(PM ? POOL_FLOATS_PM : POOL_FLOATS) * WAVE];
     const int B = cfg.num_envs;
     const int t = blockIdx.x * WAVE + threadIdx.x;
     // the next call's reset-list counter (the reset kernel zeroes it too): cp_step launches no reset
     // kernel on calls where no episode can end (cp_kernels.hip may_finish)
     if (t == 0 && b.count_next) *b.count_next = 0;
-    const int i = t >> 1, isl = t & 1;
-    const bool lead = isl == 0;  // lane 0 of the pair writes the env's outputs
+    const int i = t / LW, isl = t & 1;
+    const bool lead = (t & (LW - 1)) == 0;  // lane 0 of the env's lanes writes the env's outputs
+    const bool owner = (t & (LW - 1)) < 2;  // the lane pair that stores the env's state (WIDE: replica 0)
     const bool inb = i < B;
     const int R = cfg.action_repeats, SR = cfg.steps_per_repeat;
-    real* pool = lds_pool + threadIdx.x;
-    real* pool0 = lds_pool + (threadIdx.x & ~1u);
+    // WIDE: the replicas of an island share its pool column (the replica-0 lane's)
+    real* pool0 = lds_pool + (threadIdx.x & ~(LW - 1u));
+    real* pool = WIDE ? pool0 + isl : lds_pool + threadIdx.x;
     bool want_reset = false;
     bool render_me = false;  // simulated this step: its frames go to the render kernel
     Stamps ST;
@@ -457,7 +469,8 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
     CP_RT(r0);
     if (inb) {
         const Mem G = Mem::make(b.state, b.scratch, B, i, isl, b.pman);
-        const Lane L = Lane::make(isl, cfg.phys);
+        Lane L = Lane::make(isl, cfg.phys);
+        L.pj = (int)((t & (LW - 1)) >> 1);
         const SoaF term = SoaF::make(b.term_obs, B, R * 14);
         const uint32_t toff = SoaF::eoff(i);
         float* obs = obs_out + (size_t)i * R * 14;
@@ -507,11 +520,10 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
                     // through the loop; scratch 48 -> 24 B/lane); the 0-scratch latency kernels keep G (a lone wave
                     // pays the rebuild: latency reset list +2.6 %)
                     const Mem Gs = (LAT && !kF64) ? G : Mem::make(b.state, b.scratch, B, late_i(), late_isl(), b.pman);
-                    substep<LAT && !kF64, false, true, PM, SLP>(O, cfg.phys, L, pool,
-                                                                                                   pool0, ov, Gs, ST);
+                    substep<LAT && !kF64, false, true, PM, SLP, WIDE>(O, cfg.phys, L, pool, pool0, ov, Gs, ST);
                     if constexpr (LQR) {  // disturbance + control (:897-901), control from the pre-step state
                         apply_force_link(O, fa + u[0], fb + u[1]);
-                        float* s8 = lq.state8 ? lq.state8 + (((size_t)i * R + r) * SR + s) * 16 : nullptr;
+                        float* s8 = (lq.state8 && owner) ? lq.state8 + (((size_t)i * R + r) * SR + s) * 16 : nullptr;
                         lqr_done |= lqr_observe(O, second, cfg, lq, K, u, s8);
                     } else {
                         apply_force_link(O, fa, fb);
@@ -533,7 +545,7 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
 #pragma unroll
                     for (int f = 0; f < 14; ++f) put_out(&orow[f], row[f]);
                 }
-                if (b.rposes) write_rposes_own(O, isl, b.rposes + ((size_t)late_i() * R + r) * CP_NUM_DYN * 7);
+                if (b.rposes && owner) write_rposes_own(O, isl, b.rposes + ((size_t)late_i() * R + r) * CP_NUM_DYN * 7);
             }
             render_me = lead && b.rposes != nullptr;
             ov += (int)partner_u((uint32_t)ov);
@@ -545,7 +557,7 @@ cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float
             bool done = steps >= cfg.max_episode_len;
             if (cfg.done_on_bounds && bounds_exceeded(O, cfg)) done = true;
             if (LQR && lqr_done) done = true;
-            store_own(O, Ge, isle);  // each lane stores its own island
+            if (owner) store_own(O, Ge, isle);  // each lane stores its own island
             if constexpr (SLP) store_sleep(O, Ge, isle);
             const bool fin = env_finite(O);
             if (lead) {
@@ -883,8 +895,11 @@ void launch_nextstep_resolve(const cp_config& cfg, const Bufs& b, const uint8_t*
                        nobs, obs_out);
 }
 
-void launch_reset(bool lat, const cp_config& cfg, const Bufs& b, float* obs_out, hipStream_t st) {
-    const dim3 grid(env_grid(2 * cfg.num_envs, WAVE)), block(WAVE);  // two lanes per env
+// shape: 0 throughput, 1 latency, 2 latency on the WIDE layout (cp_set_kernel_shape; fp32 default model only)
+void launch_reset(int shape, const cp_config& cfg, const Bufs& b, float* obs_out, hipStream_t st) {
+    const bool lat = shape != 0;
+    const bool wide = shape == 2 && !kF64 && !(cfg.phys.model_flags & (CP_MODEL_PERSISTENT | CP_MODEL_SLEEPING));
+    const dim3 grid(env_grid((wide ? 16 : 2) * cfg.num_envs, WAVE)), block(WAVE);  // lanes per env
     if (cfg.phys.model_flags & CP_MODEL_PERSISTENT) {  // the persistent-manifold model: latency shape only
         hipLaunchKernelGGL((cp_reset_kernel<true, true>), grid, block, 0, st, cfg, b, obs_out);
         return;
@@ -897,16 +912,19 @@ void launch_reset(bool lat, const cp_config& cfg, const Bufs& b, float* obs_out,
         (void)lat;
         hipLaunchKernelGGL(cp_reset_kernel<true>, grid, block, 0, st, cfg, b, obs_out);
     } else {
-        if (lat) hipLaunchKernelGGL(cp_reset_kernel<true>, grid, block, 0, st, cfg, b, obs_out);
+        if (wide) hipLaunchKernelGGL((cp_reset_kernel<true, false, false, true>), grid, block, 0, st, cfg, b, obs_out);
+        else if (lat) hipLaunchKernelGGL(cp_reset_kernel<true>, grid, block, 0, st, cfg, b, obs_out);
         else hipLaunchKernelGGL(cp_reset_kernel<false>, grid, block, 0, st, cfg, b, obs_out);
     }
 }
 
 template <int K, bool Q>
-static void launch_step_t(bool lat, const cp_config& cfg, const Bufs& b, const void* actions, float* obs_out,
+static void launch_step_t(int shape, const cp_config& cfg, const Bufs& b, const void* actions, float* obs_out,
                           float* reward_out, uint8_t* done_out, float* term_out, float* readback, int rb_bug,
                           const Lqr& lq, hipStream_t st) {
-    const dim3 grid(env_grid(2 * cfg.num_envs, WAVE)), block(WAVE);  // two lanes per env
+    const bool lat = shape != 0;
+    const bool wide = shape == 2 && !kF64 && !(cfg.phys.model_flags & (CP_MODEL_PERSISTENT | CP_MODEL_SLEEPING));
+    const dim3 grid(env_grid((wide ? 16 : 2) * cfg.num_envs, WAVE)), block(WAVE);  // lanes per env
     if (cfg.phys.model_flags & CP_MODEL_PERSISTENT) {  // the persistent-manifold model: latency shape only
         hipLaunchKernelGGL((cp_step_kernel<K, Q, true, true>), grid, block, 0, st, cfg, b, actions, obs_out,
                            reward_out, done_out, term_out, readback, rb_bug, lq);
@@ -924,7 +942,10 @@ static void launch_step_t(bool lat, const cp_config& cfg, const Bufs& b, const v
         hipLaunchKernelGGL((cp_step_kernel<K, Q, true>), grid, block, 0, st, cfg, b, actions, obs_out, reward_out,
                            done_out, term_out, readback, rb_bug, lq);
     } else {
-        if (lat)
+        if (wide)
+            hipLaunchKernelGGL((cp_step_kernel<K, Q, true, false, false, true>), grid, block, 0, st, cfg, b, actions,
+                               obs_out, reward_out, done_out, term_out, readback, rb_bug, lq);
+        else if (lat)
             hipLaunchKernelGGL((cp_step_kernel<K, Q, true>), grid, block, 0, st, cfg, b, actions, obs_out, reward_out,
                                done_out, term_out, readback, rb_bug, lq);
         else
@@ -973,7 +994,7 @@ void launch_rollout(bool lat, int kind, const cp_config& cfg, const Bufs& b, int
     }
 }
 
-void launch_step(bool lat, int kind, const cp_config& cfg, const Bufs& b, const void* actions, float* obs_out,
+void launch_step(int lat, int kind, const cp_config& cfg, const Bufs& b, const void* actions, float* obs_out,
                  float* reward_out, uint8_t* done_out, float* term_out, float* readback, int rb_bug, const Lqr& lq,
                  hipStream_t st) {
     const bool q = lq.gains != nullptr;

@@ -172,8 +172,8 @@ struct cp_handle {
     float* nobs;
     int npar;
     int ninflight;
-    int reset_lat;     // 1: latency-shaped autoreset kernel (episodes end at different steps)
-    int step_lat;      // 1: latency-shaped step kernel (every wave gets a SIMD of its own)
+    int reset_lat;     // CP_SHAPE_* of the autoreset kernel: 1 latency (episodes end at different steps), 2 its WIDE layout
+    int step_lat;      // CP_SHAPE_* of the step kernel: 1 latency (every wave gets a SIMD of its own), 2 WIDE
     int reset_req;     // cp_set_kernel_shape request (CP_SHAPE_AUTO: choose_reset_shape decides)
     int step_req;
     // SAME_STEP autoreset without early termination: the number of cp_step calls since every env's
@@ -188,6 +188,10 @@ struct cp_handle {
 };
 
 static void choose_reset_shape(cp_handle* h);
+// CP_SHAPE_AUTO picks the WIDE layout for the latency-shaped kernels of batches up to kWideMax envs (C2's
+// 4,096 envs on 16 lanes each = one wave per SIMD) and for the reset lists of desynchronised episodes
+// (bounds / LQR termination: tens to hundreds of envs per list), measured in profiles/rd7d_wide
+static constexpr int kWideMax = 4096;
 
 static void timing_free(cp_timing& t) {
     for (hipEvent_t e : t.ev) (void)hipEventDestroy(e);
@@ -546,8 +550,13 @@ static void choose_reset_shape(cp_handle* h) {
     h->reset_lat = (e && (e[0] == '0' || e[0] == '1')) ? e[0] == '1' : (h->cfg.done_on_bounds || lqr_done || small);
     const char* es = std::getenv("CP_STEP_LATENCY");
     h->step_lat = (es && (es[0] == '0' || es[0] == '1')) ? es[0] == '1' : small;
-    if (h->reset_req != CP_SHAPE_AUTO) h->reset_lat = h->reset_req == CP_SHAPE_LATENCY;
-    if (h->step_req != CP_SHAPE_AUTO) h->step_lat = h->step_req == CP_SHAPE_LATENCY;
+    // the WIDE layout (16 lanes per env) where its extra waves still leave SIMDs idle
+    const bool wide_ok = !h->f64 && !(h->cfg.phys.model_flags & (CP_MODEL_PERSISTENT | CP_MODEL_SLEEPING));
+    if (wide_ok && h->step_lat && h->cfg.num_envs <= kWideMax) h->step_lat = CP_SHAPE_WIDE;
+    if (wide_ok && h->reset_lat && (h->cfg.num_envs <= kWideMax || h->cfg.done_on_bounds || lqr_done))
+        h->reset_lat = CP_SHAPE_WIDE;
+    if (h->reset_req != CP_SHAPE_AUTO) h->reset_lat = h->reset_req;
+    if (h->step_req != CP_SHAPE_AUTO) h->step_lat = h->step_req;
     if (h->f64) h->reset_lat = h->step_lat = 1;  // fp64: the 512-register shape only
     if (h->cfg.phys.model_flags & (CP_MODEL_PERSISTENT | CP_MODEL_SLEEPING))
         h->reset_lat = h->step_lat = 1;  // PM, SLEEPING: latency shape only
@@ -557,7 +566,7 @@ static int launch_reset_list(cp_handle* h, const cpc::Bufs& b, float* obs_out, h
     hipEvent_t* ev = timing_slot(h, 1);
     if (ev) CP_TRY(h, hipEventRecord(ev[0], st));
     if (h->f64) cp64::launch_reset(true, h->cfg, b, obs_out, st);
-    else cp::launch_reset(h->reset_lat != 0, h->cfg, b, obs_out, st);
+    else cp::launch_reset(h->reset_lat, h->cfg, b, obs_out, st);
     if (check(h, hipGetLastError(), "cp_reset_kernel")) return -1;
     if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
     return 0;
@@ -621,7 +630,7 @@ static int step_next_step(cp_handle* h, const void* actions, int action_kind, fl
         cp64::launch_step(true, action_kind, h->cfg, b, actions, obs_out, reward_out, done_out, terminal_obs_out,
                           h->readback, h->readback_bug, h->lqr, st);
     else
-        cp::launch_step(h->step_lat != 0, action_kind, h->cfg, b, actions, obs_out, reward_out, done_out,
+        cp::launch_step(h->step_lat, action_kind, h->cfg, b, actions, obs_out, reward_out, done_out,
                         terminal_obs_out, h->readback, h->readback_bug, h->lqr, st);
     CP_TRY(h, hipGetLastError());
     if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
@@ -691,7 +700,7 @@ int cp_step(cp_handle* h, const void* actions, int action_kind, float* obs_out, 
         cp64::launch_step(true, action_kind, h->cfg, h->b, actions, obs_out, reward_out, done_out, terminal_obs_out,
                           h->readback, h->readback_bug, h->lqr, st);
     else
-        cp::launch_step(h->step_lat != 0, action_kind, h->cfg, h->b, actions, obs_out, reward_out, done_out,
+        cp::launch_step(h->step_lat, action_kind, h->cfg, h->b, actions, obs_out, reward_out, done_out,
                         terminal_obs_out, h->readback, h->readback_bug, h->lqr, st);
     CP_TRY(h, hipGetLastError());
     if (ev) CP_TRY(h, hipEventRecord(ev[1], st));
@@ -795,11 +804,15 @@ int64_t cp_state_bytes(const cp_handle* h) {
 
 int cp_set_kernel_shape(cp_handle* h, int step_shape, int reset_shape) {
     if (!h) return fail(h, "cp_set_kernel_shape: null handle");
-    auto ok = [](int v) { return v == CP_SHAPE_AUTO || v == CP_SHAPE_THROUGHPUT || v == CP_SHAPE_LATENCY; };
+    auto ok = [](int v) {
+        return v == CP_SHAPE_AUTO || v == CP_SHAPE_THROUGHPUT || v == CP_SHAPE_LATENCY || v == CP_SHAPE_WIDE;
+    };
     if (!ok(step_shape) || !ok(reset_shape))
-        return fail(h, "cp_set_kernel_shape: shapes must be CP_SHAPE_AUTO, CP_SHAPE_THROUGHPUT or CP_SHAPE_LATENCY");
+        return fail(h, "cp_set_kernel_shape: shapes must be CP_SHAPE_AUTO, CP_SHAPE_THROUGHPUT, CP_SHAPE_LATENCY or "
+                       "CP_SHAPE_WIDE");
+    auto fixed = [](int v) { return v == CP_SHAPE_THROUGHPUT || v == CP_SHAPE_WIDE; };
     if ((h->f64 || (h->cfg.phys.model_flags & (CP_MODEL_PERSISTENT | CP_MODEL_SLEEPING))) &&
-        (step_shape == CP_SHAPE_THROUGHPUT || reset_shape == CP_SHAPE_THROUGHPUT))
+        (fixed(step_shape) || fixed(reset_shape)))
         return fail(h, "cp_set_kernel_shape: fp64, persistent-manifold and sleeping-model handles have the latency "
                        "shape only");
     h->step_req = step_shape;
@@ -810,8 +823,8 @@ int cp_set_kernel_shape(cp_handle* h, int step_shape, int reset_shape) {
 
 int cp_get_kernel_shape(const cp_handle* h, int* step_shape, int* reset_shape) {
     if (!h) return fail(nullptr, "cp_get_kernel_shape: null handle");
-    if (step_shape) *step_shape = h->step_lat ? CP_SHAPE_LATENCY : CP_SHAPE_THROUGHPUT;
-    if (reset_shape) *reset_shape = h->reset_lat ? CP_SHAPE_LATENCY : CP_SHAPE_THROUGHPUT;
+    if (step_shape) *step_shape = h->step_lat;
+    if (reset_shape) *reset_shape = h->reset_lat;
     return 0;
 }
 

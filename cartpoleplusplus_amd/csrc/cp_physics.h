@@ -528,12 +528,14 @@ __host__ __device__ constexpr int local_of(int p) {
 // Per-lane constants of the lane's island (lane-varying copies of cp_physics fields).
 struct Lane {
     int isl;
+    int pj;             // WIDE kernels: the local pair whose narrowphase this lane computes (>= 5: none)
     real im1, im2;      // inverse masses of the island's cart, pole
     real ii1[3], ii2[3];  // their body-frame inverse inertias
     real mu0, mu1, mu2; // friction products of local pairs 0..2
     CP_DEV static Lane make(int isl, const cp_physics& P) {
         Lane L;
         L.isl = isl;
+        L.pj = 0;
         L.im1 = isl ? P.inv_mass[3] : P.inv_mass[1];
         L.im2 = isl ? P.inv_mass[4] : P.inv_mass[2];
         for (int k = 0; k < 3; ++k) {
@@ -2055,7 +2057,173 @@ CP_DEV void pm_refresh(PMan& M, const Box& A, const Box& B, real thr) {
 // row setup of the lane's island, unconstrained velocity update of the whole env,
 // the island view and the warm start.  A lane with live == false (done env, padding)
 // makes no contacts and writes nothing.
-template <bool ALLIN = false, bool PM = false, bool SLP = false, bool ES = false>
+// ---- WIDE kernels (the latency-shaped step / reset kernels of small batches): an env
+// runs on 16 lanes, 8 lane pairs, and every lane pair is a replica of the env (lane 2k + p holds island p, the
+// same values on every pair k), so every DPP exchange between the two lanes of a pair and every wave-uniform
+// decision stays what it is in the two-lane layout.  The replicas share one LDS pool column per island.  Only
+// the narrowphase is divided: lane pair j (< 5) computes local pair j of both islands, so the 5 pairs of an
+// island are found side by side instead of one after another; every replica then gathers the 5 pairs'
+// point counts and normals (ds_bpermute), derives the same slots and caps the pair loop of the two-lane layout
+// derives, and the pair's lane writes its rows into the island's pool column and its warm-start id word.
+// A per-body field of a kernel argument (cp_physics) for a lane-varying body id: all five values through an
+// empty asm, then selects (an indexed load would copy the argument struct into scratch memory).
+CP_DEV real body_f(int id, const float v[CP_NUM_BODIES]) {
+    real x0 = v[0], x1 = v[1], x2 = v[2], x3 = v[3], x4 = v[4];
+    asm volatile("" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(x4));
+    return id == 0 ? x0 : (id == 1 ? x1 : (id == 2 ? x2 : (id == 3 ? x3 : x4)));
+}
+CP_DEV real body_f3(int id, const float v[CP_NUM_BODIES][3], int k) {
+    real x0 = v[0][k], x1 = v[1][k], x2 = v[2][k], x3 = v[3][k], x4 = v[4][k];
+    asm volatile("" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(x4));
+    return id == 0 ? x0 : (id == 1 ? x1 : (id == 2 ? x2 : (id == 3 ? x3 : x4)));
+}
+// the narrowphase + row setup of the substep on the WIDE layout: the same contacts, rows, slots, caps,
+// warm-start reads and writes as substep_prep's pair loop over the lane's 5 pairs (bit for bit)
+template <bool ALLIN, bool ES>
+CP_DEV void narrow_wide(Own& O, const cp_physics& P, const Lane& L, real* pool, int& overflow, const Mem& G,
+                        Stamps& ST, bool live, Step& T, int& used, int& fused) {
+    const real inv_dt = P.inv_dt;
+    const int j = L.pj;
+    const bool mine = j < CP_ISLAND_PAIRS;
+    const bool second = L.isl != 0;
+    const int g = island_pair(L.isl, mine ? j : 0);
+    const int a = pair_a(g), bi = pair_b(g);
+    const bool plive = live && mine;
+    // the partner island's bodies: the partner lane is the same pair's lane of the other island (a replica)
+    const V3 Pcx = partner(O.c.x), Ppx = partner(O.p.x);
+    real Pcq[4], Ppq[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { Pcq[k] = partner(O.c.q[k]); Ppq[k] = partner(O.p.q[k]); }
+    // A: the ground (pairs 0, 1), the own cart (pair 2; island 0's cross pairs), the partner's pole (island 1's
+    // cross pairs).  B: the own cart (pair 0; island 1's pair 3), the own pole (pairs 1, 2; island 1's pair 4),
+    // the partner's cart / pole (island 0's pairs 3 / 4) -- substep_prep's pair_body per pair
+    const bool a_ground = j < 2, a_ppole = j >= 3 && second;
+    const bool b_partner = j >= 3 && !second, b_pole = j == 1 || j == 2 || j == 4;
+    Box A, Bx;
+    real bq[4];
+    {
+        const V3 zero = mk(real(0.0), real(0.0), real(0.0));
+        A.c = a_ground ? zero : selv(a_ppole, Ppx, O.c.x);
+        real aq[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) aq[k] = a_ground ? (k == 3 ? real(1.0) : real(0.0)) : (a_ppole ? Ppq[k] : O.c.q[k]);
+        A.ax = quat_axes(aq[0], aq[1], aq[2], aq[3]);
+        A.h0 = body_f3(a, P.half_extents, 0);
+        A.h1 = body_f3(a, P.half_extents, 1);
+        A.h2 = body_f3(a, P.half_extents, 2);
+        Bx.c = b_partner ? selv(b_pole, Ppx, Pcx) : selv(b_pole, O.p.x, O.c.x);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) bq[k] = b_partner ? (b_pole ? Ppq[k] : Pcq[k]) : (b_pole ? O.p.q[k] : O.c.q[k]);
+        Bx.ax = quat_axes(real(0.0), real(0.0), real(0.0), real(1.0));  // placeholder: B's axes after the broadphase
+        Bx.h0 = body_f3(bi, P.half_extents, 0);
+        Bx.h1 = body_f3(bi, P.half_extents, 1);
+        Bx.h2 = body_f3(bi, P.half_extents, 2);
+    }
+    Contact C;
+    C.m = 0;
+    C.n = mk(real(0.0), real(0.0), real(1.0));
+    const real newmargin = real(P.contact_margin);
+    const bool near = plive && !face_separated(A, Bx, newmargin);
+    if (near) Bx.ax = quat_axes(bq[0], bq[1], bq[2], bq[3]);
+    uint32_t oid = 0xFFFFFFFFu;
+    real ol0 = real(0.0), ol1 = real(0.0), ol2 = real(0.0), ol3 = real(0.0);
+    const int jc = mine ? j : 0;
+    if (near) {  // the pair's warm-start cache (lane-varying field: into the lane's buffer offset)
+        oid = to_bits(G.st.ld(CP_SF_WS_ID(0, 0), G.woff + (uint32_t)jc * G.st.fstride));
+        const uint32_t lo = G.loff + (uint32_t)(4 * jc) * G.st.fstride;
+        ol0 = G.st.ld(CP_SF_WS_LAM(0, 0, 0), lo); ol1 = G.st.ld(CP_SF_WS_LAM(0, 0, 1), lo);
+        ol2 = G.st.ld(CP_SF_WS_LAM(0, 0, 2), lo); ol3 = G.st.ld(CP_SF_WS_LAM(0, 0, 3), lo);
+    }
+    if (near) box_box<ALLIN, ES>(A, Bx, newmargin, P.edge_bias, C, ST);
+    const real mu = body_f(a, P.friction) * body_f(bi, P.friction);
+    // every replica gathers the island's 5 pairs: point count | friction bit, normal
+    const int grp = (int)(threadIdx.x & ~15u) + L.isl;
+    const uint32_t word = (uint32_t)C.m | (mu > real(0.0) ? 8u : 0u);
+    uint32_t cw[CP_ISLAND_PAIRS];
+    V3 cn[CP_ISLAND_PAIRS];
+#pragma unroll
+    for (int k = 0; k < CP_ISLAND_PAIRS; ++k) {
+        cw[k] = (uint32_t)__shfl((int)word, grp + 2 * k, WAVE);
+        cn[k] = mk(__shfl(C.n.x, grp + 2 * k, WAVE), __shfl(C.n.y, grp + 2 * k, WAVE), __shfl(C.n.z, grp + 2 * k, WAVE));
+    }
+    // slots and caps in pair order (substep_prep: a point past MAXP rows, or a frictional point past MAXF, is
+    // dropped and counted)
+    int base = 0, fbase = 0, ov = 0, myb = 0, myfb = 0, mym = 0, myfm = 0;
+    int mk_[CP_ISLAND_PAIRS], bk_[CP_ISLAND_PAIRS], fmk_[CP_ISLAND_PAIRS], fbk_[CP_ISLAND_PAIRS];
+#pragma unroll
+    for (int k = 0; k < CP_ISLAND_PAIRS; ++k) {
+        const int n = (int)(cw[k] & 7u);
+        const bool fr = (cw[k] & 8u) != 0u;
+        const int m = n < MAXP - base ? n : MAXP - base;
+        const int fm = fr ? (m < MAXF - fbase ? m : MAXF - fbase) : 0;
+        ov += (n - m) + (fr ? m - fm : 0);
+        mk_[k] = m; bk_[k] = base; fmk_[k] = fm; fbk_[k] = fbase;
+        if (k == j) { myb = base; myfb = fbase; mym = m; myfm = fm; }
+        base += m;
+        fbase += fm;
+    }
+    overflow += ov;
+    used = base;
+    fused = fbase;
+    // the own pair's rows into the island's pool column
+    uint32_t nid = 0xFFFFFFFFu;
+    if (__ballot(mym > 0) != 0ull) {
+        const real ima = body_f(a, P.inv_mass), imb = body_f(bi, P.inv_mass);
+        const Sym Ma = world_inv_inertia(A.ax, body_f3(a, P.inv_inertia, 0), body_f3(a, P.inv_inertia, 1),
+                                         body_f3(a, P.inv_inertia, 2));
+        const Sym Mb = world_inv_inertia(Bx.ax, body_f3(bi, P.inv_inertia, 0), body_f3(bi, P.inv_inertia, 1),
+                                         body_f3(bi, P.inv_inertia, 2));
+        const V3 xa = A.c, xb = Bx.c;
+        V3 t1 = mk(real(0.0), real(0.0), real(0.0)), t2 = t1;
+        if (mu > real(0.0)) plane_space(C.n, t1, t2);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k < mym) {
+                const int s = myb + k;
+                const V3 rb = sub(C.p[k], xb);
+                const real K = row_k_dyn(a, ima, imb, xa, xb, Ma, Mb, rb, C.n);
+                const real dist = C.d[k];
+                const real tg = dist > real(0.0) ? -(dist * inv_dt) : -((P.erp * dist) * inv_dt);
+                const int id = (int)((C.ids >> (8 * k)) & 0xFFu);
+                real l0 = real(0.0);
+                if ((int)(oid & 0xFFu) == id) l0 = ol0;
+                else if ((int)((oid >> 8) & 0xFFu) == id) l0 = ol1;
+                else if ((int)((oid >> 16) & 0xFFu) == id) l0 = ol2;
+                else if ((int)((oid >> 24) & 0xFFu) == id) l0 = ol3;
+                pool_n(pool, F_RBX, s) = rb.x;
+                pool_n(pool, F_RBY, s) = rb.y;
+                pool_n(pool, F_RBZ, s) = rb.z;
+                pool_n(pool, F_IE, s) = real(1.0) / K;
+                pool_n(pool, F_TG, s) = tg;
+                pool_n(pool, F_LAM, s) = P.warmstart * l0;
+                nid = (nid & ~(0xFFu << (8 * k))) | ((uint32_t)id << (8 * k));
+                if (k < myfm) {
+                    const int fs = myfb + k;
+                    pool_f(pool, FF_IE1, fs) = real(1.0) / row_k_dyn(a, ima, imb, xa, xb, Ma, Mb, rb, t1);
+                    pool_f(pool, FF_IE2, fs) = real(1.0) / row_k_dyn(a, ima, imb, xa, xb, Ma, Mb, rb, t2);
+                    pool_f(pool, FF_L1, fs) = real(0.0);
+                    pool_f(pool, FF_L2, fs) = real(0.0);
+                }
+            }
+        }
+    }
+    // the own pair's warm-start id word (the pair's lane reads it, and rewrites it, every substep)
+    const int om = (int)((O.wsm >> (3 * jc)) & 7u);
+    const bool idw = near ? nid != oid : om > 0;
+    if (plive && idw) G.st.st(CP_SF_WS_ID(0, 0), G.woff + (uint32_t)jc * G.st.fstride, bits_to<real>(nid));
+    // every replica: the island's manifold headers and the warm-start point counts
+#pragma unroll
+    for (int k = 0; k < CP_ISLAND_PAIRS; ++k) {
+        const uint32_t omk = (O.wsm >> (3 * k)) & 7u;
+        const uint32_t m = (uint32_t)mk_[k];
+        T.n[k] = cn[k];
+        T.pk[k] = m | ((uint32_t)bk_[k] << 3) | ((uint32_t)fmk_[k] << 8) | ((uint32_t)fbk_[k] << 11) |
+                  ((live ? (m > omk ? m : omk) : 0u) << 16);
+        if (live) O.wsm = (O.wsm & ~(7u << (3 * k))) | (m << (3 * k));
+    }
+}
+
+template <bool ALLIN = false, bool PM = false, bool SLP = false, bool ES = false, bool WIDE = false>
 CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, real* pool, real* pool0, int& overflow,
                          const Mem& G, Stamps& ST, bool live, Ctx& c) {
     const real dt = P.dt, inv_dt = P.inv_dt;
@@ -2064,6 +2232,10 @@ CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, rea
     // 2. narrowphase + row setup of the lane's island: wave-uniform loop over its 5
     //    local pairs (the global pair, hence the bodies, differ between the two lanes)
     int used = 0, fused = 0;
+    static_assert(!(WIDE && (PM || SLP)), "the WIDE layout is built for the default contact model");
+    if constexpr (WIDE) {
+        narrow_wide<ALLIN, ES>(O, P, L, pool, overflow, G, ST, live, T, used, fused);
+    } else {
     // one local pair; GROUND: j is 0 or 1, whose first body is the static ground on both
     // islands, so its box is compile-time (centre 0, identity axes)
     auto pair_body = [&](auto ground_tag, const int j) {
@@ -2281,6 +2453,7 @@ CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, rea
     for (int j = 0; j < 2; ++j) pair_body(std::true_type{}, j);
 #pragma unroll 1
     for (int j = 2; j < CP_ISLAND_PAIRS; ++j) pair_body(std::false_type{}, j);
+    }
     CP_STAMP(t1);
     CP_ACC(narrow, t0, t1);
     // 3. unconstrained velocity update of the lane's own bodies (island 0's lane: cart, pole)
@@ -2364,7 +2537,7 @@ CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, rea
 // Phase 3: whole-env velocities from the two lanes' islands (both lanes of every
 // env active), the warm-start cache refresh and the integration (DESIGN.md
 // §Physics model 5b-7).
-template <bool PM = false, bool SLP = false>
+template <bool PM = false, bool SLP = false, bool WIDE = false>
 CP_DEV void substep_finish(Own& O, const cp_physics& P, const Lane& L, const Ctx& c, real* pool, const Mem& G,
                            Stamps& ST, bool live) {
     const real dt = P.dt, inv_dt = P.inv_dt;
@@ -2383,7 +2556,8 @@ CP_DEV void substep_finish(Own& O, const cp_physics& P, const Lane& L, const Ctx
 #pragma unroll
         for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
             const int cnt = pk_cnt(c.T.pk[j]), base = pk_base(c.T.pk[j]);
-            if (pk_wcnt(c.T.pk[j]) > 0) {  // one branch per pair: rewriting a zero slot with 0 is harmless
+            // (WIDE: the pair's own lane, which reads the entry in the next substep's narrowphase)
+            if (pk_wcnt(c.T.pk[j]) > 0 && (!WIDE || L.pj == j)) {  // one branch per pair: rewriting a zero slot with 0 is harmless
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
                     G.sl(CP_SF_WS_LAM(0, j, k), (k < cnt) ? pool_n(pool, F_LAM, base + k) : real(0.0));
@@ -2459,19 +2633,19 @@ CP_DEV void substep_finish(Own& O, const cp_physics& P, const Lane& L, const Ctx
 // (sweeps_c44) and the all-inside face-contact exit (face_contact<ALLIN>).
 // PM: CP_MODEL_PERSISTENT (Bullet's persistent manifold, per-row normals in the pool).
 // SLP: CP_MODEL_SLEEPING (Bullet's deactivation: sleeping islands are neither integrated nor solved).
-template <bool FAST = false, bool C44 = false, bool ALLIN = C44, bool PM = false, bool SLP = false>
+template <bool FAST = false, bool C44 = false, bool ALLIN = C44, bool PM = false, bool SLP = false, bool WIDE = false>
 CP_DEV void substep(Own& O, const cp_physics& P, const Lane& L, real* pool, real* pool0, int& overflow,
                     const Mem& G, Stamps& ST, bool live = true) {
     Ctx c;
     Sim X;  // scratch: the whole-env view of a merged env's cross rows (cross_view)
     c.slp = 0u;
     if constexpr (SLP) c.slp = sleep_islands(O, P, L.isl != 0);
-    substep_prep<ALLIN, PM, SLP, !FAST>(O, X, P, L, pool, pool0, overflow, G, ST, live, c);
+    substep_prep<ALLIN, PM, SLP, !FAST, WIDE>(O, X, P, L, pool, pool0, overflow, G, ST, live, c);
     CP_STAMP(t2);
     solve_range<FAST, C44, PM>(c, X, P, pool, pool0, L.isl != 0, 0, P.solver_iterations, ST);
     CP_STAMP(t3);
     CP_ACC(solve, t2, t3);
-    substep_finish<PM, SLP>(O, P, L, c, pool, G, ST, live);
+    substep_finish<PM, SLP, WIDE>(O, P, L, c, pool, G, ST, live);
 }
 
 // LINK_FRAME force at the COM on the lane's own cart (cart on island 0's lane, cart2 on island 1's):

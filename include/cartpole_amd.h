@@ -311,12 +311,16 @@ int64_t cp_state_bytes(const cp_handle* h);   /* CP_STATE_FIELDS * B * sizeof(re
 /* Kernel shapes.  The step and autoreset kernels each come in two register budgets:
  * THROUGHPUT (2 waves per SIMD; bursts and batches above 32,768 envs) and LATENCY (1 wave
  * per SIMD with 512 registers and fast-form solver rows; short reset lists and small
- * batches).  Both compute the same numbers (the GPU parity suite runs every case on both).
- * cp_create picks them (CP_SHAPE_AUTO: DESIGN.md §5); this call overrides either
- * (fp64 handles have only the latency shape and reject THROUGHPUT). */
+ * batches), and the latency budget in a third layout, WIDE (16 lanes per env instead of 2:
+ * the env's 10 contact pairs found side by side, for batches and reset lists that leave
+ * most SIMDs idle; fp32 default-model handles).  All compute the same numbers (the GPU
+ * parity suite runs every case on every shape).  cp_create picks them (CP_SHAPE_AUTO:
+ * DESIGN.md §5); this call overrides either (fp64 handles have only the latency shape and
+ * reject THROUGHPUT and WIDE; persistent-manifold and sleeping-model handles likewise). */
 #define CP_SHAPE_AUTO       (-1)
 #define CP_SHAPE_THROUGHPUT 0
 #define CP_SHAPE_LATENCY    1
+#define CP_SHAPE_WIDE       2
 int cp_set_kernel_shape(cp_handle* h, int step_shape, int reset_shape);
 int cp_get_kernel_shape(const cp_handle* h, int* step_shape, int* reset_shape);   /* the shapes in use */
 

@@ -85,7 +85,8 @@ def test_next_step_bounds_bitexact(oracle_mod, shape):
     _assert_same(_np(gl_), orl, "episode lengths")
 
 
-@pytest.mark.parametrize("shape", [("throughput", "throughput"), ("latency", "latency")], ids=["tp-tp", "lat-lat"])
+@pytest.mark.parametrize("shape", [("throughput", "throughput"), ("latency", "latency"), ("wide", "wide")],
+                         ids=["tp-tp", "lat-lat", "wide-wide"])
 def test_next_step_burst_every_env_at_once(oracle_mod, shape):
     """Fixed-length episodes: every env ends in the same call, so the next call's step kernel skips
     every env and the fixup hands out B resets."""
@@ -117,7 +118,8 @@ def test_next_step_refusals():
     env.close()   # a reset may be in flight: cp_destroy waits for it
 
 
-@pytest.mark.parametrize("shape", [("throughput", "throughput"), ("latency", "latency")], ids=["tp-tp", "lat-lat"])
+@pytest.mark.parametrize("shape", [("throughput", "throughput"), ("latency", "latency"), ("wide", "wide")],
+                         ids=["tp-tp", "lat-lat", "wide-wide"])
 def test_next_step_lqr_done_thresholds(oracle_mod, shape):
     """The in-kernel LQR policy with the agent's done thresholds (per-env gains) under NEXT_STEP: the
     8-states of the reset-only calls are left as they were, on both sides."""

@@ -5,7 +5,7 @@ The kernel and the fp32 oracle perform the same fp32 operations in the same orde
 bit-exact equality (raw bits: a signed-zero difference fails) of obs / reward / done /
 full state.  Every case runs on both register budgets of the step and autoreset kernels
 (SHAPES: cp_set_kernel_shape), so the throughput shape that bench.py times at 65,536 envs
-is under the same bar as the latency shape small batches pick by default.  Full-size
+is under the same bar as the latency shape and its WIDE layout, which small batches pick by default.  Full-size
 (B = 65,536) runs are checked on a random subset of envs plus size-independent properties.
 """
 import argparse
@@ -21,10 +21,11 @@ from cartpoleplusplus_amd.batched import BatchedCartpole
 pytestmark = pytest.mark.gpu
 
 
-# (step kernel shape, autoreset kernel shape): every combination the library can run
+# (step kernel shape, autoreset kernel shape): the combinations of the two register budgets, and the WIDE
+# layout of the latency budget (16 lanes per env, round 6) as step kernel, reset kernel and both
 SHAPES = [("throughput", "throughput"), ("latency", "latency"), ("throughput", "latency"),
-          ("latency", "throughput")]
-SHAPE_IDS = ["tp-tp", "lat-lat", "tp-lat", "lat-tp"]
+          ("latency", "throughput"), ("wide", "wide"), ("throughput", "wide"), ("wide", "latency")]
+SHAPE_IDS = ["tp-tp", "lat-lat", "tp-lat", "lat-tp", "wide-wide", "tp-wide", "wide-lat"]
 shapes = pytest.mark.parametrize("shape", SHAPES, ids=SHAPE_IDS)
 
 

@@ -102,6 +102,9 @@ def test_persistent_rejects_throughput_shape():
     env = BatchedCartpole(8, 0, config=cfg)
     with pytest.raises(native.CartpoleError):
         env.set_kernel_shape("throughput", "throughput")
+    with pytest.raises(native.CartpoleError):      # the WIDE layout is built for the default model only
+        env.set_kernel_shape("wide", "latency")
+    assert env.kernel_shape() == ("latency", "latency")
 
 
 def test_persistent_set_state_mid_episode_clears_manifolds(oracle_mod):

@@ -43,6 +43,7 @@ def _same(a, b, what):
 VARIANTS = {
     "tp": dict(shape=("throughput", "throughput"), kw={}),
     "lat": dict(shape=("latency", "latency"), kw={}),
+    "wide": dict(shape=("wide", "wide"), kw={}),
     "f64": dict(shape=None, kw=dict(precision="f64")),
     "sleeping": dict(shape=None, kw=dict(model_flags=abi.CP_MODEL_SLEEPING)),
     "raster": dict(shape=None, kw={}, raster=True),

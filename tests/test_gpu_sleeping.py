@@ -147,4 +147,6 @@ def test_sleeping_rejects_lqr_and_persistent():
         env.enable_lqr(torch.zeros((2, 2, 8)))
     with pytest.raises(native.CartpoleError):
         env.set_kernel_shape("throughput", "throughput")
+    with pytest.raises(native.CartpoleError):
+        env.set_kernel_shape("latency", "wide")
     env.close()
