@@ -855,9 +855,9 @@ def main():
     ap.add_argument("--streams", type=int, default=1, metavar="S",
                     help="run the GPU's batch as S shard handles on S HIP streams (the C4 shard rule inside one "
                          "GPU; each env computes what it computes in one handle)")
-    ap.add_argument("--shape", choices=("auto", "throughput", "latency", "wide"), default="auto",
+    ap.add_argument("--shape", choices=("auto", "throughput", "latency", "wide", "wide8"), default="auto",
                     help="kernel shapes (cp_set_kernel_shape) of the step and autoreset kernels")
-    ap.add_argument("--reset-shape", choices=("auto", "throughput", "latency", "wide"), default=None,
+    ap.add_argument("--reset-shape", choices=("auto", "throughput", "latency", "wide", "wide8"), default=None,
                     help="the autoreset kernel's shape when it differs from --shape")
     ap.add_argument("--sleeping", action="store_true",
                     help="the CP_MODEL_SLEEPING model (Bullet's deactivation: resting islands sleep after 2 s; "

@@ -334,14 +334,14 @@ __global__ void __launch_bounds__(256) cp_init_kernel(cp_config cfg, Bufs b) {
 // (fixed-length episodes end together).  LAT = true: one wave per SIMD with 512 registers and
 // fast-form rows, for the short lists of desynchronised episodes (bounds termination), where
 // the 130 serial substeps of one wave are the whole latency of the step.
-// WIDE (latency shape only): 16 lanes per env, 8 replicas of the env's lane pair that divide the narrowphase
-// (narrow_wide, cp_physics.h); lane 0 of the 16 is the lead, lanes 0-1 store the state.
-template <bool LAT, bool PM = false, bool SLP = false, bool WIDE = false>
+// WIDE (latency shape only): 16 (or 8) lanes per env, 8 (4) replicas of the env's lane pair that divide the
+// narrowphase (narrow_wide, cp_physics.h); lane 0 of the env's lanes is the lead, lanes 0-1 store the state.
+template <bool LAT, bool PM = false, bool SLP = false, int WIDE = 0>
 __global__ void __launch_bounds__(WAVE)
 __attribute__((amdgpu_waves_per_eu(LAT ? 1 : CP_WAVES_PER_EU, LAT ? 1 : CP_WAVES_PER_EU)))
 cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     static_assert(!WIDE || (LAT && !PM && !SLP), "WIDE: latency shape, default contact model");
-    constexpr int LW = WIDE ? 16 : 2;  // lanes per env
+    constexpr int LW = WIDE ? WIDE : 2;  // lanes per env
     __shared__ real lds_pool[(PM ? POOL_FLOATS_PM : POOL_FLOATS) * WAVE];
     const int B = cfg.num_envs;
     const int t = blockIdx.x * WAVE + threadIdx.x;
@@ -428,13 +428,13 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
 // LAT: the latency shape of cp_reset_kernel<true> (1 wave per SIMD, 512 registers, fast-form
 // rows) for batches whose waves all get a SIMD of their own (<= 32,768 envs).  WIDE: the latency shape on
 // 16 lanes per env (cp_reset_kernel), for batches that leave most SIMDs idle.
-template <int KIND, bool LQR, bool LAT, bool PM = false, bool SLP = false, bool WIDE = false>
+template <int KIND, bool LQR, bool LAT, bool PM = false, bool SLP = false, int WIDE = 0>
 __global__ void __launch_bounds__(WAVE)
 __attribute__((amdgpu_waves_per_eu(LAT ? 1 : CP_WAVES_PER_EU, LAT ? 1 : CP_WAVES_PER_EU)))
 cp_step_kernel(cp_config cfg, Bufs b, const void* actions, float* obs_out, float* reward_out, uint8_t* done_out,
                float* term_out, float* readback, int rb_bug, Lqr lq) {
     static_assert(!WIDE || (LAT && !PM && !SLP), "WIDE: latency shape, default contact model");
-    constexpr int LW = WIDE ? 16 : 2;  // lanes per env
+    constexpr int LW = WIDE ? WIDE : 2;  // lanes per env
     __shared__ real lds_pool[(PM ? POOL_FLOATS_PM : POOL_FLOATS) * WAVE];
     const int B = cfg.num_envs;
     const int t = blockIdx.x * WAVE + threadIdx.x;
@@ -898,8 +898,9 @@ void launch_nextstep_resolve(const cp_config& cfg, const Bufs& b, const uint8_t*
 // shape: 0 throughput, 1 latency, 2 latency on the WIDE layout (cp_set_kernel_shape; fp32 default model only)
 void launch_reset(int shape, const cp_config& cfg, const Bufs& b, float* obs_out, hipStream_t st) {
     const bool lat = shape != 0;
-    const bool wide = shape == 2 && !kF64 && !(cfg.phys.model_flags & (CP_MODEL_PERSISTENT | CP_MODEL_SLEEPING));
-    const dim3 grid(env_grid((wide ? 16 : 2) * cfg.num_envs, WAVE)), block(WAVE);  // lanes per env
+    const int wide = (kF64 || (cfg.phys.model_flags & (CP_MODEL_PERSISTENT | CP_MODEL_SLEEPING))) ? 0
+                     : shape == CP_SHAPE_WIDE ? 16 : shape == CP_SHAPE_WIDE8 ? 8 : 0;
+    const dim3 grid(env_grid((wide ? wide : 2) * cfg.num_envs, WAVE)), block(WAVE);  // lanes per env
     if (cfg.phys.model_flags & CP_MODEL_PERSISTENT) {  // the persistent-manifold model: latency shape only
         hipLaunchKernelGGL((cp_reset_kernel<true, true>), grid, block, 0, st, cfg, b, obs_out);
         return;
@@ -912,7 +913,8 @@ void launch_reset(int shape, const cp_config& cfg, const Bufs& b, float* obs_out
         (void)lat;
         hipLaunchKernelGGL(cp_reset_kernel<true>, grid, block, 0, st, cfg, b, obs_out);
     } else {
-        if (wide) hipLaunchKernelGGL((cp_reset_kernel<true, false, false, true>), grid, block, 0, st, cfg, b, obs_out);
+        if (wide == 16) hipLaunchKernelGGL((cp_reset_kernel<true, false, false, 16>), grid, block, 0, st, cfg, b, obs_out);
+        else if (wide == 8) hipLaunchKernelGGL((cp_reset_kernel<true, false, false, 8>), grid, block, 0, st, cfg, b, obs_out);
         else if (lat) hipLaunchKernelGGL(cp_reset_kernel<true>, grid, block, 0, st, cfg, b, obs_out);
         else hipLaunchKernelGGL(cp_reset_kernel<false>, grid, block, 0, st, cfg, b, obs_out);
     }
@@ -923,8 +925,9 @@ static void launch_step_t(int shape, const cp_config& cfg, const Bufs& b, const 
                           float* reward_out, uint8_t* done_out, float* term_out, float* readback, int rb_bug,
                           const Lqr& lq, hipStream_t st) {
     const bool lat = shape != 0;
-    const bool wide = shape == 2 && !kF64 && !(cfg.phys.model_flags & (CP_MODEL_PERSISTENT | CP_MODEL_SLEEPING));
-    const dim3 grid(env_grid((wide ? 16 : 2) * cfg.num_envs, WAVE)), block(WAVE);  // lanes per env
+    const int wide = (kF64 || (cfg.phys.model_flags & (CP_MODEL_PERSISTENT | CP_MODEL_SLEEPING))) ? 0
+                     : shape == CP_SHAPE_WIDE ? 16 : shape == CP_SHAPE_WIDE8 ? 8 : 0;
+    const dim3 grid(env_grid((wide ? wide : 2) * cfg.num_envs, WAVE)), block(WAVE);  // lanes per env
     if (cfg.phys.model_flags & CP_MODEL_PERSISTENT) {  // the persistent-manifold model: latency shape only
         hipLaunchKernelGGL((cp_step_kernel<K, Q, true, true>), grid, block, 0, st, cfg, b, actions, obs_out,
                            reward_out, done_out, term_out, readback, rb_bug, lq);
@@ -942,8 +945,11 @@ static void launch_step_t(int shape, const cp_config& cfg, const Bufs& b, const 
         hipLaunchKernelGGL((cp_step_kernel<K, Q, true>), grid, block, 0, st, cfg, b, actions, obs_out, reward_out,
                            done_out, term_out, readback, rb_bug, lq);
     } else {
-        if (wide)
-            hipLaunchKernelGGL((cp_step_kernel<K, Q, true, false, false, true>), grid, block, 0, st, cfg, b, actions,
+        if (wide == 16)
+            hipLaunchKernelGGL((cp_step_kernel<K, Q, true, false, false, 16>), grid, block, 0, st, cfg, b, actions,
+                               obs_out, reward_out, done_out, term_out, readback, rb_bug, lq);
+        else if (wide == 8)
+            hipLaunchKernelGGL((cp_step_kernel<K, Q, true, false, false, 8>), grid, block, 0, st, cfg, b, actions,
                                obs_out, reward_out, done_out, term_out, readback, rb_bug, lq);
         else if (lat)
             hipLaunchKernelGGL((cp_step_kernel<K, Q, true>), grid, block, 0, st, cfg, b, actions, obs_out, reward_out,

@@ -188,10 +188,13 @@ struct cp_handle {
 };
 
 static void choose_reset_shape(cp_handle* h);
-// CP_SHAPE_AUTO picks the WIDE layout for the latency-shaped kernels of batches up to kWideMax envs (C2's
-// 4,096 envs on 16 lanes each = one wave per SIMD) and for the reset lists of desynchronised episodes
-// (bounds / LQR termination: tens to hundreds of envs per list), measured in profiles/rd7d_wide
-static constexpr int kWideMax = 4096;
+// CP_SHAPE_AUTO picks, for the latency-shaped kernels, the widest layout whose waves still fit the chip once
+// (1,024 SIMDs x 64 lanes): 16 lanes per env up to 4,096 envs (C2), 8 up to 8,192, else the two-lane layout;
+// and WIDE for the reset lists of desynchronised episodes (bounds / LQR termination: tens to hundreds of envs
+// per list).  Measured in profiles/rd7d_wide, profiles/rd7e_wide.
+static int wide_shape_for(int envs) {
+    return envs <= 4096 ? CP_SHAPE_WIDE : (envs <= 8192 ? CP_SHAPE_WIDE8 : CP_SHAPE_LATENCY);
+}
 
 static void timing_free(cp_timing& t) {
     for (hipEvent_t e : t.ev) (void)hipEventDestroy(e);
@@ -552,9 +555,9 @@ static void choose_reset_shape(cp_handle* h) {
     h->step_lat = (es && (es[0] == '0' || es[0] == '1')) ? es[0] == '1' : small;
     // the WIDE layout (16 lanes per env) where its extra waves still leave SIMDs idle
     const bool wide_ok = !h->f64 && !(h->cfg.phys.model_flags & (CP_MODEL_PERSISTENT | CP_MODEL_SLEEPING));
-    if (wide_ok && h->step_lat && h->cfg.num_envs <= kWideMax) h->step_lat = CP_SHAPE_WIDE;
-    if (wide_ok && h->reset_lat && (h->cfg.num_envs <= kWideMax || h->cfg.done_on_bounds || lqr_done))
-        h->reset_lat = CP_SHAPE_WIDE;
+    if (wide_ok && h->step_lat) h->step_lat = wide_shape_for(h->cfg.num_envs);
+    if (wide_ok && h->reset_lat)
+        h->reset_lat = (h->cfg.done_on_bounds || lqr_done) ? CP_SHAPE_WIDE : wide_shape_for(h->cfg.num_envs);
     if (h->reset_req != CP_SHAPE_AUTO) h->reset_lat = h->reset_req;
     if (h->step_req != CP_SHAPE_AUTO) h->step_lat = h->step_req;
     if (h->f64) h->reset_lat = h->step_lat = 1;  // fp64: the 512-register shape only
@@ -805,12 +808,13 @@ int64_t cp_state_bytes(const cp_handle* h) {
 int cp_set_kernel_shape(cp_handle* h, int step_shape, int reset_shape) {
     if (!h) return fail(h, "cp_set_kernel_shape: null handle");
     auto ok = [](int v) {
-        return v == CP_SHAPE_AUTO || v == CP_SHAPE_THROUGHPUT || v == CP_SHAPE_LATENCY || v == CP_SHAPE_WIDE;
+        return v == CP_SHAPE_AUTO || v == CP_SHAPE_THROUGHPUT || v == CP_SHAPE_LATENCY || v == CP_SHAPE_WIDE ||
+               v == CP_SHAPE_WIDE8;
     };
     if (!ok(step_shape) || !ok(reset_shape))
-        return fail(h, "cp_set_kernel_shape: shapes must be CP_SHAPE_AUTO, CP_SHAPE_THROUGHPUT, CP_SHAPE_LATENCY or "
-                       "CP_SHAPE_WIDE");
-    auto fixed = [](int v) { return v == CP_SHAPE_THROUGHPUT || v == CP_SHAPE_WIDE; };
+        return fail(h, "cp_set_kernel_shape: shapes must be CP_SHAPE_AUTO, CP_SHAPE_THROUGHPUT, CP_SHAPE_LATENCY, "
+                       "CP_SHAPE_WIDE or CP_SHAPE_WIDE8");
+    auto fixed = [](int v) { return v == CP_SHAPE_THROUGHPUT || v == CP_SHAPE_WIDE || v == CP_SHAPE_WIDE8; };
     if ((h->f64 || (h->cfg.phys.model_flags & (CP_MODEL_PERSISTENT | CP_MODEL_SLEEPING))) &&
         (fixed(step_shape) || fixed(reset_shape)))
         return fail(h, "cp_set_kernel_shape: fp64, persistent-manifold and sleeping-model handles have the latency "

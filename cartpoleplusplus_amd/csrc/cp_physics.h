@@ -2077,78 +2077,153 @@ CP_DEV real body_f3(int id, const float v[CP_NUM_BODIES][3], int k) {
     asm volatile("" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(x4));
     return id == 0 ? x0 : (id == 1 ? x1 : (id == 2 ? x2 : (id == 3 ? x3 : x4)));
 }
-// the narrowphase + row setup of the substep on the WIDE layout: the same contacts, rows, slots, caps,
-// warm-start reads and writes as substep_prep's pair loop over the lane's 5 pairs (bit for bit)
+// One local pair's narrowphase on its lane of the WIDE layout: boxes, broadphase, warm-start cache, contact.
+struct WPair {
+    Box A, Bx;
+    Contact C;
+    bool near;
+    uint32_t oid;
+    real ol0, ol1, ol2, ol3;
+    real mu;
+    int a, bi;
+};
 template <bool ALLIN, bool ES>
-CP_DEV void narrow_wide(Own& O, const cp_physics& P, const Lane& L, real* pool, int& overflow, const Mem& G,
-                        Stamps& ST, bool live, Step& T, int& used, int& fused) {
-    const real inv_dt = P.inv_dt;
-    const int j = L.pj;
-    const bool mine = j < CP_ISLAND_PAIRS;
+CP_DEV void wide_contact(WPair& W, int j, bool plive, const Own& O, const V3& Pcx, const V3& Ppx, const real Pcq[4],
+                         const real Ppq[4], const cp_physics& P, const Lane& L, const Mem& G, Stamps& ST) {
     const bool second = L.isl != 0;
-    const int g = island_pair(L.isl, mine ? j : 0);
-    const int a = pair_a(g), bi = pair_b(g);
-    const bool plive = live && mine;
-    // the partner island's bodies: the partner lane is the same pair's lane of the other island (a replica)
-    const V3 Pcx = partner(O.c.x), Ppx = partner(O.p.x);
-    real Pcq[4], Ppq[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) { Pcq[k] = partner(O.c.q[k]); Ppq[k] = partner(O.p.q[k]); }
+    const int g = island_pair(L.isl, j);
+    W.a = pair_a(g);
+    W.bi = pair_b(g);
     // A: the ground (pairs 0, 1), the own cart (pair 2; island 0's cross pairs), the partner's pole (island 1's
     // cross pairs).  B: the own cart (pair 0; island 1's pair 3), the own pole (pairs 1, 2; island 1's pair 4),
     // the partner's cart / pole (island 0's pairs 3 / 4) -- substep_prep's pair_body per pair
     const bool a_ground = j < 2, a_ppole = j >= 3 && second;
     const bool b_partner = j >= 3 && !second, b_pole = j == 1 || j == 2 || j == 4;
-    Box A, Bx;
     real bq[4];
     {
         const V3 zero = mk(real(0.0), real(0.0), real(0.0));
-        A.c = a_ground ? zero : selv(a_ppole, Ppx, O.c.x);
+        W.A.c = a_ground ? zero : selv(a_ppole, Ppx, O.c.x);
         real aq[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) aq[k] = a_ground ? (k == 3 ? real(1.0) : real(0.0)) : (a_ppole ? Ppq[k] : O.c.q[k]);
-        A.ax = quat_axes(aq[0], aq[1], aq[2], aq[3]);
-        A.h0 = body_f3(a, P.half_extents, 0);
-        A.h1 = body_f3(a, P.half_extents, 1);
-        A.h2 = body_f3(a, P.half_extents, 2);
-        Bx.c = b_partner ? selv(b_pole, Ppx, Pcx) : selv(b_pole, O.p.x, O.c.x);
+        W.A.ax = quat_axes(aq[0], aq[1], aq[2], aq[3]);
+        W.A.h0 = body_f3(W.a, P.half_extents, 0);
+        W.A.h1 = body_f3(W.a, P.half_extents, 1);
+        W.A.h2 = body_f3(W.a, P.half_extents, 2);
+        W.Bx.c = b_partner ? selv(b_pole, Ppx, Pcx) : selv(b_pole, O.p.x, O.c.x);
 #pragma unroll
         for (int k = 0; k < 4; ++k) bq[k] = b_partner ? (b_pole ? Ppq[k] : Pcq[k]) : (b_pole ? O.p.q[k] : O.c.q[k]);
-        Bx.ax = quat_axes(real(0.0), real(0.0), real(0.0), real(1.0));  // placeholder: B's axes after the broadphase
-        Bx.h0 = body_f3(bi, P.half_extents, 0);
-        Bx.h1 = body_f3(bi, P.half_extents, 1);
-        Bx.h2 = body_f3(bi, P.half_extents, 2);
+        W.Bx.ax = quat_axes(real(0.0), real(0.0), real(0.0), real(1.0));  // placeholder: B's axes after the broadphase
+        W.Bx.h0 = body_f3(W.bi, P.half_extents, 0);
+        W.Bx.h1 = body_f3(W.bi, P.half_extents, 1);
+        W.Bx.h2 = body_f3(W.bi, P.half_extents, 2);
     }
-    Contact C;
-    C.m = 0;
-    C.n = mk(real(0.0), real(0.0), real(1.0));
+    W.C.m = 0;
+    W.C.n = mk(real(0.0), real(0.0), real(1.0));
     const real newmargin = real(P.contact_margin);
-    const bool near = plive && !face_separated(A, Bx, newmargin);
-    if (near) Bx.ax = quat_axes(bq[0], bq[1], bq[2], bq[3]);
-    uint32_t oid = 0xFFFFFFFFu;
-    real ol0 = real(0.0), ol1 = real(0.0), ol2 = real(0.0), ol3 = real(0.0);
-    const int jc = mine ? j : 0;
-    if (near) {  // the pair's warm-start cache (lane-varying field: into the lane's buffer offset)
-        oid = to_bits(G.st.ld(CP_SF_WS_ID(0, 0), G.woff + (uint32_t)jc * G.st.fstride));
-        const uint32_t lo = G.loff + (uint32_t)(4 * jc) * G.st.fstride;
-        ol0 = G.st.ld(CP_SF_WS_LAM(0, 0, 0), lo); ol1 = G.st.ld(CP_SF_WS_LAM(0, 0, 1), lo);
-        ol2 = G.st.ld(CP_SF_WS_LAM(0, 0, 2), lo); ol3 = G.st.ld(CP_SF_WS_LAM(0, 0, 3), lo);
+    W.near = plive && !face_separated(W.A, W.Bx, newmargin);
+    if (W.near) W.Bx.ax = quat_axes(bq[0], bq[1], bq[2], bq[3]);
+    W.oid = 0xFFFFFFFFu;
+    W.ol0 = W.ol1 = W.ol2 = W.ol3 = real(0.0);
+    if (W.near) {  // the pair's warm-start cache (lane-varying field: into the lane's buffer offset)
+        W.oid = to_bits(G.st.ld(CP_SF_WS_ID(0, 0), G.woff + (uint32_t)j * G.st.fstride));
+        const uint32_t lo = G.loff + (uint32_t)(4 * j) * G.st.fstride;
+        W.ol0 = G.st.ld(CP_SF_WS_LAM(0, 0, 0), lo); W.ol1 = G.st.ld(CP_SF_WS_LAM(0, 0, 1), lo);
+        W.ol2 = G.st.ld(CP_SF_WS_LAM(0, 0, 2), lo); W.ol3 = G.st.ld(CP_SF_WS_LAM(0, 0, 3), lo);
     }
-    if (near) box_box<ALLIN, ES>(A, Bx, newmargin, P.edge_bias, C, ST);
-    const real mu = body_f(a, P.friction) * body_f(bi, P.friction);
+    if (W.near) box_box<ALLIN, ES>(W.A, W.Bx, newmargin, P.edge_bias, W.C, ST);
+    W.mu = body_f(W.a, P.friction) * body_f(W.bi, P.friction);
+}
+// the pair's rows (its first mym points, the first myfm of them frictional) into the island's pool column from
+// slot myb / friction slot myfb, as substep_prep's row setup; returns the pair's new warm-start id word
+CP_DEV uint32_t wide_rows(const WPair& W, int myb, int myfb, int mym, int myfm, real* pool, const cp_physics& P) {
+    const real inv_dt = P.inv_dt;
+    uint32_t nid = 0xFFFFFFFFu;
+    if (__ballot(mym > 0) == 0ull) return nid;
+    const int a = W.a, bi = W.bi;
+    const real ima = body_f(a, P.inv_mass), imb = body_f(bi, P.inv_mass);
+    const Sym Ma = world_inv_inertia(W.A.ax, body_f3(a, P.inv_inertia, 0), body_f3(a, P.inv_inertia, 1),
+                                     body_f3(a, P.inv_inertia, 2));
+    const Sym Mb = world_inv_inertia(W.Bx.ax, body_f3(bi, P.inv_inertia, 0), body_f3(bi, P.inv_inertia, 1),
+                                     body_f3(bi, P.inv_inertia, 2));
+    const V3 xa = W.A.c, xb = W.Bx.c;
+    V3 t1 = mk(real(0.0), real(0.0), real(0.0)), t2 = t1;
+    if (W.mu > real(0.0)) plane_space(W.C.n, t1, t2);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (k < mym) {
+            const int s = myb + k;
+            const V3 rb = sub(W.C.p[k], xb);
+            const real K = row_k_dyn(a, ima, imb, xa, xb, Ma, Mb, rb, W.C.n);
+            const real dist = W.C.d[k];
+            const real tg = dist > real(0.0) ? -(dist * inv_dt) : -((P.erp * dist) * inv_dt);
+            const int id = (int)((W.C.ids >> (8 * k)) & 0xFFu);
+            real l0 = real(0.0);
+            if ((int)(W.oid & 0xFFu) == id) l0 = W.ol0;
+            else if ((int)((W.oid >> 8) & 0xFFu) == id) l0 = W.ol1;
+            else if ((int)((W.oid >> 16) & 0xFFu) == id) l0 = W.ol2;
+            else if ((int)((W.oid >> 24) & 0xFFu) == id) l0 = W.ol3;
+            pool_n(pool, F_RBX, s) = rb.x;
+            pool_n(pool, F_RBY, s) = rb.y;
+            pool_n(pool, F_RBZ, s) = rb.z;
+            pool_n(pool, F_IE, s) = real(1.0) / K;
+            pool_n(pool, F_TG, s) = tg;
+            pool_n(pool, F_LAM, s) = P.warmstart * l0;
+            nid = (nid & ~(0xFFu << (8 * k))) | ((uint32_t)id << (8 * k));
+            if (k < myfm) {
+                const int fs = myfb + k;
+                pool_f(pool, FF_IE1, fs) = real(1.0) / row_k_dyn(a, ima, imb, xa, xb, Ma, Mb, rb, t1);
+                pool_f(pool, FF_IE2, fs) = real(1.0) / row_k_dyn(a, ima, imb, xa, xb, Ma, Mb, rb, t2);
+                pool_f(pool, FF_L1, fs) = real(0.0);
+                pool_f(pool, FF_L2, fs) = real(0.0);
+            }
+        }
+    }
+    return nid;
+}
+// the lane pair (of the env's LW / 2) that owns local pair j: LW 16 -> pair j on lane pair j; LW 8 -> pairs 0-2
+// on lane pairs 0-2, both cross pairs (3, 4: mostly separated by the broadphase) on lane pair 3
+template <int LW>
+CP_DEV constexpr int wide_owner(int j) { return LW == 16 ? j : (j < 3 ? j : 3); }
+// the narrowphase + row setup of the substep on the WIDE layout: the same contacts, rows, slots, caps,
+// warm-start reads and writes as substep_prep's pair loop over the lane's 5 pairs (bit for bit)
+template <int LW, bool ALLIN, bool ES>
+CP_DEV void narrow_wide(Own& O, const cp_physics& P, const Lane& L, real* pool, int& overflow, const Mem& G,
+                        Stamps& ST, bool live, Step& T, int& used, int& fused) {
+    static_assert(LW == 8 || LW == 16, "WIDE: 8 or 16 lanes per env");
+    const int pj = L.pj;
+    // the lane's pairs: j0 (LW 16: pj < 5; LW 8: pj < 4), and on LW 8's lane pair 3 also pair 4
+    const bool has0 = LW == 16 ? pj < CP_ISLAND_PAIRS : pj < 4;
+    const bool has1 = LW == 8 && pj == 3;
+    const int j0 = has0 ? pj : 0;
+    // the partner island's bodies: the partner lane is the same pair's lane of the other island (a replica)
+    const V3 Pcx = partner(O.c.x), Ppx = partner(O.p.x);
+    real Pcq[4], Ppq[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { Pcq[k] = partner(O.c.q[k]); Ppq[k] = partner(O.p.q[k]); }
+    WPair W0, W1;
+    wide_contact<ALLIN, ES>(W0, j0, live && has0, O, Pcx, Ppx, Pcq, Ppq, P, L, G, ST);
+    if constexpr (LW == 8) wide_contact<ALLIN, ES>(W1, 4, live && has1, O, Pcx, Ppx, Pcq, Ppq, P, L, G, ST);
     // every replica gathers the island's 5 pairs: point count | friction bit, normal
-    const int grp = (int)(threadIdx.x & ~15u) + L.isl;
-    const uint32_t word = (uint32_t)C.m | (mu > real(0.0) ? 8u : 0u);
+    const int grp = (int)(threadIdx.x & ~(unsigned)(LW - 1)) + L.isl;
+    const uint32_t word0 = (uint32_t)W0.C.m | (W0.mu > real(0.0) ? 8u : 0u);
+    uint32_t word1 = 0u;
+    if constexpr (LW == 8) word1 = (uint32_t)W1.C.m | (W1.mu > real(0.0) ? 8u : 0u);
     uint32_t cw[CP_ISLAND_PAIRS];
     V3 cn[CP_ISLAND_PAIRS];
 #pragma unroll
     for (int k = 0; k < CP_ISLAND_PAIRS; ++k) {
-        cw[k] = (uint32_t)__shfl((int)word, grp + 2 * k, WAVE);
-        cn[k] = mk(__shfl(C.n.x, grp + 2 * k, WAVE), __shfl(C.n.y, grp + 2 * k, WAVE), __shfl(C.n.z, grp + 2 * k, WAVE));
+        const int src = grp + 2 * wide_owner<LW>(k);
+        const bool second_slot = LW == 8 && k == 4;
+        const uint32_t w = second_slot ? word1 : word0;
+        const V3 n = second_slot ? W1.C.n : W0.C.n;
+        cw[k] = (uint32_t)__shfl((int)w, src, WAVE);
+        cn[k] = mk(__shfl(n.x, src, WAVE), __shfl(n.y, src, WAVE), __shfl(n.z, src, WAVE));
     }
     // slots and caps in pair order (substep_prep: a point past MAXP rows, or a frictional point past MAXF, is
     // dropped and counted)
-    int base = 0, fbase = 0, ov = 0, myb = 0, myfb = 0, mym = 0, myfm = 0;
+    int base = 0, fbase = 0, ov = 0;
+    int b0 = 0, fb0 = 0, m0 = 0, fm0 = 0, b1 = 0, fb1 = 0, m1 = 0, fm1 = 0;
     int mk_[CP_ISLAND_PAIRS], bk_[CP_ISLAND_PAIRS], fmk_[CP_ISLAND_PAIRS], fbk_[CP_ISLAND_PAIRS];
 #pragma unroll
     for (int k = 0; k < CP_ISLAND_PAIRS; ++k) {
@@ -2158,59 +2233,28 @@ CP_DEV void narrow_wide(Own& O, const cp_physics& P, const Lane& L, real* pool, 
         const int fm = fr ? (m < MAXF - fbase ? m : MAXF - fbase) : 0;
         ov += (n - m) + (fr ? m - fm : 0);
         mk_[k] = m; bk_[k] = base; fmk_[k] = fm; fbk_[k] = fbase;
-        if (k == j) { myb = base; myfb = fbase; mym = m; myfm = fm; }
+        if (has0 && k == j0) { b0 = base; fb0 = fbase; m0 = m; fm0 = fm; }
+        if (LW == 8 && k == 4 && has1) { b1 = base; fb1 = fbase; m1 = m; fm1 = fm; }
         base += m;
         fbase += fm;
     }
     overflow += ov;
     used = base;
     fused = fbase;
-    // the own pair's rows into the island's pool column
-    uint32_t nid = 0xFFFFFFFFu;
-    if (__ballot(mym > 0) != 0ull) {
-        const real ima = body_f(a, P.inv_mass), imb = body_f(bi, P.inv_mass);
-        const Sym Ma = world_inv_inertia(A.ax, body_f3(a, P.inv_inertia, 0), body_f3(a, P.inv_inertia, 1),
-                                         body_f3(a, P.inv_inertia, 2));
-        const Sym Mb = world_inv_inertia(Bx.ax, body_f3(bi, P.inv_inertia, 0), body_f3(bi, P.inv_inertia, 1),
-                                         body_f3(bi, P.inv_inertia, 2));
-        const V3 xa = A.c, xb = Bx.c;
-        V3 t1 = mk(real(0.0), real(0.0), real(0.0)), t2 = t1;
-        if (mu > real(0.0)) plane_space(C.n, t1, t2);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (k < mym) {
-                const int s = myb + k;
-                const V3 rb = sub(C.p[k], xb);
-                const real K = row_k_dyn(a, ima, imb, xa, xb, Ma, Mb, rb, C.n);
-                const real dist = C.d[k];
-                const real tg = dist > real(0.0) ? -(dist * inv_dt) : -((P.erp * dist) * inv_dt);
-                const int id = (int)((C.ids >> (8 * k)) & 0xFFu);
-                real l0 = real(0.0);
-                if ((int)(oid & 0xFFu) == id) l0 = ol0;
-                else if ((int)((oid >> 8) & 0xFFu) == id) l0 = ol1;
-                else if ((int)((oid >> 16) & 0xFFu) == id) l0 = ol2;
-                else if ((int)((oid >> 24) & 0xFFu) == id) l0 = ol3;
-                pool_n(pool, F_RBX, s) = rb.x;
-                pool_n(pool, F_RBY, s) = rb.y;
-                pool_n(pool, F_RBZ, s) = rb.z;
-                pool_n(pool, F_IE, s) = real(1.0) / K;
-                pool_n(pool, F_TG, s) = tg;
-                pool_n(pool, F_LAM, s) = P.warmstart * l0;
-                nid = (nid & ~(0xFFu << (8 * k))) | ((uint32_t)id << (8 * k));
-                if (k < myfm) {
-                    const int fs = myfb + k;
-                    pool_f(pool, FF_IE1, fs) = real(1.0) / row_k_dyn(a, ima, imb, xa, xb, Ma, Mb, rb, t1);
-                    pool_f(pool, FF_IE2, fs) = real(1.0) / row_k_dyn(a, ima, imb, xa, xb, Ma, Mb, rb, t2);
-                    pool_f(pool, FF_L1, fs) = real(0.0);
-                    pool_f(pool, FF_L2, fs) = real(0.0);
-                }
-            }
-        }
+    // the own pairs' rows into the island's pool column, and their warm-start id words (each pair's lane reads
+    // it, and rewrites it, every substep)
+    {
+        const uint32_t nid = wide_rows(W0, b0, fb0, m0, fm0, pool, P);
+        const int om = (int)((O.wsm >> (3 * j0)) & 7u);
+        const bool idw = W0.near ? nid != W0.oid : om > 0;
+        if (live && has0 && idw) G.st.st(CP_SF_WS_ID(0, 0), G.woff + (uint32_t)j0 * G.st.fstride, bits_to<real>(nid));
     }
-    // the own pair's warm-start id word (the pair's lane reads it, and rewrites it, every substep)
-    const int om = (int)((O.wsm >> (3 * jc)) & 7u);
-    const bool idw = near ? nid != oid : om > 0;
-    if (plive && idw) G.st.st(CP_SF_WS_ID(0, 0), G.woff + (uint32_t)jc * G.st.fstride, bits_to<real>(nid));
+    if constexpr (LW == 8) {
+        const uint32_t nid = wide_rows(W1, b1, fb1, m1, fm1, pool, P);
+        const int om = (int)((O.wsm >> 12) & 7u);
+        const bool idw = W1.near ? nid != W1.oid : om > 0;
+        if (live && has1 && idw) G.st.st(CP_SF_WS_ID(0, 0), G.woff + 4u * G.st.fstride, bits_to<real>(nid));
+    }
     // every replica: the island's manifold headers and the warm-start point counts
 #pragma unroll
     for (int k = 0; k < CP_ISLAND_PAIRS; ++k) {
@@ -2223,7 +2267,7 @@ CP_DEV void narrow_wide(Own& O, const cp_physics& P, const Lane& L, real* pool, 
     }
 }
 
-template <bool ALLIN = false, bool PM = false, bool SLP = false, bool ES = false, bool WIDE = false>
+template <bool ALLIN = false, bool PM = false, bool SLP = false, bool ES = false, int WIDE = 0>
 CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, real* pool, real* pool0, int& overflow,
                          const Mem& G, Stamps& ST, bool live, Ctx& c) {
     const real dt = P.dt, inv_dt = P.inv_dt;
@@ -2233,8 +2277,8 @@ CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, rea
     //    local pairs (the global pair, hence the bodies, differ between the two lanes)
     int used = 0, fused = 0;
     static_assert(!(WIDE && (PM || SLP)), "the WIDE layout is built for the default contact model");
-    if constexpr (WIDE) {
-        narrow_wide<ALLIN, ES>(O, P, L, pool, overflow, G, ST, live, T, used, fused);
+    if constexpr (WIDE != 0) {
+        narrow_wide<WIDE, ALLIN, ES>(O, P, L, pool, overflow, G, ST, live, T, used, fused);
     } else {
     // one local pair; GROUND: j is 0 or 1, whose first body is the static ground on both
     // islands, so its box is compile-time (centre 0, identity axes)
@@ -2537,7 +2581,7 @@ CP_DEV void substep_prep(Own& O, Sim& X, const cp_physics& P, const Lane& L, rea
 // Phase 3: whole-env velocities from the two lanes' islands (both lanes of every
 // env active), the warm-start cache refresh and the integration (DESIGN.md
 // §Physics model 5b-7).
-template <bool PM = false, bool SLP = false, bool WIDE = false>
+template <bool PM = false, bool SLP = false, int WIDE = 0>
 CP_DEV void substep_finish(Own& O, const cp_physics& P, const Lane& L, const Ctx& c, real* pool, const Mem& G,
                            Stamps& ST, bool live) {
     const real dt = P.dt, inv_dt = P.inv_dt;
@@ -2557,7 +2601,7 @@ CP_DEV void substep_finish(Own& O, const cp_physics& P, const Lane& L, const Ctx
         for (int j = 0; j < CP_ISLAND_PAIRS; ++j) {
             const int cnt = pk_cnt(c.T.pk[j]), base = pk_base(c.T.pk[j]);
             // (WIDE: the pair's own lane, which reads the entry in the next substep's narrowphase)
-            if (pk_wcnt(c.T.pk[j]) > 0 && (!WIDE || L.pj == j)) {  // one branch per pair: rewriting a zero slot with 0 is harmless
+            if (pk_wcnt(c.T.pk[j]) > 0 && (WIDE == 0 || L.pj == wide_owner<WIDE == 0 ? 16 : WIDE>(j))) {  // one branch per pair: rewriting a zero slot with 0 is harmless
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
                     G.sl(CP_SF_WS_LAM(0, j, k), (k < cnt) ? pool_n(pool, F_LAM, base + k) : real(0.0));
@@ -2633,7 +2677,7 @@ CP_DEV void substep_finish(Own& O, const cp_physics& P, const Lane& L, const Ctx
 // (sweeps_c44) and the all-inside face-contact exit (face_contact<ALLIN>).
 // PM: CP_MODEL_PERSISTENT (Bullet's persistent manifold, per-row normals in the pool).
 // SLP: CP_MODEL_SLEEPING (Bullet's deactivation: sleeping islands are neither integrated nor solved).
-template <bool FAST = false, bool C44 = false, bool ALLIN = C44, bool PM = false, bool SLP = false, bool WIDE = false>
+template <bool FAST = false, bool C44 = false, bool ALLIN = C44, bool PM = false, bool SLP = false, int WIDE = 0>
 CP_DEV void substep(Own& O, const cp_physics& P, const Lane& L, real* pool, real* pool0, int& overflow,
                     const Mem& G, Stamps& ST, bool live = true) {
     Ctx c;

@@ -321,6 +321,7 @@ int64_t cp_state_bytes(const cp_handle* h);   /* CP_STATE_FIELDS * B * sizeof(re
 #define CP_SHAPE_THROUGHPUT 0
 #define CP_SHAPE_LATENCY    1
 #define CP_SHAPE_WIDE       2
+#define CP_SHAPE_WIDE8      3   /* the WIDE layout on 8 lanes per env (both cross pairs on one lane pair) */
 int cp_set_kernel_shape(cp_handle* h, int step_shape, int reset_shape);
 int cp_get_kernel_shape(const cp_handle* h, int* step_shape, int* reset_shape);   /* the shapes in use */
 

@@ -24,8 +24,9 @@ pytestmark = pytest.mark.gpu
 # (step kernel shape, autoreset kernel shape): the combinations of the two register budgets, and the WIDE
 # layout of the latency budget (16 lanes per env, round 6) as step kernel, reset kernel and both
 SHAPES = [("throughput", "throughput"), ("latency", "latency"), ("throughput", "latency"),
-          ("latency", "throughput"), ("wide", "wide"), ("throughput", "wide"), ("wide", "latency")]
-SHAPE_IDS = ["tp-tp", "lat-lat", "tp-lat", "lat-tp", "wide-wide", "tp-wide", "wide-lat"]
+          ("latency", "throughput"), ("wide", "wide"), ("throughput", "wide"), ("wide", "latency"),
+          ("wide8", "wide8")]
+SHAPE_IDS = ["tp-tp", "lat-lat", "tp-lat", "lat-tp", "wide-wide", "tp-wide", "wide-lat", "wide8-wide8"]
 shapes = pytest.mark.parametrize("shape", SHAPES, ids=SHAPE_IDS)
 
 

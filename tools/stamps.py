@@ -21,6 +21,8 @@ steps = int(os.environ.get("STEPS", "150"))
 warm = int(os.environ.get("WARM", "20"))
 bounds = os.environ.get("BOUNDS", "0") == "1"
 env = BatchedCartpole(B, 0, action_repeats=3, initial_force=55.0, autoreset=True, seed=1234, done_on_bounds=bounds)
+if os.environ.get("SHAPE"):   # e.g. SHAPE=latency,wide (step, reset); default: the library's choice
+    env.set_kernel_shape(*os.environ["SHAPE"].split(","))
 gen = torch.Generator(device="cuda").manual_seed(1234)
 acts = torch.randint(0, 5, (steps + warm, B, 2), dtype=torch.int8, device="cuda", generator=gen)
 env.reset()
@@ -32,7 +34,7 @@ assert rc == 1, "not a stamp build (set CP_LIB_PATH to libcartpole_hip_stamps.so
 for t in range(steps):
     env.step(acts[warm + t])
 env.lib.cp_debug_stamps(env.h, out, 0)
-res = {"B": B, "steps": steps, "done_on_bounds": bounds}
+res = {"B": B, "steps": steps, "done_on_bounds": bounds, "kernel_shape": env.kernel_shape()}
 for name, base in (("step_kernel", 0), ("reset_kernel", 16)):
     narrow, vel, solve, integ, sweeps, substeps, total, waves = list(out)[base:base + 8]
     sel, bb, rows = list(out)[base + 8:base + 11]
