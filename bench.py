@@ -509,8 +509,8 @@ def cpu_baseline(R, budget_s):
 
 def gym_mirror_rate(steps=400):
     """The reference's own surface (BulletCartpole, B = 1, R = 2, discrete, numpy in / numpy copy
-    out per step, the step replayed as a hipGraph) on this GPU, for comparison with the CPU
-    path's C1 rate: a B = 1 step is latency-bound (2 substeps of one wave)."""
+    out per step; the step one launch over pinned host buffers, step_io "zero_copy") on this GPU,
+    for comparison with the CPU path's C1 rate: a B = 1 step is latency-bound (2 substeps of one wave)."""
     import argparse
 
     import numpy as np
@@ -538,13 +538,13 @@ def gym_mirror_rate(steps=400):
                 env.reset()
                 resets += 1
         dt = time.perf_counter() - t0
-        use_graph = env.use_graph
+        step_io = env.step_io
         shape = "/".join(env._env.kernel_shape())
     finally:
         env.close()
         np.random.set_state(np_state)
     return {"value": round(n / dt, 1), "unit": "env-steps/s", "ms_per_step": round(dt / n * 1e3, 4),
-            "reset_ms": round(t_reset * 1e3, 2), "step_as_hipgraph": use_graph,
+            "reset_ms": round(t_reset * 1e3, 2), "step_io": step_io,
             "kernel_shape": shape,
             "sample": f"C1 config on the GPU: B=1, R=2, F_init 55, discrete random actions, {n} steps incl. "
                       f"{resets} resets ({dt:.2f} s), after 20 warm-up steps (the step graph's capture)"}

@@ -10,10 +10,10 @@ Same surface as /root/reference/bullet_cartpole.py so the agents
   .render(mode, close), .seed(), .configure()  no-ops (:169-176)
   .monkey_positions / .monkey_velocities  12-state pole readback (:212-234)
 
-The env is one lane pair of the batched kernel (B = 1) on a GPU.  After the first step the
-step is a captured hipGraph (torch.cuda.CUDAGraph on ROCm): action H2D from a pinned host
-buffer, cp_step, obs + readback D2H into pinned host buffers, then one host sync; a
-launch-bound B = 1 step pays one graph launch instead of four API calls.  Bump forces are
+The env is one env of the batched kernel (B = 1) on a GPU.  A step is one cp_step launch whose
+action, obs and readback buffers are pinned host memory mapped for the GPU (hipHostGetDevicePointer),
+then one stream sync: no copy operations around the kernel (step_io "zero_copy"; "graph" replays
+the H2D copy, cp_step and D2H copies as a captured hipGraph, "eager" issues them one by one).  Bump forces are
 drawn from the global legacy `np.random` stream in the reference's order and with
 its formula (:354-359: theta = U * 2 * pi, f = F (cos, sin)), so a given
 `np.random.seed` produces the reference's pushes exactly (parity mode,
@@ -21,13 +21,14 @@ CP_BUMP_HOST).  Errors follow the reference: step before reset -> AttributeError
 bad --num-cameras -> ValueError, bad --reward-calc -> AssertionError, an int
 action -> TypeError, a (1,2) action -> IndexError (the fork indexes action[1]).
 """
+import ctypes as C
 import sys
 import time
 
 import numpy as np
 import torch
 
-from . import abi
+from . import abi, native
 from .batched import BatchedCartpole
 from .spaces import Box, Discrete, Env
 
@@ -115,13 +116,35 @@ class BulletCartpole(Env):
             self._env.enable_raster(True, width=self.render_width, height=self.render_height,
                                     num_cameras=self.num_cameras)
         self._act = torch.zeros((1, 2, 2), dtype=torch.float32, device=self._env.device)
-        # pinned host staging for the graph-captured step (see _step_graph)
+        # pinned host buffers: the zero-copy step's own (mapped) and the graph / eager steps' staging
         self._h_act = torch.zeros((1, 2, 2), dtype=torch.float32).pin_memory()
         self._h_obs = torch.zeros((1, self.repeats, 2, 7), dtype=torch.float32).pin_memory()
         self._h_rb = torch.zeros(abi.readback_shape(1, self.repeats, self.steps_per_repeat),
                                  dtype=torch.float32).pin_memory()
+        self._h_rew = torch.zeros(1, dtype=torch.float32).pin_memory()
+        self._h_done = torch.zeros(1, dtype=torch.uint8).pin_memory()
         self._graph = None
-        self.use_graph = not self.use_raw_pixels and not self.event_log
+        # How a step crosses the host boundary: "zero_copy" (the kernel reads the action from and writes
+        # its obs and readback to pinned host memory mapped for the GPU: one launch and a stream sync, no
+        # copy operations), "graph" (H2D copy, step, D2H copies replayed as a captured hipGraph) or "eager"
+        # (the same as separate calls).  Raster obs stay on the device (eager).
+        self._zc = None
+        if not self.use_raw_pixels:
+            try:
+                self._zc = tuple(native.mapped_device_pointer(t)
+                                 for t in (self._h_act, self._h_obs, self._h_rew, self._h_done, self._h_rb))
+            except native.CartpoleError:
+                self._zc = None
+        self.step_io = "zero_copy" if self._zc else ("eager" if self.use_raw_pixels else "graph")
+        self._rb_host = False    # the handle's readback pointer: the pinned buffer (zero_copy) or the device one
+
+    @property
+    def use_graph(self):
+        return self.step_io == "graph"
+
+    @use_graph.setter
+    def use_graph(self, on):
+        self.step_io = "graph" if on else "eager"
 
     def _capture(self, obs):
         # set_state_element_for_repeat (:298-311): pixels (float16 values, float32 state)
@@ -146,7 +169,25 @@ class BulletCartpole(Env):
         self._graph = None
         self._env.close()
 
+    def _readback_to(self, host):
+        if host != self._rb_host:
+            ptr = self._zc[4] if host else C.c_void_p(self._env.readback.data_ptr())
+            native.check(self._env.h, self._env.lib.cp_set_readback(self._env.h, ptr, 1), "cp_set_readback")
+            self._rb_host = host
+
+    def _step_zero_copy(self, a):
+        """One env step in one launch: action, obs and readback in pinned host memory (mapped), then a
+        stream sync; the same kernel and numbers as the other paths."""
+        self._readback_to(True)
+        self._h_act.numpy()[...] = a.reshape(1, 2, 2)
+        d_act, d_obs, d_rew, d_done, _ = self._zc
+        st = torch.cuda.current_stream(self._env.device)
+        native.check(self._env.h, self._env.lib.cp_step(self._env.h, d_act, abi.CP_ACTION_CONTINUOUS, d_obs, d_rew,
+                                                         d_done, None, C.c_void_p(st.cuda_stream)), "cp_step")
+        st.synchronize()
+
     def _step_eager(self, a):
+        self._readback_to(False)
         self._act.copy_(torch.from_numpy(a).view(1, 2, 2))
         obs, _, _ = self._env.step(self._act)
         self._h_obs.copy_(obs)
@@ -156,6 +197,7 @@ class BulletCartpole(Env):
         """One env step as a replay of the captured graph (H2D action, cp_step, D2H obs and
         readback); the handle has no autoreset and no timing, so the launches are the same on
         every call and capture once."""
+        self._readback_to(False)
         self._h_act.numpy()[...] = a.reshape(1, 2, 2)
         if self._graph is None:
             self._graph = torch.cuda.CUDAGraph()
@@ -196,7 +238,9 @@ class BulletCartpole(Env):
             fx, fy = action[0]
             fx2, fy2 = action[1]
             a = np.asarray([[fx, fy], [fx2, fy2]], np.float32)
-        if self.use_graph:
+        if self.step_io == "zero_copy":
+            self._step_zero_copy(a)
+        elif self.step_io == "graph":
             self._step_graph(a)
         else:
             self._step_eager(a)

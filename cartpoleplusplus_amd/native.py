@@ -122,3 +122,22 @@ def check(h, status, what):
     if status != 0:
         msg = load().cp_last_error(h)
         raise CartpoleError(f"{what} failed: {msg.decode() if msg else 'unknown error'}")
+
+
+_hip = None
+
+
+def mapped_device_pointer(t):
+    """The device address of a pinned host tensor (hipHostGetDevicePointer): a kernel may read and write
+    pinned host memory the runtime has mapped for the GPU directly, with no copy operation (the gym
+    mirror's zero-copy step).  Raises CartpoleError when the memory is not mapped."""
+    global _hip
+    if not t.is_pinned():
+        raise CartpoleError("mapped_device_pointer: the tensor is not in pinned host memory")
+    if _hip is None:
+        _hip = C.CDLL("libamdhip64.so")
+    p = C.c_void_p()
+    rc = _hip.hipHostGetDevicePointer(C.byref(p), C.c_void_p(t.data_ptr()), 0)
+    if rc != 0 or not p.value:
+        raise CartpoleError(f"hipHostGetDevicePointer failed ({rc}): pinned memory not mapped for the GPU")
+    return C.c_void_p(p.value)

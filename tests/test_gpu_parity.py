@@ -352,19 +352,23 @@ def test_gym_mirror_matches_oracle_and_reference_errors(oracle_mod):
     denv.step([1, 4])
 
 
-@pytest.mark.parametrize("graph", [True, False], ids=["hipgraph", "eager"])
-def test_gym_mirror_discrete_c1_vs_oracle(oracle_mod, graph):
+@pytest.mark.parametrize("io", ["zero_copy", "graph", "eager", "mixed"])
+def test_gym_mirror_discrete_c1_vs_oracle(oracle_mod, io):
     """C1's configuration through the reference's surface: B = 1, R = 2 (the reference default),
     F_init 55, discrete actions, two episodes of 200 steps with the reference's own reset loop
     (the agent calls reset() after done); obs and the 12-state readback (monkey_positions /
-    velocities, the :224 bug included) bit-exact against the oracle, with the step replayed as a
-    hipGraph and eagerly."""
+    velocities, the :224 bug included) bit-exact against the oracle, with the step as one launch over
+    mapped pinned host buffers (the default), replayed as a hipGraph, eagerly, and switching between
+    the three every few steps (the readback pointer follows the path)."""
     from cartpoleplusplus_amd.bullet_cartpole import BulletCartpole, add_opts, draw_bump_forces
     ap = argparse.ArgumentParser()
     add_opts(ap)
     opts = ap.parse_args(["--initial-force", "55"])
     env = BulletCartpole(opts, discrete_actions=True)
-    env.use_graph = graph
+    assert env.step_io == "zero_copy"
+    ios = ["zero_copy", "graph", "eager"]
+    if io != "mixed":
+        env.step_io = io
     cfg = oracle_mod.default_config(num_envs=1, action_repeats=2, initial_force=55.0, bump_mode=abi.CP_BUMP_HOST)
     orc = oracle_mod.Envs(cfg)
     rng = np.random.default_rng(21)
@@ -377,6 +381,8 @@ def test_gym_mirror_discrete_c1_vs_oracle(oracle_mod, graph):
         done, t = False, 0
         while not done:
             a = rng.integers(0, 5, 2)
+            if io == "mixed":
+                env.step_io = ios[(t // 7) % 3]
             o, r, done, info = env.step(a)
             oo, _, od, rb = orc.step(a.astype(np.int8).reshape(1, 2), readback=True, readback_bug=True)
             _assert_same(o, oo[0], f"episode {ep} step {t} obs")
