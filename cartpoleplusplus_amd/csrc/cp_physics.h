@@ -2131,7 +2131,10 @@ CP_DEV void wide_contact(WPair& W, int j, bool plive, const Own& O, const V3& Pc
         W.ol0 = G.st.ld(CP_SF_WS_LAM(0, 0, 0), lo); W.ol1 = G.st.ld(CP_SF_WS_LAM(0, 0, 1), lo);
         W.ol2 = G.st.ld(CP_SF_WS_LAM(0, 0, 2), lo); W.ol3 = G.st.ld(CP_SF_WS_LAM(0, 0, 3), lo);
     }
+    CP_STAMP(w0);
     if (W.near) box_box<ALLIN, ES>(W.A, W.Bx, newmargin, P.edge_bias, W.C, ST);
+    CP_STAMP(w1);
+    CP_ACC(bb, w0, w1);
     W.mu = body_f(W.a, P.friction) * body_f(W.bi, P.friction);
 }
 // the pair's rows (its first mym points, the first myfm of them frictional) into the island's pool column from
@@ -2202,8 +2205,11 @@ CP_DEV void narrow_wide(Own& O, const cp_physics& P, const Lane& L, real* pool, 
 #pragma unroll
     for (int k = 0; k < 4; ++k) { Pcq[k] = partner(O.c.q[k]); Ppq[k] = partner(O.p.q[k]); }
     WPair W0, W1;
+    CP_STAMP(s0);
     wide_contact<ALLIN, ES>(W0, j0, live && has0, O, Pcx, Ppx, Pcq, Ppq, P, L, G, ST);
     if constexpr (LW == 8) wide_contact<ALLIN, ES>(W1, 4, live && has1, O, Pcx, Ppx, Pcq, Ppq, P, L, G, ST);
+    CP_STAMP(s1);
+    CP_ACC(sel, s0, s1);  // (stamp builds: boxes, broadphase, cache loads and box_box; box_box alone in bb)
     // every replica gathers the island's 5 pairs: point count | friction bit, normal
     const int grp = (int)(threadIdx.x & ~(unsigned)(LW - 1)) + L.isl;
     const uint32_t word0 = (uint32_t)W0.C.m | (W0.mu > real(0.0) ? 8u : 0u);
@@ -2265,6 +2271,8 @@ CP_DEV void narrow_wide(Own& O, const cp_physics& P, const Lane& L, real* pool, 
                   ((live ? (m > omk ? m : omk) : 0u) << 16);
         if (live) O.wsm = (O.wsm & ~(7u << (3 * k))) | (m << (3 * k));
     }
+    CP_STAMP(s3);
+    CP_ACC(rows, s1, s3);  // (stamp builds: the gather and slots, then the rows)
 }
 
 template <bool ALLIN = false, bool PM = false, bool SLP = false, bool ES = false, int WIDE = 0>
