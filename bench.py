@@ -547,7 +547,7 @@ def gym_mirror_rate(steps=400):
             "reset_ms": round(t_reset * 1e3, 2), "step_io": step_io,
             "kernel_shape": shape,
             "sample": f"C1 config on the GPU: B=1, R=2, F_init 55, discrete random actions, {n} steps incl. "
-                      f"{resets} resets ({dt:.2f} s), after 20 warm-up steps (the step graph's capture)"}
+                      f"{resets} resets ({dt:.2f} s), after 20 warm-up steps"}
 
 
 def _pose_diffs(g, o):

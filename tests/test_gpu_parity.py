@@ -436,3 +436,23 @@ def test_cart_friction_config(oracle_mod, shape):
         _assert_same(_np(go), oo, f"obs step {t}")
         _assert_same(_np(gd), od, f"done step {t}")
     _compare_state(gpu, orc, "after 70 steps")
+
+
+def test_auto_shapes_by_batch_size():
+    """CP_SHAPE_AUTO: the widest latency layout whose waves fit the chip once (16
+    lanes per env up to 4,096 envs, 8 up to 8,192, two up to 32,768), the throughput shape above; the
+    reset list of bounds-terminated episodes on 16 lanes; fp64 and the model switches on the two-lane
+    latency layout."""
+    def shapes(B, **kw):
+        env = BatchedCartpole(B, 0, **kw)
+        s = env.kernel_shape()
+        env.close()
+        return s
+    assert shapes(1) == ("wide", "wide")
+    assert shapes(4096, autoreset=True) == ("wide", "wide")
+    assert shapes(8192, autoreset=True) == ("wide8", "wide8")
+    assert shapes(16384, autoreset=True) == ("latency", "latency")
+    assert shapes(65536, autoreset=True) == ("throughput", "throughput")
+    assert shapes(65536, autoreset=True, done_on_bounds=True) == ("throughput", "wide")
+    assert shapes(64, precision="f64") == ("latency", "latency")
+    assert shapes(64, model_flags=abi.CP_MODEL_SLEEPING) == ("latency", "latency")
