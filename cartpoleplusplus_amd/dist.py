@@ -36,8 +36,12 @@ def gather_returns(returns, group=None):
 
 
 def return_histogram(returns, max_len=200):
-    """Histogram of integer episode returns (reward 1.0 per step), bins 0..max_len."""
-    return torch.bincount(returns.to(torch.int64).clamp(0, max_len), minlength=max_len + 1)
+    """Histogram of integer episode returns (reward 1.0 per step), bins 0..max_len.  A scatter-add into
+    a fixed-size histogram: torch.bincount sizes its output from the input's maximum, which waits on
+    the device from the host in the middle of the caller's stream."""
+    idx = returns.to(torch.int64).clamp(0, max_len)
+    hist = torch.zeros(max_len + 1, dtype=torch.int64, device=returns.device)
+    return hist.scatter_add_(0, idx, torch.ones_like(idx))
 
 
 def _visible_filters():
