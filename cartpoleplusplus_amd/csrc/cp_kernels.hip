@@ -2,7 +2,8 @@
 //
 // Replaces bullet_cartpole.py's hot path (BulletCartpole.step/reset and the
 // pybullet calls behind them) for B independent envs, two lanes per env (lane
-// 2e+p owns contact island p; cp_physics.h).  The env kernels (cp_env.h) are written
+// 2e+p owns contact island p; cp_physics.h), or 16 / 8 for the latency-shaped kernels of small
+// batches and reset lists (the WIDE layout: replicas of the lane pair that split the narrowphase).  The env kernels (cp_env.h) are written
 // over `real` and instantiated here for fp32 (namespace cp, the product path) and in
 // cp_kernels64.hip for fp64 (namespace cp64, the parity variant, cp_config.precision).
 // This file also holds the fp32-only kernels (reset-mask compaction, raster obs, event

@@ -13,12 +13,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from cartpoleplusplus_amd import bullet_cartpole  # noqa: E402
 
 
-def kernel_times(shape, steps=300):
+def kernel_times(shape, steps=300, reset=None):
     """B = 1 step and reset kernel times (HIP events around each launch, cp_timing) for one shape."""
     import torch
     from cartpoleplusplus_amd.batched import BatchedCartpole
     env = BatchedCartpole(1, 0, action_repeats=2, initial_force=55.0, seed=3, autoreset=True)
-    env.set_kernel_shape(shape, shape)
+    env.set_kernel_shape(shape, reset or shape)
     env.reset()
     a = torch.zeros((1, 2), dtype=torch.int8, device="cuda")
     for _ in range(20):
@@ -40,14 +40,15 @@ def kernel_times(shape, steps=300):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="auto")
+    ap.add_argument("--reset-shape", default=None)
     ap.add_argument("--steps", type=int, default=400)
     a = ap.parse_args()
-    kt = kernel_times(a.shape)
+    kt = kernel_times(a.shape, reset=a.reset_shape or a.shape)
     p = argparse.ArgumentParser()
     bullet_cartpole.add_opts(p)
     opts = p.parse_args(["--initial-force", "55"])
     env = bullet_cartpole.BulletCartpole(opts, discrete_actions=True)
-    env._env.set_kernel_shape(a.shape, a.shape)
+    env._env.set_kernel_shape(a.shape, a.reset_shape or a.shape)
     rng = np.random.default_rng(0)
     np.random.seed(0)
     env.reset()
