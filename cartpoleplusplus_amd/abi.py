@@ -108,8 +108,9 @@ CP_SHAPE_THROUGHPUT = 0
 CP_SHAPE_LATENCY = 1
 CP_SHAPE_WIDE = 2
 CP_SHAPE_WIDE8 = 3
+CP_SHAPE_WIDE64 = 4
 SHAPES = {"auto": CP_SHAPE_AUTO, "throughput": CP_SHAPE_THROUGHPUT, "latency": CP_SHAPE_LATENCY, "wide": CP_SHAPE_WIDE,
-          "wide8": CP_SHAPE_WIDE8}
+          "wide8": CP_SHAPE_WIDE8, "wide64": CP_SHAPE_WIDE64}
 
 
 class cp_config(C.Structure):

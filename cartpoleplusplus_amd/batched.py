@@ -228,7 +228,7 @@ class BatchedCartpole:
         st, rs = C.c_int(), C.c_int()
         native.check(self.h, self.lib.cp_get_kernel_shape(self.h, C.byref(st), C.byref(rs)), "cp_get_kernel_shape")
         names = {abi.CP_SHAPE_THROUGHPUT: "throughput", abi.CP_SHAPE_LATENCY: "latency", abi.CP_SHAPE_WIDE: "wide",
-                 abi.CP_SHAPE_WIDE8: "wide8"}
+                 abi.CP_SHAPE_WIDE8: "wide8", abi.CP_SHAPE_WIDE64: "wide64"}
         return names[st.value], names[rs.value]
 
     def enable_readback(self, on=True, reference_bug=True):

@@ -899,7 +899,7 @@ void launch_nextstep_resolve(const cp_config& cfg, const Bufs& b, const uint8_t*
 void launch_reset(int shape, const cp_config& cfg, const Bufs& b, float* obs_out, hipStream_t st) {
     const bool lat = shape != 0;
     const int wide = (kF64 || (cfg.phys.model_flags & (CP_MODEL_PERSISTENT | CP_MODEL_SLEEPING))) ? 0
-                     : shape == CP_SHAPE_WIDE ? 16 : shape == CP_SHAPE_WIDE8 ? 8 : 0;
+                     : shape == CP_SHAPE_WIDE ? 16 : shape == CP_SHAPE_WIDE8 ? 8 : shape == CP_SHAPE_WIDE64 ? 64 : 0;
     const dim3 grid(env_grid((wide ? wide : 2) * cfg.num_envs, WAVE)), block(WAVE);  // lanes per env
     if (cfg.phys.model_flags & CP_MODEL_PERSISTENT) {  // the persistent-manifold model: latency shape only
         hipLaunchKernelGGL((cp_reset_kernel<true, true>), grid, block, 0, st, cfg, b, obs_out);
@@ -913,7 +913,8 @@ void launch_reset(int shape, const cp_config& cfg, const Bufs& b, float* obs_out
         (void)lat;
         hipLaunchKernelGGL(cp_reset_kernel<true>, grid, block, 0, st, cfg, b, obs_out);
     } else {
-        if (wide == 16) hipLaunchKernelGGL((cp_reset_kernel<true, false, false, 16>), grid, block, 0, st, cfg, b, obs_out);
+        if (wide == 64) hipLaunchKernelGGL((cp_reset_kernel<true, false, false, 64>), grid, block, 0, st, cfg, b, obs_out);
+        else if (wide == 16) hipLaunchKernelGGL((cp_reset_kernel<true, false, false, 16>), grid, block, 0, st, cfg, b, obs_out);
         else if (wide == 8) hipLaunchKernelGGL((cp_reset_kernel<true, false, false, 8>), grid, block, 0, st, cfg, b, obs_out);
         else if (lat) hipLaunchKernelGGL(cp_reset_kernel<true>, grid, block, 0, st, cfg, b, obs_out);
         else hipLaunchKernelGGL(cp_reset_kernel<false>, grid, block, 0, st, cfg, b, obs_out);
@@ -926,7 +927,7 @@ static void launch_step_t(int shape, const cp_config& cfg, const Bufs& b, const 
                           const Lqr& lq, hipStream_t st) {
     const bool lat = shape != 0;
     const int wide = (kF64 || (cfg.phys.model_flags & (CP_MODEL_PERSISTENT | CP_MODEL_SLEEPING))) ? 0
-                     : shape == CP_SHAPE_WIDE ? 16 : shape == CP_SHAPE_WIDE8 ? 8 : 0;
+                     : shape == CP_SHAPE_WIDE ? 16 : shape == CP_SHAPE_WIDE8 ? 8 : shape == CP_SHAPE_WIDE64 ? 16 : 0;  // (64 lanes: reset lists only)
     const dim3 grid(env_grid((wide ? wide : 2) * cfg.num_envs, WAVE)), block(WAVE);  // lanes per env
     if (cfg.phys.model_flags & CP_MODEL_PERSISTENT) {  // the persistent-manifold model: latency shape only
         hipLaunchKernelGGL((cp_step_kernel<K, Q, true, true>), grid, block, 0, st, cfg, b, actions, obs_out,

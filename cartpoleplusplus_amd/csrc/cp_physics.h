@@ -2184,19 +2184,20 @@ CP_DEV uint32_t wide_rows(const WPair& W, int myb, int myfb, int mym, int myfm, 
     }
     return nid;
 }
-// the lane pair (of the env's LW / 2) that owns local pair j: LW 16 -> pair j on lane pair j; LW 8 -> pairs 0-2
-// on lane pairs 0-2, both cross pairs (3, 4: mostly separated by the broadphase) on lane pair 3
+// the lane pair (of the env's LW / 2) that owns local pair j: LW >= 16 -> pair j on lane pair j (the lane pairs
+// past 4 only replicate); LW 8 -> pairs 0-2 on lane pairs 0-2, both cross pairs (3, 4: mostly separated by the
+// broadphase) on lane pair 3
 template <int LW>
-CP_DEV constexpr int wide_owner(int j) { return LW == 16 ? j : (j < 3 ? j : 3); }
+CP_DEV constexpr int wide_owner(int j) { return LW >= 16 ? j : (j < 3 ? j : 3); }
 // the narrowphase + row setup of the substep on the WIDE layout: the same contacts, rows, slots, caps,
 // warm-start reads and writes as substep_prep's pair loop over the lane's 5 pairs (bit for bit)
 template <int LW, bool ALLIN, bool ES>
 CP_DEV void narrow_wide(Own& O, const cp_physics& P, const Lane& L, real* pool, int& overflow, const Mem& G,
                         Stamps& ST, bool live, Step& T, int& used, int& fused) {
-    static_assert(LW == 8 || LW == 16, "WIDE: 8 or 16 lanes per env");
+    static_assert(LW == 8 || LW == 16 || LW == 64, "WIDE: 8, 16 or 64 lanes per env");
     const int pj = L.pj;
     // the lane's pairs: j0 (LW 16: pj < 5; LW 8: pj < 4), and on LW 8's lane pair 3 also pair 4
-    const bool has0 = LW == 16 ? pj < CP_ISLAND_PAIRS : pj < 4;
+    const bool has0 = LW >= 16 ? pj < CP_ISLAND_PAIRS : pj < 4;
     const bool has1 = LW == 8 && pj == 3;
     const int j0 = has0 ? pj : 0;
     // the partner island's bodies: the partner lane is the same pair's lane of the other island (a replica)

@@ -322,6 +322,8 @@ int64_t cp_state_bytes(const cp_handle* h);   /* CP_STATE_FIELDS * B * sizeof(re
 #define CP_SHAPE_LATENCY    1
 #define CP_SHAPE_WIDE       2
 #define CP_SHAPE_WIDE8      3   /* the WIDE layout on 8 lanes per env (both cross pairs on one lane pair) */
+#define CP_SHAPE_WIDE64     4   /* the reset kernel on 64 lanes per env: one env per wave (reset lists;
+                                   rejected as a step shape) */
 int cp_set_kernel_shape(cp_handle* h, int step_shape, int reset_shape);
 int cp_get_kernel_shape(const cp_handle* h, int* step_shape, int* reset_shape);   /* the shapes in use */
 

@@ -25,8 +25,8 @@ pytestmark = pytest.mark.gpu
 # layout of the latency budget (16 lanes per env, round 6) as step kernel, reset kernel and both
 SHAPES = [("throughput", "throughput"), ("latency", "latency"), ("throughput", "latency"),
           ("latency", "throughput"), ("wide", "wide"), ("throughput", "wide"), ("wide", "latency"),
-          ("wide8", "wide8")]
-SHAPE_IDS = ["tp-tp", "lat-lat", "tp-lat", "lat-tp", "wide-wide", "tp-wide", "wide-lat", "wide8-wide8"]
+          ("wide8", "wide8"), ("wide", "wide64")]
+SHAPE_IDS = ["tp-tp", "lat-lat", "tp-lat", "lat-tp", "wide-wide", "tp-wide", "wide-lat", "wide8-wide8", "wide-wide64"]
 shapes = pytest.mark.parametrize("shape", SHAPES, ids=SHAPE_IDS)
 
 
@@ -190,7 +190,8 @@ def test_state_roundtrip_into_oracle(oracle_mod, shape):
         gpu.step(torch.from_numpy(rng.uniform(-1, 1, (B, 2, 2)).astype(np.float32)).cuda())
     orc.set_state(_np(gpu.get_state()))
     gpu2 = BatchedCartpole(B, 0, config=abi.cp_config.from_buffer_copy(gpu.cfg))
-    gpu2.set_kernel_shape(*shape[::-1])   # the copy runs the other shapes
+    other = shape[::-1] if shape[1] != "wide64" else ("latency", "wide")   # (WIDE64 is a reset layout only)
+    gpu2.set_kernel_shape(*other)   # the copy runs the other shapes
     gpu2.set_state(gpu.get_state())
     for t in range(10):
         a = rng.uniform(-1, 1, (B, 2, 2)).astype(np.float32)
@@ -440,19 +441,20 @@ def test_cart_friction_config(oracle_mod, shape):
 
 def test_auto_shapes_by_batch_size():
     """CP_SHAPE_AUTO: the widest latency layout whose waves fit the chip once (16
-    lanes per env up to 4,096 envs, 8 up to 8,192, two up to 32,768), the throughput shape above; the
-    reset list of bounds-terminated episodes on 16 lanes; fp64 and the model switches on the two-lane
-    latency layout."""
+    lanes per env up to 4,096 envs, 8 up to 8,192, two up to 32,768; the reset kernel one env per wave up
+    to 1,024 envs), the throughput shape above; the reset list of bounds-terminated episodes one env per
+    wave; fp64 and the model switches on the two-lane latency layout."""
     def shapes(B, **kw):
         env = BatchedCartpole(B, 0, **kw)
         s = env.kernel_shape()
         env.close()
         return s
-    assert shapes(1) == ("wide", "wide")
+    assert shapes(1) == ("wide", "wide64")
+    assert shapes(1024, autoreset=True) == ("wide", "wide64")
     assert shapes(4096, autoreset=True) == ("wide", "wide")
     assert shapes(8192, autoreset=True) == ("wide8", "wide8")
     assert shapes(16384, autoreset=True) == ("latency", "latency")
     assert shapes(65536, autoreset=True) == ("throughput", "throughput")
-    assert shapes(65536, autoreset=True, done_on_bounds=True) == ("throughput", "wide")
+    assert shapes(65536, autoreset=True, done_on_bounds=True) == ("throughput", "wide64")
     assert shapes(64, precision="f64") == ("latency", "latency")
     assert shapes(64, model_flags=abi.CP_MODEL_SLEEPING) == ("latency", "latency")
