@@ -192,8 +192,9 @@ static void choose_reset_shape(cp_handle* h);
 // CP_SHAPE_AUTO picks, for the latency-shaped kernels, the widest layout whose waves still fit the chip once
 // (1,024 SIMDs x 64 lanes): for the step kernel 16 lanes per env up to 4,096 envs (C2), 8 up to 8,192, else
 // the two-lane layout; for the reset kernel also one env per wave (64 lanes) up to 1,024 envs, and always for
-// the reset lists of desynchronised episodes (bounds / LQR termination: tens to hundreds of envs per list).
-// Measured in profiles/rd7d_wide, rd7e_wide, rd7m_reset.
+// the reset lists of desynchronised episodes (bounds / LQR termination: tens to hundreds of envs per list),
+// except under NEXT_STEP autoreset.  Measured in profiles/rd7d_wide, rd7e_wide, rd7m_reset, rd7z_bench
+// (DESIGN.md §5, round 6).
 static int wide_shape_for(int envs) {
     return envs <= 4096 ? CP_SHAPE_WIDE : (envs <= 8192 ? CP_SHAPE_WIDE8 : CP_SHAPE_LATENCY);
 }
@@ -559,7 +560,9 @@ static void choose_reset_shape(cp_handle* h) {
     // the WIDE layout (16 lanes per env) where its extra waves still leave SIMDs idle
     const bool wide_ok = !h->f64 && !(h->cfg.phys.model_flags & (CP_MODEL_PERSISTENT | CP_MODEL_SLEEPING));
     if (wide_ok && h->step_lat) h->step_lat = wide_shape_for(h->cfg.num_envs);
-    if (wide_ok && h->reset_lat)
+    // (NEXT_STEP: the reset runs beside the next call's step kernel, and a wide reset's extra waves take SIMDs
+    // from it: C3 + bounds NEXT_STEP 21.0 M with the two-lane reset, 17.3 M with one env per wave)
+    if (wide_ok && h->reset_lat && h->cfg.autoreset != CP_AUTORESET_NEXT_STEP)
         h->reset_lat = (h->cfg.done_on_bounds || lqr_done) ? CP_SHAPE_WIDE64 : wide_reset_shape_for(h->cfg.num_envs);
     if (h->reset_req != CP_SHAPE_AUTO) h->reset_lat = h->reset_req;
     if (h->step_req != CP_SHAPE_AUTO) h->step_lat = h->step_req;

@@ -456,5 +456,7 @@ def test_auto_shapes_by_batch_size():
     assert shapes(16384, autoreset=True) == ("latency", "latency")
     assert shapes(65536, autoreset=True) == ("throughput", "throughput")
     assert shapes(65536, autoreset=True, done_on_bounds=True) == ("throughput", "wide64")
+    # NEXT_STEP: the reset overlaps the next step kernel, the two-lane reset leaves it the SIMDs
+    assert shapes(65536, autoreset="next_step", done_on_bounds=True) == ("throughput", "latency")
     assert shapes(64, precision="f64") == ("latency", "latency")
     assert shapes(64, model_flags=abi.CP_MODEL_SLEEPING) == ("latency", "latency")
