@@ -18,4 +18,4 @@ for k,(a,t) in enumerate(ins):
     if j is None or not (minlen<=k-j+1<=maxlen): continue
     body=[x for _,x in ins[j:k+1]]
     c=lambda p: sum(1 for x in body if x.startswith(p))
-    print(f"{j:6d}-{k:6d} n={len(body):4d} v={c('v_'):4d} ds={c('ds_'):3d} scr={c('scratch_')+c('buffer_'):3d} acc={c('v_accvgpr'):3d} nop={c('s_nop'):3d} dpp={sum(1 for x in body if 'quad_perm' in x or 'row_' in x):3d} cnd={c('v_cndmask'):3d}")
+    print(f"{j:6d}-{k:6d} n={len(body):4d} v={c('v_'):4d} ds={c('ds_'):3d} scr={c('scratch_')+c('buffer_'):3d} acc={c('v_accvgpr'):3d} nop={c('s_nop'):3d} dpp={sum(1 for x in body if 'quad_perm' in x or 'row_' in x):3d} cnd={c('v_cndmask'):3d} rl={c('v_readlane'):3d}")
