@@ -2679,15 +2679,17 @@ CP_DEV void substep_finish(Own& O, const cp_physics& P, const Lane& L, const Ctx
 #endif
 }
 
-// The WIDE kernels' physics parameters through an opaque zero offset (an SGPR), once for the substep's
-// narrowphase and once for its finish: the kernel-argument loads are then made where each phase needs them
-// instead of hoisted out of the substep loop, whose uniform values (the per-body tables the WIDE narrowphase
-// selects from) otherwise stay live through the sweep loops, spilled to VGPR lanes and reloaded in the sweep
-// loop's header every sweep (the WIDE64 reset kernel's settle sweep: 16 v_readlane of ~240 instructions).
-// The two-lane kernels keep the hoisted loads: their register allocation spills more with the fresh ones.
-template <int WIDE>
+// The physics parameters through an opaque zero offset (an SGPR), once for the substep's narrowphase and once
+// for its finish: the kernel-argument loads are then made where each phase needs them instead of hoisted out
+// of the substep loop, whose uniform values (the per-body tables the WIDE narrowphase selects from) otherwise
+// stay live through the sweep loops, spilled to VGPR lanes and reloaded in the sweep loop's header every sweep
+// (the WIDE64 reset kernel's settle sweep: 16 v_readlane of ~240 instructions).  Used by the WIDE kernels and
+// the fp64 reset kernel (its frame 280 -> 0 B per lane, reset 13.6 -> 13.1 ms); the fp32 two-lane kernels and
+// the fp64 step kernel keep the hoisted loads (their register allocation spills more, or runs slower, with
+// the fresh ones).
+template <bool FRESH>
 CP_DEV const cp_physics& fresh_phys(const cp_physics& P) {
-    if constexpr (WIDE == 0) return P;
+    if constexpr (!FRESH) return P;
     uint32_t z = 0;
     asm volatile("" : "+s"(z));
     return *reinterpret_cast<const cp_physics*>(reinterpret_cast<const char*>(&P) + z);
@@ -2702,7 +2704,8 @@ CP_DEV const cp_physics& fresh_phys(const cp_physics& P) {
 template <bool FAST = false, bool C44 = false, bool ALLIN = C44, bool PM = false, bool SLP = false, int WIDE = 0>
 CP_DEV void substep(Own& O, const cp_physics& P0, const Lane& L, real* pool, real* pool0, int& overflow,
                     const Mem& G, Stamps& ST, bool live = true) {
-    const cp_physics& P = fresh_phys<WIDE>(P0);
+    constexpr bool kFresh = WIDE != 0 || (sizeof(real) == 8 && C44);
+    const cp_physics& P = fresh_phys<kFresh>(P0);
     Ctx c;
     Sim X;  // scratch: the whole-env view of a merged env's cross rows (cross_view)
     c.slp = 0u;
@@ -2712,7 +2715,7 @@ CP_DEV void substep(Own& O, const cp_physics& P0, const Lane& L, real* pool, rea
     solve_range<FAST, C44, PM>(c, X, P, pool, pool0, L.isl != 0, 0, P.solver_iterations, ST);
     CP_STAMP(t3);
     CP_ACC(solve, t2, t3);
-    substep_finish<PM, SLP, WIDE>(O, fresh_phys<WIDE>(P0), L, c, pool, G, ST, live);
+    substep_finish<PM, SLP, WIDE>(O, fresh_phys<kFresh>(P0), L, c, pool, G, ST, live);
 }
 
 // LINK_FRAME force at the COM on the lane's own cart (cart on island 0's lane, cart2 on island 1's):
