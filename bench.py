@@ -857,7 +857,7 @@ def main():
                          "GPU; each env computes what it computes in one handle)")
     ap.add_argument("--shape", choices=("auto", "throughput", "latency", "wide", "wide8"), default="auto",
                     help="kernel shapes (cp_set_kernel_shape) of the step and autoreset kernels")
-    ap.add_argument("--reset-shape", choices=("auto", "throughput", "latency", "wide", "wide8", "wide64"), default=None,
+    ap.add_argument("--reset-shape", choices=("auto", "throughput", "latency", "wide", "wide8", "wide64", "list"), default=None,
                     help="the autoreset kernel's shape when it differs from --shape")
     ap.add_argument("--sleeping", action="store_true",
                     help="the CP_MODEL_SLEEPING model (Bullet's deactivation: resting islands sleep after 2 s; "

@@ -109,8 +109,9 @@ CP_SHAPE_LATENCY = 1
 CP_SHAPE_WIDE = 2
 CP_SHAPE_WIDE8 = 3
 CP_SHAPE_WIDE64 = 4
+CP_SHAPE_LIST = 5   # reset lists: the layout picked on the device by the list's length (include/cartpole_amd.h)
 SHAPES = {"auto": CP_SHAPE_AUTO, "throughput": CP_SHAPE_THROUGHPUT, "latency": CP_SHAPE_LATENCY, "wide": CP_SHAPE_WIDE,
-          "wide8": CP_SHAPE_WIDE8, "wide64": CP_SHAPE_WIDE64}
+          "wide8": CP_SHAPE_WIDE8, "wide64": CP_SHAPE_WIDE64, "list": CP_SHAPE_LIST}
 
 
 class cp_config(C.Structure):

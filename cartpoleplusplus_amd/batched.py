@@ -218,17 +218,16 @@ class BatchedCartpole:
         return obs[:K], rew[:K], done[:K], (term_obs[:K] if want_term else None)
 
     def set_kernel_shape(self, step="auto", reset="auto"):
-        """Override the step / autoreset kernel shapes ("auto", "throughput", "latency" or "wide";
-        cp_set_kernel_shape).  Every shape computes the same numbers."""
+        """Override the step / autoreset kernel shapes ("auto", "throughput", "latency", "wide", "wide8"; the reset
+        kernel also "wide64" and "list"; cp_set_kernel_shape).  Every shape computes the same numbers."""
         native.check(self.h, self.lib.cp_set_kernel_shape(self.h, abi.SHAPES[step], abi.SHAPES[reset]),
                      "cp_set_kernel_shape")
 
     def kernel_shape(self):
-        """-> (step shape, reset shape) in use: "throughput" or "latency"."""
+        """-> (step shape, reset shape) in use, by the names of abi.SHAPES."""
         st, rs = C.c_int(), C.c_int()
         native.check(self.h, self.lib.cp_get_kernel_shape(self.h, C.byref(st), C.byref(rs)), "cp_get_kernel_shape")
-        names = {abi.CP_SHAPE_THROUGHPUT: "throughput", abi.CP_SHAPE_LATENCY: "latency", abi.CP_SHAPE_WIDE: "wide",
-                 abi.CP_SHAPE_WIDE8: "wide8", abi.CP_SHAPE_WIDE64: "wide64"}
+        names = {v: k for k, v in abi.SHAPES.items()}
         return names[st.value], names[rs.value]
 
     def enable_readback(self, on=True, reference_bug=True):

@@ -150,6 +150,8 @@ struct Bufs {
     int32_t npar;      // CP_AUTORESET_NEXT_STEP: the reset list this call appends to (0 / 1); a finishing
                        // env's done field becomes 2 + npar until the next call returns its reset obs
     int32_t keep_done; // reset kernel: leave the done field (NEXT_STEP's in-flight reset; the fixup clears it)
+    int32_t nlo, nhi;  // reset kernel: serve a list of length n only if nlo < n <= nhi (nhi 0: no upper bound;
+                       // CP_SHAPE_LIST's launches, one per layout)
 };
 
 }  // namespace cpc

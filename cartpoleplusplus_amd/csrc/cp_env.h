@@ -347,6 +347,7 @@ cp_reset_kernel(cp_config cfg, Bufs b, float* obs_out) {
     const int t = blockIdx.x * WAVE + threadIdx.x;
     if (t == 0 && b.count_next) *b.count_next = 0;  // the next cp_step's list starts empty
     const int n = *b.count;
+    if (n <= b.nlo || (b.nhi > 0 && n > b.nhi)) return;  // CP_SHAPE_LIST: another layout's range of list lengths
     if ((t / LW) >= n) return;  // envs past the compacted list
     const int isl = t & 1;
     const bool lead = (t & (LW - 1)) == 0;
@@ -912,6 +913,23 @@ void launch_reset(int shape, const cp_config& cfg, const Bufs& b, float* obs_out
     if constexpr (kF64) {
         (void)lat;
         hipLaunchKernelGGL(cp_reset_kernel<true>, grid, block, 0, st, cfg, b, obs_out);
+    } else if (shape == CP_SHAPE_LIST) {
+        // a launch per layout, each with the grid of its largest list and the range of list lengths it serves;
+        // the others' waves read the length and exit (the tiers of wide_reset_shape_for by the list's length)
+        const int B = cfg.num_envs;
+        Bufs bt = b;
+#define CP_LIST_TIER(KERN, LANES, LO, HI)                                                                \
+        if (B > (LO)) {                                                                                   \
+            bt.nlo = (LO);                                                                                \
+            bt.nhi = (HI);                                                                                \
+            const int cap = ((HI) > 0 && B > (HI)) ? (HI) : B;                                            \
+            hipLaunchKernelGGL(KERN, dim3(env_grid((LANES) * cap, WAVE)), block, 0, st, cfg, bt, obs_out); \
+        }
+        CP_LIST_TIER((cp_reset_kernel<true, false, false, 64>), 64, 0, 1024)
+        CP_LIST_TIER((cp_reset_kernel<true, false, false, 16>), 16, 1024, 4096)
+        CP_LIST_TIER(cp_reset_kernel<true>, 2, 4096, 32768)
+        CP_LIST_TIER(cp_reset_kernel<false>, 2, 32768, 0)
+#undef CP_LIST_TIER
     } else {
         if (wide == 64) hipLaunchKernelGGL((cp_reset_kernel<true, false, false, 64>), grid, block, 0, st, cfg, b, obs_out);
         else if (wide == 16) hipLaunchKernelGGL((cp_reset_kernel<true, false, false, 16>), grid, block, 0, st, cfg, b, obs_out);

@@ -191,10 +191,12 @@ struct cp_handle {
 static void choose_reset_shape(cp_handle* h);
 // CP_SHAPE_AUTO picks, for the latency-shaped kernels, the widest layout whose waves still fit the chip once
 // (1,024 SIMDs x 64 lanes): for the step kernel 16 lanes per env up to 4,096 envs (C2), 8 up to 8,192, else
-// the two-lane layout; for the reset kernel also one env per wave (64 lanes) up to 1,024 envs, and always for
-// the reset lists of desynchronised episodes (bounds / LQR termination: tens to hundreds of envs per list),
-// except under NEXT_STEP autoreset.  Measured in profiles/rd7d_wide, rd7e_wide, rd7m_reset, rd7z_bench
-// (DESIGN.md §5, round 6).
+// the two-lane layout; for the reset kernel also one env per wave (64 lanes) up to 1,024 envs.  The reset lists
+// of desynchronised episodes (bounds / LQR termination) have a length only the device knows: tens to hundreds
+// of envs per step, thousands where many episodes reach max_episode_len together, the whole batch at the first
+// cp_reset; CP_SHAPE_LIST launches one kernel per layout and the list's length picks the one that runs
+// (one env per wave for short lists).  Measured in profiles/rd7d_wide, rd7e_wide, rd7m_reset, rd7z_bench,
+// rd8f_list.
 static int wide_shape_for(int envs) {
     return envs <= 4096 ? CP_SHAPE_WIDE : (envs <= 8192 ? CP_SHAPE_WIDE8 : CP_SHAPE_LATENCY);
 }
@@ -560,10 +562,14 @@ static void choose_reset_shape(cp_handle* h) {
     // the WIDE layout (16 lanes per env) where its extra waves still leave SIMDs idle
     const bool wide_ok = !h->f64 && !(h->cfg.phys.model_flags & (CP_MODEL_PERSISTENT | CP_MODEL_SLEEPING));
     if (wide_ok && h->step_lat) h->step_lat = wide_shape_for(h->cfg.num_envs);
-    // (NEXT_STEP: the reset runs beside the next call's step kernel, and a wide reset's extra waves take SIMDs
-    // from it: C3 + bounds NEXT_STEP 21.0 M with the two-lane reset, 17.3 M with one env per wave)
-    if (wide_ok && h->reset_lat && h->cfg.autoreset != CP_AUTORESET_NEXT_STEP)
-        h->reset_lat = (h->cfg.done_on_bounds || lqr_done) ? CP_SHAPE_WIDE64 : wide_reset_shape_for(h->cfg.num_envs);
+    // Lists of desynchronised episodes: CP_SHAPE_LIST under either autoreset mode (bounds regime, steps 61-260:
+    // SAME_STEP 10.9 M with one env per wave whatever the list's length, 11.1 M two-lane, 13.2 M by the length;
+    // NEXT_STEP 17.6 / 21.5 / 24.9 M; profiles/rd8f_list).  Fixed-length episodes under NEXT_STEP keep the
+    // two-lane reset beside the next call's step kernel.
+    if (wide_ok && h->reset_lat && (h->cfg.done_on_bounds || lqr_done))
+        h->reset_lat = CP_SHAPE_LIST;
+    else if (wide_ok && h->reset_lat && h->cfg.autoreset != CP_AUTORESET_NEXT_STEP)
+        h->reset_lat = wide_reset_shape_for(h->cfg.num_envs);
     if (h->reset_req != CP_SHAPE_AUTO) h->reset_lat = h->reset_req;
     if (h->step_req != CP_SHAPE_AUTO) h->step_lat = h->step_req;
     if (h->f64) h->reset_lat = h->step_lat = 1;  // fp64: the 512-register shape only
@@ -815,16 +821,17 @@ int cp_set_kernel_shape(cp_handle* h, int step_shape, int reset_shape) {
     if (!h) return fail(h, "cp_set_kernel_shape: null handle");
     auto ok = [](int v) {
         return v == CP_SHAPE_AUTO || v == CP_SHAPE_THROUGHPUT || v == CP_SHAPE_LATENCY || v == CP_SHAPE_WIDE ||
-               v == CP_SHAPE_WIDE8 || v == CP_SHAPE_WIDE64;
+               v == CP_SHAPE_WIDE8 || v == CP_SHAPE_WIDE64 || v == CP_SHAPE_LIST;
     };
     if (!ok(step_shape) || !ok(reset_shape))
         return fail(h, "cp_set_kernel_shape: shapes must be CP_SHAPE_AUTO, CP_SHAPE_THROUGHPUT, CP_SHAPE_LATENCY, "
-                       "CP_SHAPE_WIDE, CP_SHAPE_WIDE8 or CP_SHAPE_WIDE64");
+                       "CP_SHAPE_WIDE, CP_SHAPE_WIDE8, CP_SHAPE_WIDE64 or CP_SHAPE_LIST");
     auto fixed = [](int v) {
-        return v == CP_SHAPE_THROUGHPUT || v == CP_SHAPE_WIDE || v == CP_SHAPE_WIDE8 || v == CP_SHAPE_WIDE64;
+        return v == CP_SHAPE_THROUGHPUT || v == CP_SHAPE_WIDE || v == CP_SHAPE_WIDE8 || v == CP_SHAPE_WIDE64 ||
+               v == CP_SHAPE_LIST;
     };
-    if (step_shape == CP_SHAPE_WIDE64)
-        return fail(h, "cp_set_kernel_shape: CP_SHAPE_WIDE64 is a reset-kernel layout (one env per wave)");
+    if (step_shape == CP_SHAPE_WIDE64 || step_shape == CP_SHAPE_LIST)
+        return fail(h, "cp_set_kernel_shape: CP_SHAPE_WIDE64 and CP_SHAPE_LIST are reset-kernel layouts");
     if ((h->f64 || (h->cfg.phys.model_flags & (CP_MODEL_PERSISTENT | CP_MODEL_SLEEPING))) &&
         (fixed(step_shape) || fixed(reset_shape)))
         return fail(h, "cp_set_kernel_shape: fp64, persistent-manifold and sleeping-model handles have the latency "

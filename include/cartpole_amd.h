@@ -324,6 +324,11 @@ int64_t cp_state_bytes(const cp_handle* h);   /* CP_STATE_FIELDS * B * sizeof(re
 #define CP_SHAPE_WIDE8      3   /* the WIDE layout on 8 lanes per env (both cross pairs on one lane pair) */
 #define CP_SHAPE_WIDE64     4   /* the reset kernel on 64 lanes per env: one env per wave (reset lists;
                                    rejected as a step shape) */
+#define CP_SHAPE_LIST       5   /* reset lists whose length only the device knows (bounds / LQR termination):
+                                   one launch per layout, each serving one range of the list's length and
+                                   exiting at once outside it -- one env per wave up to 1,024 envs, 16 lanes
+                                   up to 4,096, the two-lane latency layout up to 32,768, THROUGHPUT above
+                                   (rejected as a step shape) */
 int cp_set_kernel_shape(cp_handle* h, int step_shape, int reset_shape);
 int cp_get_kernel_shape(const cp_handle* h, int* step_shape, int* reset_shape);   /* the shapes in use */
 

@@ -25,8 +25,9 @@ pytestmark = pytest.mark.gpu
 # layout of the latency budget (16 lanes per env, round 6) as step kernel, reset kernel and both
 SHAPES = [("throughput", "throughput"), ("latency", "latency"), ("throughput", "latency"),
           ("latency", "throughput"), ("wide", "wide"), ("throughput", "wide"), ("wide", "latency"),
-          ("wide8", "wide8"), ("wide", "wide64")]
-SHAPE_IDS = ["tp-tp", "lat-lat", "tp-lat", "lat-tp", "wide-wide", "tp-wide", "wide-lat", "wide8-wide8", "wide-wide64"]
+          ("wide8", "wide8"), ("wide", "wide64"), ("throughput", "list")]
+SHAPE_IDS = ["tp-tp", "lat-lat", "tp-lat", "lat-tp", "wide-wide", "tp-wide", "wide-lat", "wide8-wide8", "wide-wide64",
+             "tp-list"]
 shapes = pytest.mark.parametrize("shape", SHAPES, ids=SHAPE_IDS)
 
 
@@ -190,7 +191,7 @@ def test_state_roundtrip_into_oracle(oracle_mod, shape):
         gpu.step(torch.from_numpy(rng.uniform(-1, 1, (B, 2, 2)).astype(np.float32)).cuda())
     orc.set_state(_np(gpu.get_state()))
     gpu2 = BatchedCartpole(B, 0, config=abi.cp_config.from_buffer_copy(gpu.cfg))
-    other = shape[::-1] if shape[1] != "wide64" else ("latency", "wide")   # (WIDE64 is a reset layout only)
+    other = shape[::-1] if shape[1] not in ("wide64", "list") else ("latency", "wide")   # (reset layouts only)
     gpu2.set_kernel_shape(*other)   # the copy runs the other shapes
     gpu2.set_state(gpu.get_state())
     for t in range(10):
@@ -443,7 +444,8 @@ def test_auto_shapes_by_batch_size():
     """CP_SHAPE_AUTO: the widest latency layout whose waves fit the chip once (16
     lanes per env up to 4,096 envs, 8 up to 8,192, two up to 32,768; the reset kernel one env per wave up
     to 1,024 envs), the throughput shape above; the reset list of bounds-terminated episodes one env per
-    wave; fp64 and the model switches on the two-lane latency layout."""
+    wave up to 1,024 envs by the list's own length (CP_SHAPE_LIST); fp64 and the model switches on the two-lane
+    latency layout."""
     def shapes(B, **kw):
         env = BatchedCartpole(B, 0, **kw)
         s = env.kernel_shape()
@@ -455,8 +457,39 @@ def test_auto_shapes_by_batch_size():
     assert shapes(8192, autoreset=True) == ("wide8", "wide8")
     assert shapes(16384, autoreset=True) == ("latency", "latency")
     assert shapes(65536, autoreset=True) == ("throughput", "throughput")
-    assert shapes(65536, autoreset=True, done_on_bounds=True) == ("throughput", "wide64")
-    # NEXT_STEP: the reset overlaps the next step kernel, the two-lane reset leaves it the SIMDs
-    assert shapes(65536, autoreset="next_step", done_on_bounds=True) == ("throughput", "latency")
+    assert shapes(65536, autoreset=True, done_on_bounds=True) == ("throughput", "list")
+    # NEXT_STEP: the same by the list's length; fixed-length episodes keep the two-lane reset beside the step
+    assert shapes(65536, autoreset="next_step", done_on_bounds=True) == ("throughput", "list")
+    assert shapes(4096, autoreset="next_step") == ("wide", "latency")
     assert shapes(64, precision="f64") == ("latency", "latency")
     assert shapes(64, model_flags=abi.CP_MODEL_SLEEPING) == ("latency", "latency")
+
+
+@pytest.mark.parametrize("B", [8192, 33000])
+def test_reset_list_tiers_by_length(oracle_mod, B):
+    """CP_SHAPE_LIST (the reset shape of bounds-terminated handles): one launch per layout, and the list's
+    length picks the one that runs -- one env per wave up to 1,024 envs, 16 lanes up to 4,096, the two-lane
+    latency layout up to 32,768, the throughput shape above.  Masked resets on both sides of every tier
+    boundary on one handle, then lists made by the step kernel itself, bit-exact against the oracle (obs and
+    the whole state SoA).  33,000 envs: the full reset is the throughput tier's (the oracle resets serially)."""
+    gpu, orc = _pair(oracle_mod, ("throughput", "list"), num_envs=B, action_repeats=3, initial_force=55.0,
+                     seed=99, done_on_bounds=1, autoreset=1)
+    _assert_same(_np(gpu.reset()), orc.reset(), "full reset")   # B envs: the latency or throughput tier
+    _compare_state(gpu, orc, "full reset")
+    rng = np.random.default_rng(B)
+    for n in ((1, 1024, 1025, 4096, 4097, B) if B <= 32768 else ()):
+        mask = np.zeros(B, np.uint8)
+        mask[rng.choice(B, n, replace=False)] = 1
+        gpu.reset(torch.from_numpy(mask).cuda())
+        orc_obs = _np(gpu.obs).copy()   # unmasked rows are left untouched by both
+        orc.reset(mask, obs=orc_obs)
+        _assert_same(_np(gpu.obs), orc_obs, f"reset of {n} envs obs")
+        _compare_state(gpu, orc, f"reset of {n} envs")
+    T = 30 if B <= 32768 else 4
+    a = rng.integers(0, 5, (T, B, 2)).astype(np.int8)
+    for t in range(T):   # lists made by the step kernel (bounds termination), through the same launches
+        go, gr, gd = gpu.step(torch.from_numpy(a[t]).cuda())
+        oo, orw, od = orc.step(a[t])
+        _assert_same(_np(go), oo, f"obs step {t}")
+        _assert_same(_np(gd), od, f"done step {t}")
+    _compare_state(gpu, orc, f"after {T} steps")
